@@ -1,0 +1,494 @@
+"""Round engines: one federated client's local train -> local eval -> FedAvg loop.
+
+Two implementations with one interface and identical semantics:
+
+* :class:`HipRoundEngine` -- the MI355X path.  Shard, flat parameters, Adam state, gradient
+  slab, round state and metric history are device-resident; each round is three fused
+  gfx950 kernels plus one RCCL all-reduce issued from C++ (``fedmi/ops/csrc``), optionally
+  replayed as a captured HIP graph.  Early stopping is evaluated on the device.
+* :class:`TorchRoundEngine` -- eager torch ops (``nn.Linear``, ``CrossEntropyLoss``,
+  ``torch.optim.Adam`` + ``StepLR``), i.e. the reference's own numerics
+  (``FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:30-120``).  Used on CPU (the
+  gloo plumbing config) and as the oracle the HIP kernels are tested against.
+
+Round semantics (reference-compat): ``local_steps`` full-batch Adam steps
+(reference: 1), StepLR stepped once per round, Adam moments never reset, local metrics of
+the post-step model on the local *training* shard, global metrics = mean over clients of
+local metrics (``metric_mode='mean'``, Q3) or pooled confusion (``'pooled'``, Q4),
+weights averaged with weights n_i / N (C:110-116), early stop with patience/atol on the
+4-metric vector (C:181-192).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field, asdict
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..models.mlp import MLPModel, flat_to_dict, param_count
+from .early_stop import EarlyStopper
+from .metrics import METRIC_NAMES, confusion_matrix, metrics_from_confusion, metric_vector
+
+
+@dataclass
+class EngineConfig:
+    hidden: Sequence[int] = (50, 200)
+    lr: float = 0.004
+    betas: Sequence[float] = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 0.0
+    step_size: int = 30
+    gamma: float = 0.5
+    local_steps: int = 1
+    prox_mu: float = 0.0
+    early_stop: bool = True
+    patience: int = 10
+    tolerance: float = 1e-4
+    rtol: float = 1e-5
+    max_rounds: int = 300
+    metric_mode: str = "mean"       # 'mean' (C:169) | 'pooled' (S:130)
+    rows_per_block: int = 32        # R rows per workgroup of the fused kernels
+    graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
+    seed: int = 0
+
+    def to_dict(self) -> dict:
+        d = asdict(self)
+        d["hidden"] = list(self.hidden)
+        d["betas"] = list(self.betas)
+        return d
+
+
+def _metric_mode_id(mode: str) -> int:
+    if mode not in ("mean", "pooled"):
+        raise ValueError(f"metric_mode must be 'mean' or 'pooled', got {mode!r}")
+    return 0 if mode == "mean" else 1
+
+
+class _History:
+    def __init__(self, max_rounds: int, world: int):
+        self.glob = np.zeros((max_rounds, 4))
+        self.rank = np.zeros((max_rounds, world, 4))
+        self.loss = np.zeros(max_rounds, dtype=np.float32)
+        self.rounds_run = 0
+        self.stop_round = -1       # round index at which training stopped early (-1: never)
+        self.stop_trigger = -1     # round whose metrics triggered the stop
+
+    def as_dict(self) -> dict:
+        n = self.rounds_run
+        return {
+            "rounds_run": n,
+            "stop_round": self.stop_round,
+            "stop_trigger": self.stop_trigger,
+            "global": self.glob[:n].copy(),
+            "per_rank": self.rank[:n].copy(),
+            "loss": self.loss[:n].copy(),
+        }
+
+    def global_metrics_dict(self) -> Dict[str, List[float]]:
+        """Same structure as the reference's returned ``global_metrics`` (C:124)."""
+        n = self.rounds_run
+        return {k: [float(x) for x in self.glob[:n, i]] for i, k in enumerate(METRIC_NAMES)}
+
+
+class RoundEngineBase:
+    def __init__(self, X: np.ndarray, y: np.ndarray, n_classes: int, cfg: EngineConfig, comm,
+                 init_flat: np.ndarray, n_total: Optional[int] = None):
+        self.cfg = cfg
+        self.comm = comm
+        self.world = comm.size if comm is not None else 1
+        self.rank = comm.rank if comm is not None else 0
+        self.n_local = int(len(X))
+        if self.n_local == 0:
+            raise ValueError("client shard is empty (reference SURVEY Q12 would deadlock)")
+        self.dims = [int(X.shape[1]), *[int(h) for h in cfg.hidden], int(n_classes)]
+        self.n_classes = int(n_classes)
+        self.P = param_count(self.dims)
+        if n_total is None:
+            n_total = self._allreduce_scalar(float(self.n_local))
+        self.n_total = int(n_total)
+        self.agg_scale = float(self.n_local) / float(self.n_total)
+        self.tail_stride = self.n_classes * self.n_classes + 1
+        self.hist = _History(cfg.max_rounds, self.world)
+        assert init_flat.shape == (self.P,)
+
+    def _allreduce_scalar(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        import torch.distributed as dist
+        dist.all_reduce(t)
+        return float(t.item())
+
+    # subclass API
+    def run(self, n_rounds: int) -> int:
+        raise NotImplementedError
+
+    def global_flat(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def local_flat(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def get_weights(self) -> Dict[str, np.ndarray]:
+        return flat_to_dict(self.local_flat(), self.dims)
+
+    def history(self) -> dict:
+        return self.hist.as_dict()
+
+
+# ---------------------------------------------------------------------------------------
+# Torch (CPU / oracle) engine
+# ---------------------------------------------------------------------------------------
+class TorchRoundEngine(RoundEngineBase):
+    def __init__(self, X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None,
+                 device="cpu", X_dtype=torch.float32):
+        super().__init__(X, y, n_classes, cfg, comm, init_flat, n_total)
+        self.device = torch.device(device)
+        self.X = torch.as_tensor(np.asarray(X), dtype=X_dtype, device=self.device)
+        self.y = torch.as_tensor(np.asarray(y), dtype=torch.long, device=self.device)
+        self.model = MLPModel(self.dims[0], self.dims[1:-1], self.dims[-1], device=self.device)
+        with torch.no_grad():
+            self.model.flat.copy_(torch.as_tensor(init_flat))
+        self.criterion = torch.nn.CrossEntropyLoss()
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=cfg.lr, betas=tuple(cfg.betas),
+                                          eps=cfg.eps, weight_decay=cfg.weight_decay)
+        self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=cfg.step_size,
+                                                         gamma=cfg.gamma)
+        self.stopper = EarlyStopper(cfg.patience, cfg.tolerance, cfg.rtol, enabled=cfg.early_stop)
+        self.global_params = self.model.flat.detach().clone()
+        self.rounds_issued = 0
+
+    def train_one_epoch(self) -> float:
+        """``local_steps`` full-batch Adam steps + one StepLR step (reference C:63-73)."""
+        self.model.train()
+        anchor = self.model.flat.detach().clone() if self.cfg.prox_mu else None
+        loss_v = 0.0
+        for _ in range(self.cfg.local_steps):
+            self.optimizer.zero_grad()
+            out = self.model(self.X)
+            loss = self.criterion(out, self.y)
+            loss.backward()
+            if anchor is not None:
+                with torch.no_grad():
+                    for (name, shape, off), p in zip(self.model.layout, self.model.parameters()):
+                        n = int(np.prod(shape))
+                        p.grad.add_(self.cfg.prox_mu * (p.detach() - anchor[off:off + n].view(shape)))
+            self.optimizer.step()
+            loss_v = float(loss.detach())
+        self.scheduler.step()
+        return loss_v
+
+    def confusion(self, X=None, y=None, flat=None) -> np.ndarray:
+        Xt = self.X if X is None else torch.as_tensor(np.asarray(X), dtype=torch.float32, device=self.device)
+        yt = self.y if y is None else torch.as_tensor(np.asarray(y), dtype=torch.long, device=self.device)
+        model = self.model
+        if flat is not None:
+            model = MLPModel(self.dims[0], self.dims[1:-1], self.dims[-1], device=self.device)
+            with torch.no_grad():
+                model.flat.copy_(torch.as_tensor(flat))
+        model.eval()
+        with torch.no_grad():
+            _, pred = torch.max(model(Xt), 1)
+        return confusion_matrix(yt.cpu().numpy(), pred.cpu().numpy(), self.n_classes)
+
+    # -- step-by-step API (reference train_one_epoch / evaluate_local / federated_averaging)
+    def step_train(self) -> None:
+        self._loss = self.train_one_epoch()
+
+    def step_eval(self) -> np.ndarray:
+        self._cm = self.confusion()
+        return self._cm
+
+    def step_aggregate(self) -> None:
+        r = self.rounds_issued
+        # one SUM all-reduce of [w * n_i/N | per-rank (confusion, loss) tails]
+        buf = torch.zeros(self.P + self.world * self.tail_stride, dtype=torch.float32)
+        buf[:self.P] = self.model.flat.detach().cpu() * self.agg_scale
+        t0 = self.P + self.rank * self.tail_stride
+        buf[t0:t0 + self.n_classes ** 2] = torch.as_tensor(self._cm.reshape(-1), dtype=torch.float32)
+        buf[t0 + self.n_classes ** 2] = self._loss
+        if self.comm is not None:
+            self.comm.allreduce_(buf)
+        with torch.no_grad():
+            self.model.flat.copy_(buf[:self.P].to(self.device))
+        self.global_params = self.model.flat.detach().clone()
+        self._finalize(r, buf[self.P:].numpy())
+        self.rounds_issued += 1
+
+    def run(self, n_rounds: int) -> int:
+        ran = 0
+        for _ in range(n_rounds):
+            if self.stopper.stopped or self.rounds_issued >= self.cfg.max_rounds:
+                break
+            self.step_train()
+            self.step_eval()
+            self.step_aggregate()
+            ran += 1
+        return ran
+
+    def sync_history(self) -> None:
+        pass
+
+    @property
+    def stopped(self) -> bool:
+        return self.stopper.stopped
+
+    def _finalize(self, r: int, tail: np.ndarray) -> None:
+        tails = tail.reshape(self.world, self.tail_stride)
+        C = self.n_classes
+        per = [metrics_from_confusion(t[:C * C].reshape(C, C)) for t in tails]
+        if self.cfg.metric_mode == "mean":
+            g = metric_vector({k: float(np.mean([m[k] for m in per])) for k in METRIC_NAMES})
+        else:
+            g = metric_vector(metrics_from_confusion(tails[:, :C * C].sum(0).reshape(C, C)))
+        self.hist.glob[r] = g
+        self.hist.rank[r] = np.stack([metric_vector(m) for m in per])
+        self.hist.loss[r] = float(tails[:, C * C].mean())
+        self.hist.rounds_run = r + 1
+        if self.stopper.update(g):
+            self.hist.stop_trigger = r
+            self.hist.stop_round = r + 1
+
+    def global_flat(self) -> np.ndarray:
+        return self.global_params.cpu().numpy().copy()
+
+    def local_flat(self) -> np.ndarray:
+        return self.model.flat.detach().cpu().numpy().copy()
+
+    def set_global_flat(self, flat: np.ndarray) -> None:
+        with torch.no_grad():
+            self.model.flat.copy_(torch.as_tensor(flat))
+        self.global_params = self.model.flat.detach().clone()
+
+    def state_dict(self) -> dict:
+        return {"params": self.global_flat(), "optimizer": self.optimizer.state_dict(),
+                "scheduler": self.scheduler.state_dict(), "stopper": self.stopper.state_dict(),
+                "rounds": self.rounds_issued, "history": self.hist.as_dict()}
+
+
+# ---------------------------------------------------------------------------------------
+# HIP engine
+# ---------------------------------------------------------------------------------------
+_STATE_DTYPE = np.dtype([("next_round", "<i4"), ("finalized", "<i4"), ("stopped", "<i4"), ("live", "<i4"),
+                         ("cur_round", "<i4"), ("count", "<i4"), ("has_prev", "<i4"), ("stop_round", "<i4"),
+                         ("prev", "<f8", (4,))])
+
+
+class HipRoundEngine(RoundEngineBase):
+    """Device-resident client.  ``X``/``y`` may be numpy arrays (uploaded once) or CUDA
+    tensors already on the device (e.g. from the synthetic generator)."""
+
+    def __init__(self, X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None, device=None):
+        from ..ops import native
+        self.m = native()
+        if device is None:
+            device = comm.device if comm is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if isinstance(X, torch.Tensor):
+            Xn_len = X.shape[0]
+            Xshape1 = X.shape[1]
+        else:
+            Xn_len, Xshape1 = X.shape
+        super().__init__(_ShapeOnly(Xn_len, Xshape1), y, n_classes, cfg, comm, init_flat, n_total)
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.X = (X if isinstance(X, torch.Tensor) else torch.as_tensor(np.ascontiguousarray(X, np.float32))).to(**f32).contiguous()
+        self.y = (y if isinstance(y, torch.Tensor) else torch.as_tensor(np.asarray(y))).to(dtype=torch.int32, device=dev).contiguous()
+        R = int(cfg.rows_per_block)
+        self.R = R
+        n_slabs = (self.n_local + R - 1) // R
+        slab_stride = ((self.P + 1) + 3) & ~3
+        comm_len = self.P + self.world * self.tail_stride
+        self.params = [torch.zeros(comm_len, **f32), torch.zeros(comm_len, **f32)]
+        self.params[0][:self.P] = torch.as_tensor(init_flat, dtype=torch.float32)
+        self.local = self.params[0][:self.P].clone()
+        self.mom = torch.zeros(self.P, **f32)
+        self.vel = torch.zeros(self.P, **f32)
+        self.slab = torch.zeros(n_slabs * slab_stride, **f32)
+        sb = self.m.STATE_BYTES
+        assert sb == _STATE_DTYPE.itemsize, (sb, _STATE_DTYPE.itemsize)
+        init = np.zeros(1, dtype=_STATE_DTYPE)
+        init["count"] = cfg.patience
+        init["stop_round"] = -1
+        st = torch.as_tensor(init.view(np.uint8).copy())
+        self.state = [st.to(dev), st.to(dev)]
+        mr = int(cfg.max_rounds)
+        self.h_global = torch.zeros(mr * 4, dtype=torch.float64, device=dev)
+        self.h_rank = torch.zeros(mr * self.world * 4, dtype=torch.float64, device=dev)
+        self.h_loss = torch.zeros(mr, dtype=torch.float32, device=dev)
+        ecfg = {
+            "R": R, "n_rows": self.n_local, "world": self.world, "rank": self.rank, "agg_scale": self.agg_scale,
+            "local_steps": int(cfg.local_steps), "lr": float(cfg.lr), "gamma": float(cfg.gamma),
+            "step_size": int(cfg.step_size), "beta1": float(cfg.betas[0]), "beta2": float(cfg.betas[1]),
+            "eps": float(cfg.eps), "weight_decay": float(cfg.weight_decay), "prox_mu": float(cfg.prox_mu),
+            "early_stop": bool(cfg.early_stop), "patience": int(cfg.patience), "atol": float(cfg.tolerance),
+            "rtol": float(cfg.rtol), "max_rounds": mr, "metric_mode": _metric_mode_id(cfg.metric_mode),
+        }
+        bufs = {
+            "X": self.X.data_ptr(), "y": self.y.data_ptr(), "slab": self.slab.data_ptr(),
+            "local": self.local.data_ptr(), "m": self.mom.data_ptr(), "v": self.vel.data_ptr(),
+            "hist_global": self.h_global.data_ptr(), "hist_rank": self.h_rank.data_ptr(),
+            "hist_loss": self.h_loss.data_ptr(), "params0": self.params[0].data_ptr(),
+            "params1": self.params[1].data_ptr(), "state0": self.state[0].data_ptr(),
+            "state1": self.state[1].data_ptr(),
+        }
+        self.engine = self.m.FLEngine(self.dims, ecfg, bufs)
+        self.layout = self.engine.layout()
+        # the engine owns a non-default stream: graph capture is illegal on the null stream
+        self.stream = torch.cuda.Stream(device=dev)
+        self.stream.wait_stream(torch.cuda.current_stream(dev))
+        self.rounds_issued = 0
+        self._stopped_seen = False
+        self._native_comm = comm.native if (comm is not None and self.world > 1) else None
+        self._graph_ready = False
+
+    # -- execution --
+    def _stream(self) -> int:
+        return self.stream.cuda_stream
+
+    def _issue(self, n: int) -> None:
+        """Issue rounds [rounds_issued, rounds_issued + n) on the current stream."""
+        s = self._stream()
+        r0 = self.rounds_issued
+        g = int(self.cfg.graph_rounds)
+        if self.world > 1 and self._native_comm is None:
+            # torch-owned communicator: all-reduce from Python between rounds
+            with torch.cuda.stream(self.stream):
+                for r in range(r0, r0 + n):
+                    self.engine.run_local(r, s)
+                    self.comm.allreduce_(self.params[(r + 1) & 1])
+            self.rounds_issued += n
+            return
+        r = r0
+        while r < r0 + n:
+            left = r0 + n - r
+            if g >= 2 and r % 2 == 0 and left >= g:
+                if not self._graph_ready:
+                    self.engine.capture(g, s, self._native_comm)
+                    self._graph_ready = True
+                self.engine.replay(s)
+                r += g
+            else:
+                self.engine.run(r, 1, s, self._native_comm)
+                r += 1
+        self.rounds_issued = r
+
+    def _read_state(self, idx: int) -> np.ndarray:
+        self.stream.synchronize()
+        return self.state[idx].cpu().numpy().view(_STATE_DTYPE)[0]
+
+    # -- step-by-step API (reference train_one_epoch / evaluate_local / federated_averaging)
+    def step_train(self) -> None:
+        self.engine.phase(self.rounds_issued, 0, self._stream(), None)
+
+    def step_eval(self) -> np.ndarray:
+        r = self.rounds_issued
+        self.engine.phase(r, 1, self._stream(), None)
+        self.stream.synchronize()
+        C = self.n_classes
+        t0 = self.P + self.rank * self.tail_stride
+        return self.params[(r + 1) & 1][t0:t0 + C * C].cpu().numpy().reshape(C, C).astype(np.int64)
+
+    def step_aggregate(self) -> None:
+        r = self.rounds_issued
+        if self.world > 1:
+            if self._native_comm is not None:
+                self.engine.phase(r, 2, self._stream(), self._native_comm)
+            else:
+                with torch.cuda.stream(self.stream):
+                    self.comm.allreduce_(self.params[(r + 1) & 1])
+        self.rounds_issued += 1
+        st = self._read_state(self.rounds_issued & 1)
+        if st["stopped"]:
+            self._stopped_seen = True
+
+    def run(self, n_rounds: int, check_every: int = 64) -> int:
+        """Run up to ``n_rounds`` rounds; returns the number of live rounds.  The stop
+        flag is polled once per ``check_every`` rounds (rounds issued past an early stop
+        are exact no-ops on the device)."""
+        before = self.hist.rounds_run
+        left = min(n_rounds, self.cfg.max_rounds - self.rounds_issued)
+        while left > 0 and not self._stopped_seen:
+            n = min(left, check_every)
+            self._issue(n)
+            left -= n
+            st = self._read_state(self.rounds_issued & 1)
+            if st["stopped"]:
+                self._stopped_seen = True
+        self.sync_history()
+        return self.hist.rounds_run - before
+
+    @property
+    def stopped(self) -> bool:
+        return self._stopped_seen
+
+    def sync_history(self) -> None:
+        r = self.rounds_issued
+        s = self._stream()
+        self.engine.finalize(r, s)
+        st = self._read_state((r + 1) & 1)   # synchronizes the engine stream
+        n = int(st["finalized"])
+        self.hist.rounds_run = n
+        if n:
+            self.hist.glob[:n] = self.h_global[:n * 4].cpu().numpy().reshape(n, 4)
+            self.hist.rank[:n] = self.h_rank[:n * self.world * 4].cpu().numpy().reshape(n, self.world, 4)
+            self.hist.loss[:n] = self.h_loss[:n].cpu().numpy()
+        if st["stopped"]:
+            self.hist.stop_round = int(st["stop_round"])
+            self.hist.stop_trigger = int(st["stop_round"]) - 1
+            self._stopped_seen = True
+
+    def global_flat(self) -> np.ndarray:
+        self.stream.synchronize()
+        return self.params[self.rounds_issued & 1][:self.P].cpu().numpy().copy()
+
+    def local_flat(self) -> np.ndarray:
+        self.stream.synchronize()
+        return self.local.cpu().numpy().copy()
+
+    def set_global_flat(self, flat: np.ndarray) -> None:
+        self.stream.synchronize()
+        self.params[self.rounds_issued & 1][:self.P].copy_(torch.as_tensor(flat, dtype=torch.float32))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def confusion(self, X=None, y=None, flat=None) -> np.ndarray:
+        Xt = self.X if X is None else torch.as_tensor(np.ascontiguousarray(X, np.float32), device=self.device)
+        yt = self.y if y is None else torch.as_tensor(np.asarray(y), dtype=torch.int32, device=self.device)
+        if flat is None:
+            p = self.local
+        else:
+            p = torch.as_tensor(flat, dtype=torch.float32, device=self.device)
+        cm = torch.zeros(self.n_classes ** 2, dtype=torch.float32, device=self.device)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.engine.confusion(Xt.data_ptr(), yt.data_ptr(), int(Xt.shape[0]), p.data_ptr(), cm.data_ptr(),
+                              self._stream())
+        self.stream.synchronize()
+        return cm.cpu().numpy().reshape(self.n_classes, self.n_classes).astype(np.int64)
+
+    def state_dict(self) -> dict:
+        self.stream.synchronize()
+        return {"params": self.global_flat(), "local": self.local_flat(), "exp_avg": self.mom.cpu().numpy(),
+                "exp_avg_sq": self.vel.cpu().numpy(), "rounds": self.rounds_issued,
+                "state": self.state[self.rounds_issued & 1].cpu().numpy(), "history": self.hist.as_dict()}
+
+
+class _ShapeOnly:
+    """Stand-in so the base class can read ``len(X)``/``X.shape`` of device tensors."""
+
+    def __init__(self, n, f):
+        self.shape = (n, f)
+
+    def __len__(self):
+        return self.shape[0]
+
+
+def make_engine(X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None, backend: str = "auto"):
+    if backend == "auto":
+        backend = "hip" if (comm is not None and comm.device.type == "cuda") or \
+            (comm is None and torch.cuda.is_available()) else "torch"
+    if backend == "hip":
+        return HipRoundEngine(X, y, n_classes, cfg, comm, init_flat, n_total)
+    if backend == "torch":
+        return TorchRoundEngine(X, y, n_classes, cfg, comm, init_flat, n_total)
+    raise ValueError(f"unknown engine backend {backend!r}")

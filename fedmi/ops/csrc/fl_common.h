@@ -1,0 +1,108 @@
+// Shared host/device declarations of the fused federated-round engine.
+//
+// One client per GPU keeps everything resident: the local shard, a flat fp32 parameter
+// buffer in the reference's named_parameters() order (model.0.weight, model.0.bias,
+// model.2.weight, ...; FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:93-99),
+// the Adam moments (which persist across rounds), a per-block gradient slab,
+// and a small device-side round state that carries the early-stopping rule (C:181-192)
+// so the host never has to read metrics back to decide whether to continue.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FL_MAX_LAYERS 4
+#define FL_MAX_CLASSES 16
+#define FL_MAX_WORLD 64
+
+struct MLPDesc {
+    int L;                            // number of Linear layers
+    int dim[FL_MAX_LAYERS + 1];       // dim[0] = features, dim[L] = classes
+    int ld[FL_MAX_LAYERS + 1];        // LDS leading dimension (floats) per activation buffer
+    int act_off[FL_MAX_LAYERS + 1];   // LDS float offset of each activation buffer (R rows)
+    int w_off[FL_MAX_LAYERS];         // float offset of W_l [dim[l+1], dim[l]] in the flat buffer
+    int b_off[FL_MAX_LAYERS];         // float offset of b_l [dim[l+1]]
+    int P;                            // number of parameters (dense, reference order)
+    int lds_floats;                   // LDS floats needed per block
+};
+
+struct FLConfig {
+    int R;              // rows per workgroup (16, 32 or 64)
+    int n_rows;         // local training rows
+    float inv_n;        // 1 / n_rows  (CrossEntropyLoss 'mean', C:43)
+    int world;
+    int rank;
+    float agg_scale;    // n_rank / N_total (sample-size-weighted FedAvg, C:110-116)
+    int slab_stride;    // floats per slab row (P + loss slot, padded)
+    int n_slabs;        // workgroups of the train kernel = ceil(n_rows / R)
+    int tail_off;       // == P: start of the per-rank metric tail in the comm buffer
+    int tail_stride;    // C*C confusion counts + 1 loss slot
+    int tail_len;       // world * tail_stride
+    int local_steps;    // optimizer steps per round (reference: 1 full-batch step, C:63-73)
+    // optimizer (torch.optim.Adam + StepLR, C:44-46); scalars kept in double like torch
+    double lr0;
+    double gamma;
+    int step_size;
+    double beta1;
+    double beta2;
+    float omb1;         // (float)(1 - beta1)  lerp weight
+    float omb2;         // (float)(1 - beta2)  addcmul value
+    float beta2f;       // (float)beta2
+    float eps;
+    float weight_decay; // L2 on the gradient (torch Adam weight_decay / sklearn alpha)
+    float prox_mu;      // FedProx proximal coefficient (0 = FedAvg)
+    // early stopping (C:122, C:181-192)
+    int es_enabled;
+    int patience;
+    double atol;
+    double rtol;
+    int max_rounds;
+    int metric_mode;    // 0 = mean of per-client metrics (C:169), 1 = pooled confusion (S:130)
+};
+
+// Device-resident round state; double-buffered by round parity so every workgroup of the
+// train kernel can recompute the stop decision from an immutable input copy.
+struct FLState {
+    int next_round;     // index of the next round to run
+    int finalized;      // rounds whose metrics have been folded into the history
+    int stopped;        // early-stop signal (C:132-136 / C:189)
+    int live;           // this launch's round is live (not past the stop)
+    int cur_round;      // index of the round running now (valid when live)
+    int count;          // patience counter (termination_count, C:125)
+    int has_prev;
+    int stop_round;     // round index at which the stop took effect (-1 = none)
+    double prev[4];     // prev_metric (C:126)
+};
+
+struct FLBuffers {
+    const float* X;     // [n_rows, dim0] row-major, device resident
+    const int* y;       // [n_rows]
+    float* slab;        // [n_slabs, slab_stride]
+    float* local;       // [P] post-step local weights (evaluated, C:148)
+    float* m;           // [P] Adam exp_avg
+    float* v;           // [P] Adam exp_avg_sq
+    double* hist_global;  // [max_rounds, 4]
+    double* hist_rank;    // [max_rounds, world, 4]
+    float* hist_loss;     // [max_rounds] mean CE over clients
+};
+
+// Launchers (fl_kernels.hip). `pg` = params the round trains from (the previous round's
+// all-reduced comm buffer), `comm` = buffer this round publishes into (P + tail floats).
+hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
+                           const float* pg, const FLState* st_in, FLState* st_out,
+                           int local_step, hipStream_t s);
+hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
+                          const float* pin, const float* anchor, float* comm,
+                          const FLState* st, int local_step, hipStream_t s);
+hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
+                          const float* params, float* comm, const FLState* st, hipStream_t s);
+hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
+                              const float* pg, const FLState* st_in, FLState* st_out,
+                              hipStream_t s);
+// Stand-alone forward + confusion on an arbitrary row set (held-out evaluation).
+hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const int* y, int n_rows,
+                               const float* params, float* cm_out, hipStream_t s);
+// Fill a device shard with synthetic income-shaped rows (Philox4x32-10).
+hipError_t fl_launch_synth(float* X, int* y, long long n_rows, int n_features,
+                           unsigned long long seed, unsigned long long row_offset,
+                           const float* teacher_w1, const float* teacher_w2, int teacher_hidden,
+                           hipStream_t s);

@@ -1,0 +1,363 @@
+// Native runtime of the federated round engine: kernel sequencing, HIP-graph capture of
+// whole rounds, and an RCCL communicator owned by the engine (no torch / pickle in the
+// round loop).  Exposed to Python as module `fedmi.ops._fedmi_hip` (pybind11).
+//
+// The reference runs the round loop in Python with 3 gathers + 3 bcasts + (2 + 2k)
+// barriers per round (FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:130-201,
+// SURVEY §2.4).  Here `FLEngine::run` issues, per round, three kernels and one
+// ncclAllReduce on the caller's stream; `capture` records an even number of rounds into a
+// hipGraph that is replayed with one host call.  Early stopping is decided on the device,
+// so nothing in the loop waits on the host.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fl_common.h"
+
+namespace py = pybind11;
+
+#define HIP_CHECK(expr)                                                                       \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +     \
+                                     " at " #expr);                                           \
+    } while (0)
+
+#define NCCL_CHECK(expr)                                                                      \
+    do {                                                                                      \
+        ncclResult_t _r = (expr);                                                             \
+        if (_r != ncclSuccess)                                                                \
+            throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(_r) +   \
+                                     " at " #expr);                                           \
+    } while (0)
+
+hipError_t fl_set_lds_limit(size_t bytes);  // fl_kernels.hip
+
+static inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <typename T>
+static inline T* as_ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+// ---------------------------------------------------------------------------------------
+// RCCL communicator: one per process (= one per GPU / federated client).
+// ---------------------------------------------------------------------------------------
+class RcclComm {
+  public:
+    RcclComm(int nranks, int rank, py::bytes uid, int device) : nranks_(nranks), rank_(rank) {
+        std::string s = uid;
+        if (s.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad RCCL unique id size");
+        ncclUniqueId id;
+        std::memcpy(&id, s.data(), sizeof(id));
+        HIP_CHECK(hipSetDevice(device));
+        NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    }
+    ~RcclComm() { destroy(); }
+
+    static py::bytes unique_id() {
+        ncclUniqueId id;
+        NCCL_CHECK(ncclGetUniqueId(&id));
+        return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+    }
+
+    void allreduce_f32(uintptr_t buf, size_t count, uintptr_t stream) {
+        NCCL_CHECK(ncclAllReduce(as_ptr<float>(buf), as_ptr<float>(buf), count, ncclFloat32, ncclSum,
+                                 comm_, as_stream(stream)));
+    }
+    void allreduce_f64(uintptr_t buf, size_t count, uintptr_t stream) {
+        NCCL_CHECK(ncclAllReduce(as_ptr<double>(buf), as_ptr<double>(buf), count, ncclFloat64, ncclSum,
+                                 comm_, as_stream(stream)));
+    }
+    void broadcast_bytes(uintptr_t buf, size_t nbytes, int root, uintptr_t stream) {
+        NCCL_CHECK(ncclBroadcast(as_ptr<void>(buf), as_ptr<void>(buf), nbytes, ncclUint8, root, comm_,
+                                 as_stream(stream)));
+    }
+    void allgather_f32(uintptr_t send, uintptr_t recv, size_t count, uintptr_t stream) {
+        NCCL_CHECK(ncclAllGather(as_ptr<float>(send), as_ptr<float>(recv), count, ncclFloat32, comm_,
+                                 as_stream(stream)));
+    }
+    void abort() {
+        if (comm_) {
+            ncclCommAbort(comm_);
+            comm_ = nullptr;
+        }
+    }
+    void destroy() {
+        if (comm_) {
+            ncclCommDestroy(comm_);
+            comm_ = nullptr;
+        }
+    }
+    int rank() const { return rank_; }
+    int size() const { return nranks_; }
+    ncclComm_t handle() const { return comm_; }
+
+  private:
+    int nranks_, rank_;
+    ncclComm_t comm_ = nullptr;
+};
+
+// ---------------------------------------------------------------------------------------
+// Engine
+// ---------------------------------------------------------------------------------------
+static int pick_ld(int dim) {
+    int ld = (dim + 15) & ~15;
+    while (ld % 32 != 17) ++ld;
+    return ld;
+}
+
+class FLEngine {
+  public:
+    FLEngine(std::vector<int> dims, py::dict cfg, py::dict bufs) {
+        const int L = (int)dims.size() - 1;
+        if (L < 1 || L > FL_MAX_LAYERS) throw std::runtime_error("FLEngine: 1..4 Linear layers supported");
+        std::memset(&d_, 0, sizeof(d_));
+        std::memset(&c_, 0, sizeof(c_));
+        std::memset(&b_, 0, sizeof(b_));
+        d_.L = L;
+        int off = 0;
+        for (int l = 0; l <= L; ++l) d_.dim[l] = dims[l];
+        for (int l = 0; l < L; ++l) {
+            d_.w_off[l] = off;
+            off += dims[l] * dims[l + 1];
+            d_.b_off[l] = off;
+            off += dims[l + 1];
+        }
+        d_.P = off;
+        const int C = dims[L];
+        if (C > FL_MAX_CLASSES) throw std::runtime_error("FLEngine: at most 16 classes");
+        if (dims[0] > 4096) throw std::runtime_error("FLEngine: too many features");
+
+        c_.R = cfg["R"].cast<int>();
+        if (c_.R != 16 && c_.R != 32 && c_.R != 64) throw std::runtime_error("FLEngine: R must be 16, 32 or 64");
+        int lds = 0;
+        for (int l = 0; l <= L; ++l) {
+            d_.ld[l] = pick_ld(dims[l]);
+            d_.act_off[l] = lds;
+            lds += c_.R * d_.ld[l];
+            lds = (lds + 3) & ~3;
+        }
+        d_.lds_floats = lds;
+        if ((size_t)lds * 4 > 150 * 1024)
+            throw std::runtime_error("FLEngine: activations exceed LDS; use a smaller R or the layered path");
+        HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));
+
+        c_.n_rows = cfg["n_rows"].cast<int>();
+        c_.inv_n = 1.0f / (float)c_.n_rows;
+        c_.world = cfg["world"].cast<int>();
+        c_.rank = cfg["rank"].cast<int>();
+        if (c_.world > FL_MAX_WORLD) throw std::runtime_error("FLEngine: world too large");
+        c_.agg_scale = cfg["agg_scale"].cast<float>();
+        c_.slab_stride = ((d_.P + 1) + 3) & ~3;
+        c_.n_slabs = (c_.n_rows + c_.R - 1) / c_.R;
+        c_.tail_off = d_.P;
+        c_.tail_stride = C * C + 1;
+        c_.tail_len = c_.world * c_.tail_stride;
+        c_.local_steps = cfg["local_steps"].cast<int>();
+        c_.lr0 = cfg["lr"].cast<double>();
+        c_.gamma = cfg["gamma"].cast<double>();
+        c_.step_size = cfg["step_size"].cast<int>();
+        c_.beta1 = cfg["beta1"].cast<double>();
+        c_.beta2 = cfg["beta2"].cast<double>();
+        c_.omb1 = (float)(1.0 - c_.beta1);
+        c_.omb2 = (float)(1.0 - c_.beta2);
+        c_.beta2f = (float)c_.beta2;
+        c_.eps = (float)cfg["eps"].cast<double>();
+        c_.weight_decay = (float)cfg["weight_decay"].cast<double>();
+        c_.prox_mu = (float)cfg["prox_mu"].cast<double>();
+        c_.es_enabled = cfg["early_stop"].cast<bool>() ? 1 : 0;
+        c_.patience = cfg["patience"].cast<int>();
+        c_.atol = cfg["atol"].cast<double>();
+        c_.rtol = cfg["rtol"].cast<double>();
+        c_.max_rounds = cfg["max_rounds"].cast<int>();
+        c_.metric_mode = cfg["metric_mode"].cast<int>();
+
+        b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
+        b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
+        b_.slab = as_ptr<float>(bufs["slab"].cast<uintptr_t>());
+        b_.local = as_ptr<float>(bufs["local"].cast<uintptr_t>());
+        b_.m = as_ptr<float>(bufs["m"].cast<uintptr_t>());
+        b_.v = as_ptr<float>(bufs["v"].cast<uintptr_t>());
+        b_.hist_global = as_ptr<double>(bufs["hist_global"].cast<uintptr_t>());
+        b_.hist_rank = as_ptr<double>(bufs["hist_rank"].cast<uintptr_t>());
+        b_.hist_loss = as_ptr<float>(bufs["hist_loss"].cast<uintptr_t>());
+        pbuf_[0] = as_ptr<float>(bufs["params0"].cast<uintptr_t>());
+        pbuf_[1] = as_ptr<float>(bufs["params1"].cast<uintptr_t>());
+        st_[0] = as_ptr<FLState>(bufs["state0"].cast<uintptr_t>());
+        st_[1] = as_ptr<FLState>(bufs["state1"].cast<uintptr_t>());
+    }
+
+    ~FLEngine() { drop_graph(); }
+
+    // Issue rounds [r0, r0 + n): three kernels (+1 train/adam pair per extra local step)
+    // and, when a communicator is attached and world > 1, one all-reduce per round.
+    void run(int r0, int n, uintptr_t stream, RcclComm* comm) {
+        hipStream_t s = as_stream(stream);
+        for (int r = r0; r < r0 + n; ++r) issue_round(r, s, comm);
+    }
+
+    void run_local(int r, uintptr_t stream) { issue_round(r, as_stream(stream), nullptr); }
+
+    // One phase of round r: 0 = local training (all local steps), 1 = local evaluation,
+    // 2 = FedAvg all-reduce.  Used by the step-by-step reference API
+    // (train_one_epoch / evaluate_local / federated_averaging).
+    void phase(int r, int which, uintptr_t stream, RcclComm* comm) {
+        hipStream_t s = as_stream(stream);
+        if (which == 0) issue_train(r, s);
+        else if (which == 1) issue_eval(r, s);
+        else if (which == 2) issue_allreduce(r, s, comm);
+        else throw std::runtime_error("phase: 0, 1 or 2");
+    }
+
+    void finalize(int r, uintptr_t stream) {
+        HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], as_stream(stream)));
+    }
+
+    // Record `n` rounds (n even, starting at an even round) into one hipGraph.  Round
+    // indices live on the device, so the same graph is replayed for every chunk.
+    void capture(int n, uintptr_t stream, RcclComm* comm) {
+        if (n <= 0 || (n & 1)) throw std::runtime_error("capture: n must be a positive even number");
+        drop_graph();
+        hipStream_t s = as_stream(stream);
+        HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        try {
+            for (int r = 0; r < n; ++r) issue_round(r, s, comm);
+        } catch (...) {
+            hipGraph_t g;
+            hipStreamEndCapture(s, &g);
+            if (g) hipGraphDestroy(g);
+            throw;
+        }
+        HIP_CHECK(hipStreamEndCapture(s, &graph_));
+        HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+        graph_rounds_ = n;
+    }
+
+    void replay(uintptr_t stream) {
+        if (!exec_) throw std::runtime_error("replay: no captured graph");
+        HIP_CHECK(hipGraphLaunch(exec_, as_stream(stream)));
+    }
+
+    int graph_rounds() const { return graph_rounds_; }
+
+    // held-out evaluation: confusion matrix of `params` on (X, y) accumulated into cm_out
+    void confusion(uintptr_t X, uintptr_t y, int n_rows, uintptr_t params, uintptr_t cm_out, uintptr_t stream) {
+        HIP_CHECK(fl_launch_confusion(d_, c_.R, as_ptr<const float>(X), as_ptr<const int>(y), n_rows,
+                                      as_ptr<const float>(params), as_ptr<float>(cm_out), as_stream(stream)));
+    }
+
+    py::dict layout() const {
+        py::dict o;
+        std::vector<int> w, bb, ld, dims;
+        for (int l = 0; l < d_.L; ++l) { w.push_back(d_.w_off[l]); bb.push_back(d_.b_off[l]); }
+        for (int l = 0; l <= d_.L; ++l) { ld.push_back(d_.ld[l]); dims.push_back(d_.dim[l]); }
+        o["P"] = d_.P;
+        o["w_off"] = w;
+        o["b_off"] = bb;
+        o["ld"] = ld;
+        o["dims"] = dims;
+        o["lds_bytes"] = d_.lds_floats * 4;
+        o["slab_stride"] = c_.slab_stride;
+        o["n_slabs"] = c_.n_slabs;
+        o["tail_off"] = c_.tail_off;
+        o["tail_stride"] = c_.tail_stride;
+        o["tail_len"] = c_.tail_len;
+        o["comm_len"] = d_.P + c_.tail_len;
+        o["state_bytes"] = (int)sizeof(FLState);
+        return o;
+    }
+
+  private:
+    void issue_train(int r, hipStream_t s) {
+        float* pg = pbuf_[r & 1];
+        float* cb = pbuf_[(r + 1) & 1];
+        FLState* si = st_[r & 1];
+        FLState* so = st_[(r + 1) & 1];
+        for (int ls = 0; ls < c_.local_steps; ++ls) {
+            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, ls == 0 ? si : so, so, ls, s));
+            HIP_CHECK(fl_launch_adam(d_, c_, b_, ls == 0 ? pg : b_.local, pg, cb, so, ls, s));
+        }
+    }
+    void issue_eval(int r, hipStream_t s) {
+        HIP_CHECK(fl_launch_eval(d_, c_, b_, b_.local, pbuf_[(r + 1) & 1], st_[(r + 1) & 1], s));
+    }
+    void issue_allreduce(int r, hipStream_t s, RcclComm* comm) {
+        if (comm != nullptr && c_.world > 1)
+            comm->allreduce_f32((uintptr_t)pbuf_[(r + 1) & 1], (size_t)(d_.P + c_.tail_len), (uintptr_t)s);
+    }
+    void issue_round(int r, hipStream_t s, RcclComm* comm) {
+        issue_train(r, s);
+        issue_eval(r, s);
+        issue_allreduce(r, s, comm);
+    }
+
+    void drop_graph() {
+        if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
+        if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+        graph_rounds_ = 0;
+    }
+
+    MLPDesc d_;
+    FLConfig c_;
+    FLBuffers b_;
+    float* pbuf_[2];
+    FLState* st_[2];
+    hipGraph_t graph_ = nullptr;
+    hipGraphExec_t exec_ = nullptr;
+    int graph_rounds_ = 0;
+};
+
+// Thin wrappers used by tests and the synthetic-data path.
+static void synth(uintptr_t X, uintptr_t y, long long n, int F, unsigned long long seed, unsigned long long off,
+                  uintptr_t w1, uintptr_t w2, int H, uintptr_t stream) {
+    HIP_CHECK(fl_launch_synth(as_ptr<float>(X), as_ptr<int>(y), n, F, seed, off, as_ptr<const float>(w1),
+                              as_ptr<const float>(w2), H, as_stream(stream)));
+}
+
+static py::dict device_info(int dev) {
+    hipDeviceProp_t p;
+    HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    py::dict o;
+    o["name"] = std::string(p.name);
+    o["arch"] = std::string(p.gcnArchName);
+    o["cus"] = p.multiProcessorCount;
+    o["lds_per_block"] = (long long)p.sharedMemPerBlock;
+    o["hbm_bytes"] = (long long)p.totalGlobalMem;
+    return o;
+}
+
+PYBIND11_MODULE(_fedmi_hip, m) {
+    m.doc() = "fedmi native runtime: fused FL round kernels (gfx950), HIP graphs, RCCL";
+    py::class_<RcclComm>(m, "RcclComm")
+        .def(py::init<int, int, py::bytes, int>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
+             py::arg("device"))
+        .def_static("unique_id", &RcclComm::unique_id)
+        .def("allreduce_f32", &RcclComm::allreduce_f32)
+        .def("allreduce_f64", &RcclComm::allreduce_f64)
+        .def("allgather_f32", &RcclComm::allgather_f32)
+        .def("broadcast_bytes", &RcclComm::broadcast_bytes)
+        .def("abort", &RcclComm::abort)
+        .def("destroy", &RcclComm::destroy)
+        .def_property_readonly("rank", &RcclComm::rank)
+        .def_property_readonly("size", &RcclComm::size);
+    py::class_<FLEngine>(m, "FLEngine")
+        .def(py::init<std::vector<int>, py::dict, py::dict>())
+        .def("run", &FLEngine::run, py::arg("r0"), py::arg("n"), py::arg("stream"), py::arg("comm") = nullptr)
+        .def("run_local", &FLEngine::run_local)
+        .def("phase", &FLEngine::phase, py::arg("r"), py::arg("which"), py::arg("stream"), py::arg("comm") = nullptr)
+        .def("finalize", &FLEngine::finalize)
+        .def("capture", &FLEngine::capture, py::arg("n"), py::arg("stream"), py::arg("comm") = nullptr)
+        .def("replay", &FLEngine::replay)
+        .def("graph_rounds", &FLEngine::graph_rounds)
+        .def("confusion", &FLEngine::confusion)
+        .def("layout", &FLEngine::layout);
+    m.def("synth", &synth);
+    m.def("device_info", &device_info);
+    m.attr("STATE_BYTES") = (int)sizeof(FLState);
+}

@@ -1,0 +1,164 @@
+"""Process-group runtime: one process per GPU (= one federated client).
+
+The reference talks MPI through mpi4py's pickle collectives on ``MPI.COMM_WORLD``
+(``FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:212-214``; every call site in
+SURVEY §2.4).  :class:`Comm` keeps that object API -- ``Get_rank``, ``Get_size``,
+``gather``, ``bcast``, ``Barrier``, ``Abort`` -- so reference-style driver code keeps
+working, but the data plane is different:
+
+* **control plane** (rare, host objects: start-up checks, final reports): gloo via
+  ``torch.distributed``;
+* **data plane** (every round, device buffers): one in-place SUM all-reduce on a flat
+  device buffer.  Backends:
+
+  - ``rccl``  -- the engine-owned RCCL communicator in the native extension
+    (``RcclComm``: ``ncclCommInitRank`` over xGMI, unique id exchanged over the gloo
+    store).  The engine issues ``ncclAllReduce`` itself, inside captured HIP graphs.
+  - ``nccl``  -- torch's ProcessGroupNCCL (which *is* RCCL on ROCm), for callers that
+    want torch to own the communicator.
+  - ``gloo``  -- CPU tensors (BASELINE config 1: "2-client FedAvg ... CPU + gloo").
+
+Launch with ``torchrun --nproc-per-node N --master-addr 127.0.0.1 ...``; ``LOCAL_RANK``
+selects the device (fixes the reference's everyone-on-GPU-0).
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+class Comm:
+    def __init__(self, backend: str = "auto", device: Optional[str] = None, timeout_s: float = 600.0):
+        self.rank = _env_int("RANK", 0)
+        self.size = _env_int("WORLD_SIZE", 1)
+        self.local_rank = _env_int("LOCAL_RANK", self.rank)
+        if device is None or device == "auto":
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if device.startswith("cuda"):
+            idx = self.local_rank if device == "cuda" else int(device.split(":")[1])
+            torch.cuda.set_device(idx)
+            self.device = torch.device("cuda", idx)
+        else:
+            self.device = torch.device("cpu")
+        if backend == "auto":
+            backend = "rccl" if self.device.type == "cuda" else "gloo"
+        if self.device.type == "cpu" and backend != "gloo":
+            raise ValueError(f"backend {backend!r} needs a GPU device")
+        self.backend = backend
+        self.native = None       # RcclComm
+        self._nccl_group = None
+        self._initialized_here = False
+        if self.size > 1:
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", "29500")
+                from datetime import timedelta
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.size,
+                                        timeout=timedelta(seconds=timeout_s))
+                self._initialized_here = True
+            if backend == "rccl":
+                from ..ops import native
+                m = native()
+                uid = [m.RcclComm.unique_id() if self.rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                self.native = m.RcclComm(self.size, self.rank, uid[0], self.device.index)
+            elif backend == "nccl":
+                self._nccl_group = dist.new_group(backend="nccl")
+
+    # ---- mpi4py-compatible object API (reference call sites) ----
+    def Get_rank(self) -> int:
+        return self.rank
+
+    def Get_size(self) -> int:
+        return self.size
+
+    def gather(self, obj: Any, root: int = 0) -> Optional[List[Any]]:
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size if self.rank == root else None
+        dist.gather_object(obj, out, dst=root)
+        return out
+
+    def allgather(self, obj: Any) -> List[Any]:
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj)
+        return out
+
+    def bcast(self, obj: Any, root: int = 0) -> Any:
+        if self.size == 1:
+            return obj
+        box = [obj if self.rank == root else None]
+        dist.broadcast_object_list(box, src=root)
+        return box[0]
+
+    def Barrier(self) -> None:
+        if self.size > 1:
+            dist.barrier()
+
+    def Abort(self, code: int = 1) -> None:
+        """Tear the job down (reference C:203-205).  Aborting the RCCL communicator first
+        unblocks peers stuck in a collective; the launcher then kills the rest."""
+        try:
+            if self.native is not None:
+                self.native.abort()
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(code)
+
+    # ---- data plane ----
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place SUM over ranks on the current stream."""
+        if self.size == 1:
+            return t
+        if t.is_cuda:
+            if self.native is not None:
+                stream = torch.cuda.current_stream(t.device).cuda_stream
+                if t.dtype == torch.float32:
+                    self.native.allreduce_f32(t.data_ptr(), t.numel(), stream)
+                elif t.dtype == torch.float64:
+                    self.native.allreduce_f64(t.data_ptr(), t.numel(), stream)
+                else:
+                    raise TypeError(f"allreduce_: unsupported dtype {t.dtype}")
+            else:
+                dist.all_reduce(t, group=self._nccl_group)
+        else:
+            dist.all_reduce(t)
+        return t
+
+    def close(self) -> None:
+        if self.native is not None:
+            self.native.destroy()
+            self.native = None
+        if self._initialized_here and dist.is_initialized():
+            dist.destroy_process_group()
+            self._initialized_here = False
+
+
+_WORLD: Optional[Comm] = None
+
+
+def get_world(backend: str = "auto", device: Optional[str] = None) -> Comm:
+    """Process-wide communicator (the analogue of ``MPI.COMM_WORLD``)."""
+    global _WORLD
+    if _WORLD is None:
+        _WORLD = Comm(backend=backend, device=device)
+    return _WORLD
+
+
+def reset_world() -> None:
+    global _WORLD
+    if _WORLD is not None:
+        _WORLD.close()
+    _WORLD = None
