@@ -1,0 +1,171 @@
+"""Flagship benchmark: federated rounds of the reference [C] workload on MI355X.
+
+One process per GPU, each GPU one federated client (the reference's mpiexec ranks).  A
+*step* is one full federated round exactly as the reference runs it
+(``FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:130-201``): a full-batch
+forward/backward + Adam step + StepLR step on the client's shard (MLP 14->50->200->2,
+fp32), local evaluation of the post-step model on the shard (forward + argmax + weighted
+metrics), and the sample-size-weighted FedAvg of all clients' weights (one RCCL
+all-reduce; per-round metrics and the early-stop state ride in the same collective).
+
+Data: synthetic balanced-income-shaped rows (14 features, 2 classes) generated on the
+device, ``--rows-per-client`` rows per client (default 8000 = the reference's
+single-client training shard), weights random-init.  Per-GPU work is fixed
+as N grows (weak scaling).  ``value`` = training samples processed per second summed over
+all clients; ``vs_baseline`` divides by the reference's measured train samples/s/client
+at the same client count times N (408k / 398k / 323k / 264k per client at
+k = 1 / 2 / 4 / 8; the reference's time excludes its eval and FedAvg, ours includes
+them).  After the timed region, rounds-to-target on the real income CSV (compat mode,
+this client count) is measured and reported as ``rounds_to_target``.
+
+    python bench.py --gpus 1 --steps 2000 --warmup 200
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+REF_PER_CLIENT = {1: 408e3, 2: 398e3, 4: 323e3, 8: 264e3}  # BASELINE.md, [C] train samples/s/client
+METRIC = "samples/sec/client + rounds-to-target-accuracy, MLP on income data at 1/2/4/8 clients"
+
+
+def ref_per_client(n: int) -> float:
+    if n in REF_PER_CLIENT:
+        return REF_PER_CLIENT[n]
+    ks = sorted(REF_PER_CLIENT)
+    k = min(ks, key=lambda x: abs(x - n))
+    return REF_PER_CLIENT[k]
+
+
+def synth_shard(n_rows: int, rank: int, device, seed: int = 7):
+    """Income-shaped rows generated on the device by the Philox kernel."""
+    from fedmi.data.synthetic import teacher_weights, make_income_like
+    from fedmi.ops import native
+    m = native()
+    w1, w2 = teacher_weights()
+    # balance threshold estimated on a host sample from the same distribution
+    Xs, _ = make_income_like(4096, seed=123)
+    th = float(np.median(np.maximum(Xs @ w1.T, 0.0) @ w2))
+    X = torch.empty((n_rows, 14), dtype=torch.float32, device=device)
+    y = torch.empty(n_rows, dtype=torch.int32, device=device)
+    tw1 = torch.as_tensor(w1, device=device)
+    tw2 = torch.as_tensor(np.append(w2, th).astype(np.float32), device=device)
+    m.synth(X.data_ptr(), y.data_ptr(), n_rows, 14, seed, rank * n_rows, tw1.data_ptr(), tw2.data_ptr(),
+            int(w1.shape[0]), torch.cuda.current_stream(device).cuda_stream)
+    torch.cuda.synchronize(device)
+    return X, y
+
+
+def rounds_to_target(comm, targets=(0.80, 0.83), max_rounds=300):
+    """Reference-compat convergence on the real CSV at this client count (untimed)."""
+    from fedmi.data.tabular import load_tabular
+    from fedmi.fl.engine import EngineConfig
+    from fedmi.fl.trainer import FederatedMLPLearning
+    ds = load_tabular()
+    cfg = EngineConfig(max_rounds=max_rounds, graph_rounds=16)
+    tr = FederatedMLPLearning(ds.X_train, ds.y_train, comm.rank, comm.size, comm=comm, config=cfg,
+                              mode="compat", seed=0)
+    tr.train_and_evaluate(comm, rounds=max_rounds, verbose=False)
+    h = tr.history()
+    acc = h["global"][:, 0]
+    out = {}
+    for t in targets:
+        hit = np.flatnonzero(acc >= t)
+        out[f"{t:.2f}"] = int(hit[0]) + 1 if len(hit) else None
+    out["early_stop_round"] = int(h["stop_round"]) if h["stop_round"] >= 0 else None
+    out["final_acc"] = float(acc[-1]) if len(acc) else None
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--rows-per-client", type=int, default=8000)
+    ap.add_argument("--hidden", type=int, nargs="+", default=[50, 200])
+    ap.add_argument("--rows-per-block", type=int, default=32)
+    ap.add_argument("--graph-rounds", type=int, default=16)
+    ap.add_argument("--backend", default="rccl", choices=["rccl", "nccl"])
+    ap.add_argument("--no-convergence", action="store_true")
+    a = ap.parse_args(argv)
+
+    from fedmi.fl.engine import EngineConfig, HipRoundEngine
+    from fedmi.models.mlp import init_flat
+    from fedmi.parallel.comm import get_world
+    import torch.distributed as dist
+
+    comm = get_world(backend=a.backend, device="cuda")
+    N = comm.size
+    if N != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
+    dev = comm.device
+    X, y = synth_shard(a.rows_per_client, comm.rank, dev)
+    dims = [14, *a.hidden, 2]
+    cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=a.warmup + a.steps + 8, early_stop=False,
+                       rows_per_block=a.rows_per_block, graph_rounds=a.graph_rounds)
+    eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank),
+                         n_total=a.rows_per_client * N)
+
+    def barrier():
+        if N > 1:
+            dist.barrier()
+
+    eng.run(a.warmup, check_every=max(a.warmup, 1))
+    eng.stream.synchronize()
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    eng._issue(a.steps)               # exactly K rounds, no host polling inside
+    eng.stream.synchronize()
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = time.perf_counter() - t0
+    if N > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    eng.sync_history()
+    h = eng.history()
+    assert h["rounds_run"] == a.warmup + a.steps, h["rounds_run"]
+    samples = a.rows_per_client * N * a.steps
+    value = samples / dt
+    rtt = None if a.no_convergence else rounds_to_target(comm)
+    if comm.rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "train samples/s (sum over clients; step = 1 federated round incl. eval + FedAvg)",
+            "n_gpus": N,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": value / (ref_per_client(N) * N),
+            "dtype": "fp32",
+            "data": f"synthetic income-shaped (device Philox), {a.rows_per_client} rows/client; random-init weights",
+            "config": {"model": f"MLP {'-'.join(map(str, dims))} (reference [C])",
+                       "global_batch": a.rows_per_client * N, "seq_len": 1,
+                       "parallelism": f"fedavg{N} (1 client/GPU, RCCL all-reduce)",
+                       "rows_per_client": a.rows_per_client, "optimizer": "Adam(0.004)+StepLR(30,0.5)"},
+            "samples_per_sec_per_client": value / N,
+            "final_train_acc_synthetic": float(h["global"][-1][0]),
+            "rounds_to_target": rtt,
+        }
+        print(json.dumps(rec), flush=True)
+    comm.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -26,7 +26,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from ..models.mlp import MLPModel, flat_to_dict, param_count
+from ..models.mlp import (MLPModel, dense_to_image, flat_to_dict, image_layout, image_to_dense,
+                          param_count)
 from .early_stop import EarlyStopper
 from .metrics import METRIC_NAMES, confusion_matrix, metrics_from_confusion, metric_vector
 
@@ -299,12 +300,14 @@ class HipRoundEngine(RoundEngineBase):
         self.R = R
         n_slabs = (self.n_local + R - 1) // R
         slab_stride = ((self.P + 1) + 3) & ~3
-        comm_len = self.P + self.world * self.tail_stride
+        # device parameter buffers use the padded image layout (fl_common.h)
+        self.Pimg = image_layout(self.dims)[2]
+        comm_len = self.Pimg + self.world * self.tail_stride
         self.params = [torch.zeros(comm_len, **f32), torch.zeros(comm_len, **f32)]
-        self.params[0][:self.P] = torch.as_tensor(init_flat, dtype=torch.float32)
-        self.local = self.params[0][:self.P].clone()
-        self.mom = torch.zeros(self.P, **f32)
-        self.vel = torch.zeros(self.P, **f32)
+        self.params[0][:self.Pimg] = torch.as_tensor(dense_to_image(init_flat, self.dims))
+        self.local = self.params[0][:self.Pimg].clone()
+        self.mom = torch.zeros(self.Pimg, **f32)
+        self.vel = torch.zeros(self.Pimg, **f32)
         self.slab = torch.zeros(n_slabs * slab_stride, **f32)
         sb = self.m.STATE_BYTES
         assert sb == _STATE_DTYPE.itemsize, (sb, _STATE_DTYPE.itemsize)
@@ -335,6 +338,9 @@ class HipRoundEngine(RoundEngineBase):
         }
         self.engine = self.m.FLEngine(self.dims, ecfg, bufs)
         self.layout = self.engine.layout()
+        iw, ib, _ = image_layout(self.dims)
+        if (self.layout["Pimg"], list(self.layout["iw_off"]), list(self.layout["ib_off"])) != (self.Pimg, iw, ib):
+            raise RuntimeError(f"image layout mismatch between C++ and Python: {self.layout}")
         # the engine owns a non-default stream: graph capture is illegal on the null stream
         self.stream = torch.cuda.Stream(device=dev)
         self.stream.wait_stream(torch.cuda.current_stream(dev))
@@ -387,7 +393,7 @@ class HipRoundEngine(RoundEngineBase):
         self.engine.phase(r, 1, self._stream(), None)
         self.stream.synchronize()
         C = self.n_classes
-        t0 = self.P + self.rank * self.tail_stride
+        t0 = self.Pimg + self.rank * self.tail_stride
         return self.params[(r + 1) & 1][t0:t0 + C * C].cpu().numpy().reshape(C, C).astype(np.int64)
 
     def step_aggregate(self) -> None:
@@ -441,15 +447,15 @@ class HipRoundEngine(RoundEngineBase):
 
     def global_flat(self) -> np.ndarray:
         self.stream.synchronize()
-        return self.params[self.rounds_issued & 1][:self.P].cpu().numpy().copy()
+        return image_to_dense(self.params[self.rounds_issued & 1][:self.Pimg].cpu().numpy(), self.dims)
 
     def local_flat(self) -> np.ndarray:
         self.stream.synchronize()
-        return self.local.cpu().numpy().copy()
+        return image_to_dense(self.local.cpu().numpy(), self.dims)
 
     def set_global_flat(self, flat: np.ndarray) -> None:
         self.stream.synchronize()
-        self.params[self.rounds_issued & 1][:self.P].copy_(torch.as_tensor(flat, dtype=torch.float32))
+        self.params[self.rounds_issued & 1][:self.Pimg].copy_(torch.as_tensor(dense_to_image(flat, self.dims)))
         torch.cuda.current_stream(self.device).synchronize()
 
     def confusion(self, X=None, y=None, flat=None) -> np.ndarray:
@@ -458,7 +464,7 @@ class HipRoundEngine(RoundEngineBase):
         if flat is None:
             p = self.local
         else:
-            p = torch.as_tensor(flat, dtype=torch.float32, device=self.device)
+            p = torch.as_tensor(dense_to_image(flat, self.dims), device=self.device)
         cm = torch.zeros(self.n_classes ** 2, dtype=torch.float32, device=self.device)
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         self.engine.confusion(Xt.data_ptr(), yt.data_ptr(), int(Xt.shape[0]), p.data_ptr(), cm.data_ptr(),
@@ -468,8 +474,9 @@ class HipRoundEngine(RoundEngineBase):
 
     def state_dict(self) -> dict:
         self.stream.synchronize()
-        return {"params": self.global_flat(), "local": self.local_flat(), "exp_avg": self.mom.cpu().numpy(),
-                "exp_avg_sq": self.vel.cpu().numpy(), "rounds": self.rounds_issued,
+        return {"params": self.global_flat(), "local": self.local_flat(),
+                "exp_avg": image_to_dense(self.mom.cpu().numpy(), self.dims),
+                "exp_avg_sq": image_to_dense(self.vel.cpu().numpy(), self.dims), "rounds": self.rounds_issued,
                 "state": self.state[self.rounds_issued & 1].cpu().numpy(), "history": self.hist.as_dict()}
 
 

@@ -112,6 +112,53 @@ def flat_to_sklearn(flat, dims: Sequence[int]):
     return coefs, inter
 
 
+def _ldw(K: int) -> int:
+    return ((K + 15) & ~15) + 4
+
+
+def _r16(n: int) -> int:
+    return (n + 15) & ~15
+
+
+def image_layout(dims: Sequence[int]):
+    """Offsets of the padded device parameter image (fedmi/ops/csrc/fl_common.h): per layer
+    W_l as [roundup16(N)][roundup16(K)+2] then b_l as [roundup16(N)], zero padded."""
+    iw, ib, off = [], [], 0
+    for l in range(len(dims) - 1):
+        K, N = dims[l], dims[l + 1]
+        iw.append(off)
+        off += _r16(N) * _ldw(K)
+        ib.append(off)
+        off += _r16(N)
+    return iw, ib, (off + 3) & ~3
+
+
+def dense_to_image(flat: np.ndarray, dims: Sequence[int]) -> np.ndarray:
+    iw, ib, total = image_layout(dims)
+    img = np.zeros(total, dtype=np.float32)
+    flat = np.asarray(flat, dtype=np.float32)
+    for l, (name, shape, off) in enumerate(param_layout(dims)[0::2]):
+        N, K = shape
+        W = flat[off:off + N * K].reshape(N, K)
+        bo = off + N * K
+        ldw = _ldw(K)
+        img[iw[l]:iw[l] + _r16(N) * ldw].reshape(_r16(N), ldw)[:N, :K] = W
+        img[ib[l]:ib[l] + N] = flat[bo:bo + N]
+    return img
+
+
+def image_to_dense(img: np.ndarray, dims: Sequence[int]) -> np.ndarray:
+    iw, ib, total = image_layout(dims)
+    img = np.asarray(img, dtype=np.float32)
+    out = np.empty(param_count(dims), dtype=np.float32)
+    for l, (name, shape, off) in enumerate(param_layout(dims)[0::2]):
+        N, K = shape
+        ldw = _ldw(K)
+        out[off:off + N * K] = img[iw[l]:iw[l] + _r16(N) * ldw].reshape(_r16(N), ldw)[:N, :K].reshape(-1)
+        out[off + N * K:off + N * K + N] = img[ib[l]:ib[l] + N]
+    return out
+
+
 def init_flat(dims: Sequence[int], seed: int) -> np.ndarray:
     """torch ``nn.Linear`` default init (kaiming-uniform a=sqrt(5) => U(-1/sqrt(fan_in),
     1/sqrt(fan_in)) for weight and bias), drawn from a seeded generator."""

@@ -1,11 +1,19 @@
 // Shared host/device declarations of the fused federated-round engine.
 //
-// One client per GPU keeps everything resident: the local shard, a flat fp32 parameter
-// buffer in the reference's named_parameters() order (model.0.weight, model.0.bias,
-// model.2.weight, ...; FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:93-99),
-// the Adam moments (which persist across rounds), a per-block gradient slab,
-// and a small device-side round state that carries the early-stopping rule (C:181-192)
-// so the host never has to read metrics back to decide whether to continue.
+// One client per GPU keeps everything resident: the local shard, the parameters, the Adam
+// moments (which persist across rounds), a per-block gradient slab, and a small
+// device-side round state that carries the early-stopping rule
+// (FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:181-192) so the host never has to
+// read metrics back to decide whether to continue.
+//
+// Parameter "image" layout.  Every parameter-shaped device buffer (global/comm, local, m, v)
+// stores, per layer l, W_l ([N][K], torch Linear layout) as fl_wrows(N) rows of fl_ldw(K)
+// floats followed by b_l padded to roundup16(N), all padding zero.  The image is exactly the
+// LDS image the kernels compute from, so staging a model into LDS is one contiguous float4
+// copy, and every MFMA operand read of a 16x16 tile / 16-deep k chunk is in bounds and reads
+// zeros in the padding (no predication, no exec-mask branches in inner loops).  The dense
+// reference layout (named_parameters() order: model.0.weight, model.0.bias, ...; C:93-99)
+// exists only at the API boundary (get/set weights, checkpoints) and in the gradient slab.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -14,27 +22,36 @@
 #define FL_MAX_CLASSES 16
 #define FL_MAX_WORLD 64
 
+// ldw = roundup16(K) + 4 (4 mod 8 floats): 16-byte aligned rows, and the 16 rows of a
+// 16-lane ds_read_b128 group land on 16 distinct 16-byte bank slots.
+__host__ __device__ inline int fl_ldw(int K) { return ((K + 15) & ~15) + 4; }
+__host__ __device__ inline int fl_wrows(int N) { return (N + 15) & ~15; }
+
 struct MLPDesc {
     int L;                            // number of Linear layers
     int dim[FL_MAX_LAYERS + 1];       // dim[0] = features, dim[L] = classes
     int ld[FL_MAX_LAYERS + 1];        // LDS leading dimension (floats) per activation buffer
     int act_off[FL_MAX_LAYERS + 1];   // LDS float offset of each activation buffer (R rows)
-    int w_off[FL_MAX_LAYERS];         // float offset of W_l [dim[l+1], dim[l]] in the flat buffer
-    int b_off[FL_MAX_LAYERS];         // float offset of b_l [dim[l+1]]
-    int P;                            // number of parameters (dense, reference order)
+    int w_off[FL_MAX_LAYERS];         // dense (reference) offset of W_l
+    int b_off[FL_MAX_LAYERS];         // dense offset of b_l
+    int P;                            // dense parameter count
+    int iw_off[FL_MAX_LAYERS];        // image offset of W_l
+    int ib_off[FL_MAX_LAYERS];        // image offset of b_l
+    int Pimg;                         // image floats (multiple of 4)
+    int img_lds;                      // LDS float offset of the staged image
     int lds_floats;                   // LDS floats needed per block
 };
 
 struct FLConfig {
-    int R;              // rows per workgroup (16, 32 or 64)
+    int R;              // rows per workgroup (16 or 32)
     int n_rows;         // local training rows
     float inv_n;        // 1 / n_rows  (CrossEntropyLoss 'mean', C:43)
     int world;
     int rank;
     float agg_scale;    // n_rank / N_total (sample-size-weighted FedAvg, C:110-116)
-    int slab_stride;    // floats per slab row (P + loss slot, padded)
+    int slab_stride;    // floats per slab row (dense P + loss slot, padded)
     int n_slabs;        // workgroups of the train kernel = ceil(n_rows / R)
-    int tail_off;       // == P: start of the per-rank metric tail in the comm buffer
+    int tail_off;       // == Pimg: start of the per-rank metric tail in the comm buffer
     int tail_stride;    // C*C confusion counts + 1 loss slot
     int tail_len;       // world * tail_stride
     int local_steps;    // optimizer steps per round (reference: 1 full-batch step, C:63-73)
@@ -76,17 +93,18 @@ struct FLState {
 struct FLBuffers {
     const float* X;     // [n_rows, dim0] row-major, device resident
     const int* y;       // [n_rows]
-    float* slab;        // [n_slabs, slab_stride]
-    float* local;       // [P] post-step local weights (evaluated, C:148)
-    float* m;           // [P] Adam exp_avg
-    float* v;           // [P] Adam exp_avg_sq
+    float* slab;        // [n_slabs, slab_stride] dense gradient partials
+    float* local;       // [Pimg] post-step local weights (evaluated, C:148)
+    float* m;           // [Pimg] Adam exp_avg
+    float* v;           // [Pimg] Adam exp_avg_sq
     double* hist_global;  // [max_rounds, 4]
     double* hist_rank;    // [max_rounds, world, 4]
     float* hist_loss;     // [max_rounds] mean CE over clients
+    unsigned long long* dbg;  // optional [blocks, 16] s_memrealtime phase stamps (profiling)
 };
 
-// Launchers (fl_kernels.hip). `pg` = params the round trains from (the previous round's
-// all-reduced comm buffer), `comm` = buffer this round publishes into (P + tail floats).
+// Launchers (fl_kernels.hip). `pg` = image the round trains from (the previous round's
+// all-reduced comm buffer), `comm` = buffer this round publishes into (Pimg + tail floats).
 hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                            const float* pg, const FLState* st_in, FLState* st_out,
                            int local_step, hipStream_t s);

@@ -106,11 +106,9 @@ class RcclComm {
 // ---------------------------------------------------------------------------------------
 // Engine
 // ---------------------------------------------------------------------------------------
-static int pick_ld(int dim) {
-    int ld = (dim + 15) & ~15;
-    while (ld % 32 != 17) ++ld;
-    return ld;
-}
+// Activation row stride: roundup16(dim) + 4 floats (16-byte aligned rows, 4 mod 8 so the
+// b128 / b32 MFMA operand patterns of fl_kernels.hip are bank-conflict free).
+static int pick_ld(int dim) { return ((dim + 15) & ~15) + 4; }
 
 class FLEngine {
   public:
@@ -134,8 +132,18 @@ class FLEngine {
         if (C > FL_MAX_CLASSES) throw std::runtime_error("FLEngine: at most 16 classes");
         if (dims[0] > 4096) throw std::runtime_error("FLEngine: too many features");
 
+        // parameter image (fl_common.h): per layer [wrows(N)][ldw(K)] then bias[roundup16(N)]
+        int io = 0;
+        for (int l = 0; l < L; ++l) {
+            d_.iw_off[l] = io;
+            io += fl_wrows(dims[l + 1]) * fl_ldw(dims[l]);
+            d_.ib_off[l] = io;
+            io += (dims[l + 1] + 15) & ~15;
+        }
+        d_.Pimg = (io + 3) & ~3;
+
         c_.R = cfg["R"].cast<int>();
-        if (c_.R != 16 && c_.R != 32 && c_.R != 64) throw std::runtime_error("FLEngine: R must be 16, 32 or 64");
+        if (c_.R != 16 && c_.R != 32) throw std::runtime_error("FLEngine: R must be 16 or 32");
         int lds = 0;
         for (int l = 0; l <= L; ++l) {
             d_.ld[l] = pick_ld(dims[l]);
@@ -143,6 +151,8 @@ class FLEngine {
             lds += c_.R * d_.ld[l];
             lds = (lds + 3) & ~3;
         }
+        d_.img_lds = lds;
+        lds += d_.Pimg;
         d_.lds_floats = lds;
         if ((size_t)lds * 4 > 150 * 1024)
             throw std::runtime_error("FLEngine: activations exceed LDS; use a smaller R or the layered path");
@@ -156,7 +166,7 @@ class FLEngine {
         c_.agg_scale = cfg["agg_scale"].cast<float>();
         c_.slab_stride = ((d_.P + 1) + 3) & ~3;
         c_.n_slabs = (c_.n_rows + c_.R - 1) / c_.R;
-        c_.tail_off = d_.P;
+        c_.tail_off = d_.Pimg;
         c_.tail_stride = C * C + 1;
         c_.tail_len = c_.world * c_.tail_stride;
         c_.local_steps = cfg["local_steps"].cast<int>();
@@ -246,6 +256,51 @@ class FLEngine {
 
     int graph_rounds() const { return graph_rounds_; }
 
+    // Enable (ptr != 0) / disable in-kernel phase stamps: [blocks, 16] uint64 buffer.
+    void set_debug(uintptr_t ptr) { b_.dbg = as_ptr<unsigned long long>(ptr); }
+
+    // Launch one kernel of round r on its live state (0 = train, 1 = adam, 2 = eval).
+    void launch_one(int r, int which, uintptr_t stream) {
+        hipStream_t s = as_stream(stream);
+        float* pg = pbuf_[r & 1];
+        float* cb = pbuf_[(r + 1) & 1];
+        FLState* so = st_[(r + 1) & 1];
+        if (which == 0) HIP_CHECK(fl_launch_train(d_, c_, b_, pg, so, so, 1, s));
+        else if (which == 1) HIP_CHECK(fl_launch_adam(d_, c_, b_, b_.local, pg, cb, so, 1, s));
+        else HIP_CHECK(fl_launch_eval(d_, c_, b_, b_.local, cb, so, s));
+    }
+
+    // Per-kernel device time (us, averaged over `iters` back-to-back launches, hipEvents)
+    // re-running the kernels of the last issued round `r` on its (live) state.  Training
+    // launches use local_step=1 semantics so the round state is not advanced.
+    py::dict time_kernels(int r, int iters, uintptr_t stream) {
+        hipStream_t s = as_stream(stream);
+        float* pg = pbuf_[r & 1];
+        float* cb = pbuf_[(r + 1) & 1];
+        FLState* so = st_[(r + 1) & 1];
+        hipEvent_t e0, e1;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        py::dict out;
+        auto timeit = [&](const char* name, auto&& launch) {
+            launch();
+            HIP_CHECK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i) launch();
+            HIP_CHECK(hipEventRecord(e1, s));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            out[name] = 1e3 * ms / iters;
+        };
+        const int ls = 1;
+        timeit("train", [&] { HIP_CHECK(fl_launch_train(d_, c_, b_, pg, so, so, ls, s)); });
+        timeit("adam", [&] { HIP_CHECK(fl_launch_adam(d_, c_, b_, b_.local, pg, cb, so, ls, s)); });
+        timeit("eval", [&] { HIP_CHECK(fl_launch_eval(d_, c_, b_, b_.local, cb, so, s)); });
+        HIP_CHECK(hipEventDestroy(e0));
+        HIP_CHECK(hipEventDestroy(e1));
+        return out;
+    }
+
     // held-out evaluation: confusion matrix of `params` on (X, y) accumulated into cm_out
     void confusion(uintptr_t X, uintptr_t y, int n_rows, uintptr_t params, uintptr_t cm_out, uintptr_t stream) {
         HIP_CHECK(fl_launch_confusion(d_, c_.R, as_ptr<const float>(X), as_ptr<const int>(y), n_rows,
@@ -254,12 +309,18 @@ class FLEngine {
 
     py::dict layout() const {
         py::dict o;
-        std::vector<int> w, bb, ld, dims;
-        for (int l = 0; l < d_.L; ++l) { w.push_back(d_.w_off[l]); bb.push_back(d_.b_off[l]); }
+        std::vector<int> w, bb, iw, ib, ld, dims;
+        for (int l = 0; l < d_.L; ++l) {
+            w.push_back(d_.w_off[l]); bb.push_back(d_.b_off[l]);
+            iw.push_back(d_.iw_off[l]); ib.push_back(d_.ib_off[l]);
+        }
         for (int l = 0; l <= d_.L; ++l) { ld.push_back(d_.ld[l]); dims.push_back(d_.dim[l]); }
         o["P"] = d_.P;
+        o["Pimg"] = d_.Pimg;
         o["w_off"] = w;
         o["b_off"] = bb;
+        o["iw_off"] = iw;
+        o["ib_off"] = ib;
         o["ld"] = ld;
         o["dims"] = dims;
         o["lds_bytes"] = d_.lds_floats * 4;
@@ -268,7 +329,7 @@ class FLEngine {
         o["tail_off"] = c_.tail_off;
         o["tail_stride"] = c_.tail_stride;
         o["tail_len"] = c_.tail_len;
-        o["comm_len"] = d_.P + c_.tail_len;
+        o["comm_len"] = d_.Pimg + c_.tail_len;
         o["state_bytes"] = (int)sizeof(FLState);
         return o;
     }
@@ -289,7 +350,7 @@ class FLEngine {
     }
     void issue_allreduce(int r, hipStream_t s, RcclComm* comm) {
         if (comm != nullptr && c_.world > 1)
-            comm->allreduce_f32((uintptr_t)pbuf_[(r + 1) & 1], (size_t)(d_.P + c_.tail_len), (uintptr_t)s);
+            comm->allreduce_f32((uintptr_t)pbuf_[(r + 1) & 1], (size_t)(d_.Pimg + c_.tail_len), (uintptr_t)s);
     }
     void issue_round(int r, hipStream_t s, RcclComm* comm) {
         issue_train(r, s);
@@ -355,6 +416,9 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("capture", &FLEngine::capture, py::arg("n"), py::arg("stream"), py::arg("comm") = nullptr)
         .def("replay", &FLEngine::replay)
         .def("graph_rounds", &FLEngine::graph_rounds)
+        .def("time_kernels", &FLEngine::time_kernels)
+        .def("set_debug", &FLEngine::set_debug)
+        .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);
     m.def("synth", &synth);

@@ -2,124 +2,208 @@
 //
 // The reference round (FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:130-201)
 // is ~20 ATen launches + 6 H2D/D2H copies + pickled MPI gather/bcast per round.  Here a
-// round is three kernels and one all-reduce, all on one stream:
+// round is three kernels and one all-reduce on one stream:
 //
 //   fl_train  : finalize(prev round metrics, early stop) ; per-workgroup fwd + CE + bwd
-//               over R rows with every activation in LDS, per-workgroup weight-gradient
-//               partials -> slab                                   (K2-K17)
-//   fl_adam   : deterministic slab reduction + Adam (+L2, +FedProx) + StepLR, writes the
-//               local weights and the pre-scaled (n_i/N) FedAvg contribution  (K18, K22)
+//               over R rows with the parameter image AND activations in LDS; dense
+//               weight-gradient partials -> slab row              (K2-K17)
+//   fl_adam   : wide deterministic slab reduction (16 waves per 64 parameters) + Adam
+//               (+L2, +FedProx) + StepLR; writes the local image and the pre-scaled (n_i/N)
+//               FedAvg contribution                                (K18, K22)
 //   fl_eval   : forward of the post-step local model on the local shard, argmax and the
-//               C x C confusion matrix, accumulated into this rank's tail slot  (K20, Q2)
-//   allreduce : one RCCL SUM over [weights*n_i/N | per-rank tails] = gather+average+bcast
-//               of weights, sizes, metrics and the stop signal in one collective (§2.4)
+//               C x C confusion matrix into this rank's tail slot  (K20, Q2)
+//   allreduce : one RCCL SUM over [image*n_i/N | per-rank tails] = gather + average +
+//               bcast of weights, sizes, metrics and stop signal in one collective (§2.4)
 //
-// GEMMs run on the f32-input MFMA (v_mfma_f32_16x16x4_f32, exact f32 fma chain -- the
-// reference trains in fp32), one 16x16 output tile per wave at a time, A operands from
-// LDS, B operands (weights) streamed from L2 with the next k-step prefetched.
+// GEMM-shaped work runs on the f32-input MFMA (v_mfma_f32_16x16x4_f32: exact f32 fma chain;
+// the reference trains in fp32).  Work items are 16-wide column tiles spread over the 8
+// waves of a 512-thread workgroup; a wave keeps one accumulator per 16-row tile so a B
+// fragment is read once per k and reused RT times, and the next 16-deep k chunk is loaded
+// while the current one is multiplied.  The skinny classifier head (C outputs) runs on the
+// VALU with a fixed-order split-K shuffle reduction.
 #include "fl_common.h"
 #include <math.h>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#define FL_THREADS 256
+#define FL_THREADS 512
 #define FL_WAVES (FL_THREADS / 64)
+
+// In-kernel phase stamps (100 MHz s_memrealtime) for profiling; off unless b.dbg is set.
+#define FL_STAMP(i)                                                                            \
+    do {                                                                                       \
+        if (b.dbg != nullptr && threadIdx.x == 0)                                              \
+            b.dbg[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime();                   \
+    } while (0)
+
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits vmcnt(0), which puts
+// every in-flight global store (the per-block gradient slab) and load on the critical path
+// of each phase; the phases here only hand data to each other through LDS.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ f32x4 mfma_f32(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------------------
-// Block-cooperative GEMM building blocks.  All LDS matrices are row-major with leading
-// dimensions chosen on the host (ld % 32 == 17) so both MFMA operand read patterns
-// ([16 rows x 4 k] and [4 rows x 16 cols] per wave) are (almost) bank-conflict free.
-// MFMA 16x16x4 f32 operand maps: A lane l -> A[l&15][l>>4]; B lane l -> B[l>>4][l&15];
-// C/D: col = l&15, row = 4*(l>>4) + j.
+// Block-cooperative GEMM pieces (operand maps of 16x16x4 f32 MFMA:
+//   A lane l -> A[l&15][l>>4], B lane l -> B[l>>4][l&15], C/D: col l&15, row 4(l>>4)+j).
+// The contraction order is free, so k is permuted: in a 16-deep chunk q, MFMA step j takes
+// k = 16q + 4*lg + j from lane group lg.  A lane then owns 4 CONSECUTIVE k, i.e. one 16-byte
+// ds_read_b128 per operand wherever k runs along an LDS row (row strides are 4 mod 8 floats,
+// so 16 rows of one 16-lane group hit 16 distinct 16-byte bank slots).  All loads of a chunk
+// are issued before its MFMAs (sched_barrier), so LDS latency overlaps the matrix pipe.
 // ---------------------------------------------------------------------------------------
 
-// out[r][n] = act(sum_k in[r][k] * W[n][k] + bias[n]); W is [N][K] (torch Linear layout).
-// Columns n in [N, roundup16(N)) are written as 0 so later K-loops may read them.
+__device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float f4(const float4& v, int j) {
+    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+// out[r][n] = act(sum_k in[r][k] W[n][k] + bias[n]) for all R rows; columns
+// [N, roundup16(N)) come out 0 (zero image rows + zero bias padding).
 template <int RT>
-__device__ void fwd_layer(const float* __restrict__ W, const float* __restrict__ bias, int K, int N,
-                          const float* in, int ld_in, float* out, int ld_out, bool relu) {
+__device__ void fwd_layer_mfma(const float* w, int ldw, const float* bias, int K, int N, const float* in,
+                               int ld_in, float* out, int ld_out, bool relu) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     const int ntiles = (N + 15) >> 4;
-    const int ksteps = (K + 3) >> 2;
+    const int kchunks = (K + 15) >> 4;
     for (int nt = wave; nt < ntiles; nt += FL_WAVES) {
         const int n = nt * 16 + lr;
-        const bool nvalid = n < N;
-        const float* wrow = W + (size_t)(nvalid ? n : 0) * K;
+        const float* wr = w + n * ldw + 4 * lg;
+        const float* ar = in + lr * ld_in + 4 * lg;
         f32x4 acc[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        int k = lg;
-        float bnext = (nvalid && k < K) ? wrow[k] : 0.f;
-        for (int s = 0; s < ksteps; ++s) {
-            const float b = bnext;
-            const int kn = k + 4;
-            bnext = (nvalid && kn < K) ? wrow[kn] : 0.f;
+        float4 bc = lds4(wr), ac[RT];
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-                const float a = in[(rt * 16 + lr) * ld_in + k];
-                acc[rt] = mfma_f32(a, b, acc[rt]);
-            }
-            k = kn;
+        for (int rt = 0; rt < RT; ++rt) ac[rt] = lds4(ar + rt * 16 * ld_in);
+        for (int q = 0; q < kchunks; ++q) {
+            const int qn = (q + 1 < kchunks) ? q + 1 : q;  // prefetch (last: harmless reload)
+            const float4 bn = lds4(wr + 16 * qn);
+            float4 an[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) an[rt] = lds4(ar + rt * 16 * ld_in + 16 * qn);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma_f32(f4(ac[rt], j), f4(bc, j), acc[rt]);
+            __builtin_amdgcn_sched_barrier(0);
+            bc = bn;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) ac[rt] = an[rt];
         }
-        const float bv = nvalid ? bias[n] : 0.f;
+        const float bv = bias[n];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float v = acc[rt][j] + bv;
                 if (relu) v = fmaxf(v, 0.f);
-                out[(rt * 16 + lg * 4 + j) * ld_out + n] = nvalid ? v : 0.f;
+                out[(rt * 16 + lg * 4 + j) * ld_out + n] = v;
             }
-        }
     }
 }
 
-// dH[r][i] = (sum_o dZ[r][o] * W[o][i]) * (act[r][i] > 0), written in place over act.
-// W is [N][K]: N = fan-out (reduction), K = fan-in (output columns).
+// Skinny head on the VALU: z[r][c] = bias[c] + sum_k in[r][k] W[c][k] for R*C <= 128.
+// T threads per output (power of 2), fixed-order xor-shuffle reduction (deterministic).
 template <int RT>
-__device__ void dgrad_layer(const float* __restrict__ W, int K, int N, const float* dz, int ld_z,
-                            float* act, int ld_a) {
+__device__ void fwd_head_valu(const float* w, int ldw, const float* bias, int K, int C, const float* in,
+                              int ld_in, float* out, int ld_out) {
+    const int R = RT * 16;
+    const int nout = R * C;
+    int T = FL_THREADS / nout;
+    T = T >= 64 ? 64 : (T >= 32 ? 32 : (T >= 16 ? 16 : (T >= 8 ? 8 : (T >= 4 ? 4 : (T >= 2 ? 2 : 1)))));
+    const int K16 = (K + 15) & ~15;  // zero padded in both operands
+    for (int base = 0; base < nout * T; base += FL_THREADS) {
+        const int gid = base + threadIdx.x;
+        const int o = gid / T, part = gid - o * T;
+        const int oc = o < nout ? o : nout - 1;
+        const int r = oc / C, c = oc - r * C;
+        const float* ar = in + r * ld_in;
+        const float* wr = w + c * ldw;
+        float s0 = 0.f, s1 = 0.f;
+        // 4 consecutive k per thread per step: float4 reads
+        int k = 4 * part;
+        for (; k + 4 * T < K16; k += 8 * T) {
+            const float4 a0 = lds4(ar + k), w0 = lds4(wr + k);
+            const float4 a1 = lds4(ar + k + 4 * T), w1 = lds4(wr + k + 4 * T);
+            s0 = fmaf(a0.x, w0.x, s0); s0 = fmaf(a0.y, w0.y, s0); s0 = fmaf(a0.z, w0.z, s0); s0 = fmaf(a0.w, w0.w, s0);
+            s1 = fmaf(a1.x, w1.x, s1); s1 = fmaf(a1.y, w1.y, s1); s1 = fmaf(a1.z, w1.z, s1); s1 = fmaf(a1.w, w1.w, s1);
+        }
+        if (k < K16) {
+            const float4 a0 = lds4(ar + k), w0 = lds4(wr + k);
+            s0 = fmaf(a0.x, w0.x, s0); s0 = fmaf(a0.y, w0.y, s0); s0 = fmaf(a0.z, w0.z, s0); s0 = fmaf(a0.w, w0.w, s0);
+        }
+        float s = s0 + s1;
+        for (int off = 1; off < T; off <<= 1) s += __shfl_xor(s, off, 64);
+        if (o < nout && part == 0) out[r * ld_out + c] = s + bias[c];
+    }
+    const int Cp = (C + 15) & ~15;  // zero padded columns [C, roundup16(C))
+    for (int e = threadIdx.x; e < R * (Cp - C); e += FL_THREADS) {
+        const int r = e / (Cp - C), c = C + (e - r * (Cp - C));
+        out[r * ld_out + c] = 0.f;
+    }
+}
+
+// dH[r][i] = (sum_o dZ[r][o] W[o][i]) * (act[r][i] > 0), in place over act.
+// Item = 16-column tile of dH (all R rows); B fragment W[o][i] reused across the RT rows.
+template <int RT>
+__device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* dz, int ld_z, float* act,
+                            int ld_a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     const int itiles = (K + 15) >> 4;
-    const int osteps = (N + 3) >> 2;
+    const int ochunks = (N + 15) >> 4;
     for (int it = wave; it < itiles; it += FL_WAVES) {
         const int i = it * 16 + lr;
-        const bool ivalid = i < K;
+        const float* wc = w + 4 * lg * ldw + i;     // B: W[16q + 4lg + j][i]
+        const float* ar = dz + lr * ld_z + 4 * lg;  // A: dZ[r][16q + 4lg + j]
         f32x4 acc[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        int o = lg;
-        float bnext = (ivalid && o < N) ? W[(size_t)o * K + i] : 0.f;
-        for (int s = 0; s < osteps; ++s) {
-            const float b = bnext;
-            const int on = o + 4;
-            bnext = (ivalid && on < N) ? W[(size_t)on * K + i] : 0.f;
+        float bc[4];
+        float4 ac[RT];
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-                const float a = dz[(rt * 16 + lr) * ld_z + o];
-                acc[rt] = mfma_f32(a, b, acc[rt]);
-            }
-            o = on;
+        for (int j = 0; j < 4; ++j) bc[j] = wc[j * ldw];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) ac[rt] = lds4(ar + rt * 16 * ld_z);
+        for (int q = 0; q < ochunks; ++q) {
+            const int qn = (q + 1 < ochunks) ? q + 1 : q;
+            float bn[4];
+            float4 an[RT];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bn[j] = wc[(16 * qn + j) * ldw];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) an[rt] = lds4(ar + rt * 16 * ld_z + 16 * qn);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma_f32(f4(ac[rt], j), bc[j], acc[rt]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bc[j] = bn[j];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) ac[rt] = an[rt];
         }
+        const bool ivalid = i < K;
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float* p = act + (rt * 16 + lg * 4 + j) * ld_a + i;
                 const float a = *p;
                 *p = (ivalid && a > 0.f) ? acc[rt][j] : 0.f;
             }
-        }
     }
 }
 
-// dW[o][i] = sum_r dZ[r][o] * act[r][i] over the block's R rows -> gW (global, [N][K]).
+// dW[o][i] = sum_r dZ[r][o] act[r][i] over the block's rows -> gW ([N][K] dense, global);
+// gb[o] = sum_r dZ[r][o].  Two output tiles per wave are interleaved (independent chains);
+// row r = 16q + 4lg + j of chunk q feeds MFMA step j of lane group lg.
 template <int RT>
 __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float* act, int ld_a,
                             float* __restrict__ gW, float* __restrict__ gb) {
@@ -127,50 +211,85 @@ __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float
     const int lr = lane & 15, lg = lane >> 4;
     const int otiles = (N + 15) >> 4, itiles = (K + 15) >> 4;
     const int ntile = otiles * itiles;
-    for (int t = wave; t < ntile; t += FL_WAVES) {
-        const int ot = t / itiles, it = t - ot * itiles;
-        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t0 = wave; t0 < ntile; t0 += 2 * FL_WAVES) {
+        const int t1raw = t0 + FL_WAVES;
+        const bool has1 = t1raw < ntile;
+        const int t1 = has1 ? t1raw : t0;
+        const int ot0 = t0 / itiles, it0 = t0 - ot0 * itiles;
+        const int ot1 = t1 / itiles, it1 = t1 - ot1 * itiles;
+        const float* ap0 = dz + 4 * lg * ld_z + ot0 * 16 + lr;
+        const float* bp0 = act + 4 * lg * ld_a + it0 * 16 + lr;
+        const float* ap1 = dz + 4 * lg * ld_z + ot1 * 16 + lr;
+        const float* bp1 = act + 4 * lg * ld_a + it1 * 16 + lr;
+        float a0[RT * 4], b0[RT * 4], a1[RT * 4], b1[RT * 4];
 #pragma unroll
-        for (int s = 0; s < RT * 4; ++s) {
-            const int r = s * 4 + lg;
-            const float a = dz[r * ld_z + ot * 16 + lr];
-            const float b = act[r * ld_a + it * 16 + lr];
-            acc = mfma_f32(a, b, acc);
-        }
-        const int i = it * 16 + lr;
-        if (i < K) {
+        for (int q = 0; q < RT; ++q)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int o = ot * 16 + lg * 4 + j;
-                if (o < N) gW[(size_t)o * K + i] = acc[j];
+                const int s = 4 * q + j;
+                a0[s] = ap0[(16 * q + j) * ld_z]; b0[s] = bp0[(16 * q + j) * ld_a];
+                a1[s] = ap1[(16 * q + j) * ld_z]; b1[s] = bp1[(16 * q + j) * ld_a];
             }
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+        for (int s = 0; s < RT * 4; ++s) {
+            acc0 = mfma_f32(a0[s], b0[s], acc0);
+            acc1 = mfma_f32(a1[s], b1[s], acc1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const int i0 = it0 * 16 + lr, i1 = it1 * 16 + lr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int o0 = ot0 * 16 + lg * 4 + j, o1 = ot1 * 16 + lg * 4 + j;
+            if (i0 < K && o0 < N) gW[o0 * K + i0] = acc0[j];
+            if (has1 && i1 < K && o1 < N) gW[o1 * K + i1] = acc1[j];
         }
     }
-    // bias gradient: column sums of dZ
     for (int o = threadIdx.x; o < N; o += FL_THREADS) {
-        float sacc = 0.f;
-#pragma unroll 8
-        for (int r = 0; r < RT * 16; ++r) sacc += dz[r * ld_z + o];
-        gb[o] = sacc;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int r = 0; r < RT * 16; r += 2) {
+            s0 += dz[r * ld_z + o];
+            s1 += dz[(r + 1) * ld_z + o];
+        }
+        gb[o] = s0 + s1;
     }
 }
 
-// Stage R rows of X (zero-padded to ld columns and beyond n_rows) into LDS.
 template <int RT>
 __device__ void stage_rows(const float* __restrict__ X, int n_rows, int F, int row0, float* xs, int ld) {
     for (int e = threadIdx.x; e < RT * 16 * ld; e += FL_THREADS) {
         const int r = e / ld, c = e - r * ld;
         const int row = row0 + r;
-        xs[e] = (row < n_rows && c < F) ? X[(size_t)row * F + c] : 0.f;
+        const bool ok = row < n_rows && c < F;
+        const float v = X[(size_t)(ok ? row : 0) * F + (ok ? c : 0)];  // unpredicated load
+        xs[e] = ok ? v : 0.f;
     }
 }
 
+// The global parameter image is bit-identical to the LDS image: one float4 copy.
+__device__ __forceinline__ void stage_image(const MLPDesc& d, const float* __restrict__ params, float* li) {
+    const float4* src = reinterpret_cast<const float4*>(params);
+    float4* dst = reinterpret_cast<float4*>(li);
+    const int n4 = d.Pimg >> 2;
+    for (int e = threadIdx.x; e < n4; e += FL_THREADS) dst[e] = src[e];
+}
+
 template <int RT>
-__device__ void forward_block(const MLPDesc& d, const float* __restrict__ params, float* lds) {
+__device__ void forward_block(const MLPDesc& d, float* acts, const float* li, unsigned long long* dbg = nullptr) {
     for (int l = 0; l < d.L; ++l) {
-        fwd_layer<RT>(params + d.w_off[l], params + d.b_off[l], d.dim[l], d.dim[l + 1],
-                      lds + d.act_off[l], d.ld[l], lds + d.act_off[l + 1], d.ld[l + 1], l + 1 < d.L);
-        __syncthreads();
+        if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
+        const int K = d.dim[l], N = d.dim[l + 1];
+        const float* w = li + d.iw_off[l];
+        const float* bias = li + d.ib_off[l];
+        if (l + 1 == d.L && RT * 16 * N <= 128)
+            fwd_head_valu<RT>(w, fl_ldw(K), bias, K, N, acts + d.act_off[l], d.ld[l], acts + d.act_off[l + 1],
+                              d.ld[l + 1]);
+        else
+            fwd_layer_mfma<RT>(w, fl_ldw(K), bias, K, N, acts + d.act_off[l], d.ld[l], acts + d.act_off[l + 1],
+                               d.ld[l + 1], l + 1 < d.L);
+        lds_barrier();
     }
 }
 
@@ -183,56 +302,71 @@ __device__ __forceinline__ float wave_sum(float v) {
 // ---------------------------------------------------------------------------------------
 // Metrics + early stopping on the device (reference C:85-90, C:165-195).
 // ---------------------------------------------------------------------------------------
-__device__ void metrics_from_cm(const float* cm, int C, double out[4]) {
+
+// Accuracy + weighted precision / recall / F1 (zero_division=0) of a confusion matrix given
+// by an accessor cmv(t, p) (sklearn semantics, fedmi/fl/metrics.py).  No local arrays: the
+// accessor is re-read per class so nothing spills to scratch.
+template <typename CM>
+__device__ void metrics_from_cm(CM cmv, int C, double out[4]) {
     double total = 0, tp_sum = 0;
-    double support[FL_MAX_CLASSES], pred[FL_MAX_CLASSES];
-    for (int t = 0; t < C; ++t) { support[t] = 0; pred[t] = 0; }
     for (int t = 0; t < C; ++t)
         for (int p = 0; p < C; ++p) {
-            const double x = (double)cm[t * C + p];
-            support[t] += x; pred[p] += x; total += x;
+            const double x = cmv(t, p);
+            total += x;
+            if (t == p) tp_sum += x;
         }
-    for (int t = 0; t < C; ++t) tp_sum += (double)cm[t * C + t];
     if (total <= 0) { out[0] = out[1] = out[2] = out[3] = 0; return; }
     double prec = 0, rec = 0, f1 = 0;
     for (int t = 0; t < C; ++t) {
-        const double tp = (double)cm[t * C + t];
-        const double w = support[t] / total;
-        const double pc = pred[t] > 0 ? tp / pred[t] : 0.0;
-        const double rc = support[t] > 0 ? tp / support[t] : 0.0;
-        const double den = 2 * tp + (pred[t] - tp) + (support[t] - tp);
+        double support = 0, pred = 0;
+        for (int p = 0; p < C; ++p) { support += cmv(t, p); pred += cmv(p, t); }
+        const double tp = cmv(t, t);
+        const double w = support / total;
+        const double pc = pred > 0 ? tp / pred : 0.0;
+        const double rc = support > 0 ? tp / support : 0.0;
+        const double den = 2 * tp + (pred - tp) + (support - tp);
         const double fc = den > 0 ? 2 * tp / den : 0.0;
         prec += w * pc; rec += w * rc; f1 += w * fc;
     }
     out[0] = tp_sum / total; out[1] = prec; out[2] = rec; out[3] = f1;
 }
 
-// Fold the previous round's all-reduced tails into the state; returns the new state.
-// Called redundantly by every workgroup (identical inputs -> identical decision); only
-// the caller passed write_hist=true stores history.
+// Fold the previous round's all-reduced tails into the state.  Executed by one full wave:
+// lane k computes client k's metrics, lane 0 combines them in rank order (the reference's
+// np.mean order) and applies the early-stop rule.  Returns the new state in lane 0.
 __device__ FLState finalize_state(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                                   const float* pg, FLState S, bool write_hist) {
+    const int lane = threadIdx.x & 63;
     if (!S.stopped && S.next_round > S.finalized) {
         const int r = S.next_round - 1;
         const int C = d.dim[d.L];
+        const float* tails = pg + c.tail_off;
+        double mk[4] = {0, 0, 0, 0};
+        double lk = 0;
+        if (lane < c.world) {
+            const float* cm = tails + lane * c.tail_stride;
+            metrics_from_cm([&](int t, int p) { return (double)cm[t * C + p]; }, C, mk);
+            lk = (double)cm[C * C];
+            if (write_hist && r < c.max_rounds)
+                for (int q = 0; q < 4; ++q) b.hist_rank[((size_t)r * c.world + lane) * 4 + q] = mk[q];
+        }
         double mean[4] = {0, 0, 0, 0};
-        float pooled[FL_MAX_CLASSES * FL_MAX_CLASSES];
-        for (int e = 0; e < C * C; ++e) pooled[e] = 0.f;
         double loss = 0;
         for (int k = 0; k < c.world; ++k) {
-            const float* cm = pg + c.tail_off + k * c.tail_stride;
-            double mk[4];
-            metrics_from_cm(cm, C, mk);
-            for (int e = 0; e < C * C; ++e) pooled[e] += cm[e];
-            loss += (double)cm[C * C];
-            for (int q = 0; q < 4; ++q) mean[q] += mk[q];
-            if (write_hist && r < c.max_rounds)
-                for (int q = 0; q < 4; ++q) b.hist_rank[((size_t)r * c.world + k) * 4 + q] = mk[q];
+            for (int q = 0; q < 4; ++q) mean[q] += __shfl(mk[q], k, 64);
+            loss += __shfl(lk, k, 64);
         }
+        if (lane != 0) return S;
         if (c.metric_mode == 0) {
             for (int q = 0; q < 4; ++q) mean[q] /= (double)c.world;
         } else {
-            metrics_from_cm(pooled, C, mean);
+            metrics_from_cm(
+                [&](int t, int p) {
+                    double x = 0;
+                    for (int k = 0; k < c.world; ++k) x += (double)tails[k * c.tail_stride + t * C + p];
+                    return x;
+                },
+                C, mean);
         }
         if (write_hist && r < c.max_rounds) {
             for (int q = 0; q < 4; ++q) b.hist_global[(size_t)r * 4 + q] = mean[q];
@@ -266,40 +400,49 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
                 const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ FLState S_sh;
-    if (threadIdx.x == 0) {
+    FL_STAMP(0);
+    if (b.dbg != nullptr && threadIdx.x == 0) b.dbg[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x < 64) {  // wave 0: round bookkeeping while the other waves stage
         FLState S0 = *st_in;
         if (local_step == 0) {
             S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
-            S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-            if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
-            if (blockIdx.x == 0) *st_out = S0;
+            if (threadIdx.x == 0) {
+                S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
+                if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
+                if (blockIdx.x == 0) *st_out = S0;
+            }
         }
-        S_sh = S0;
+        if (threadIdx.x == 0) S_sh = S0;
     }
-    __syncthreads();
-    const FLState S = S_sh;
-    if (!S.live) return;
-    // local_step > 0: train from the in-progress local weights
     const float* params = (local_step == 0) ? pg : b.local;
     const int R = RT * 16;
     const int row0 = blockIdx.x * R;
     const int L = d.L;
+    float* acts = lds;
+    float* li = lds + d.img_lds;
+    // staging does not depend on the state: it overlaps the finalize above
+    // labels are needed only after the forward pass: issue the load now
+    const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
+    stage_image(d, params, li);
+    stage_rows<RT>(b.X, c.n_rows, d.dim[0], row0, acts + d.act_off[0], d.ld[0]);
+    lds_barrier();
+    FL_STAMP(1);
+    if (!S_sh.live) return;
     float* slab = b.slab + (size_t)blockIdx.x * c.slab_stride;
-
-    stage_rows<RT>(b.X, c.n_rows, d.dim[0], row0, lds + d.act_off[0], d.ld[0]);
-    __syncthreads();
-    forward_block<RT>(d, params, lds);
+    forward_block<RT>(d, acts, li, b.dbg);
+    FL_STAMP(2);
+    if (b.dbg != nullptr && threadIdx.x == 0) b.dbg[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
 
     // softmax cross-entropy (mean over the local shard): dZ = (softmax - onehot) / n
     const int C = d.dim[L];
-    float* z = lds + d.act_off[L];
+    float* z = acts + d.act_off[L];
     const int ldz = d.ld[L];
     float lossv = 0.f;
     if (threadIdx.x < R) {
         const int r = threadIdx.x, row = row0 + r;
         float* zr = z + r * ldz;
         if (row < c.n_rows) {
-            const int y = b.y[row];
+            const int y = ylab;
             float mx = zr[0];
             for (int k = 1; k < C; ++k) mx = fmaxf(mx, zr[k]);
             float se = 0.f;
@@ -315,84 +458,129 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
         }
         for (int k = C; k < ((C + 15) & ~15); ++k) zr[k] = 0.f;
     }
-    lossv = wave_sum(lossv);
-    __syncthreads();
+    if (threadIdx.x < 64) {
+        lossv = wave_sum(lossv);
+        if (threadIdx.x == 0) slab[d.P] = lossv;  // R <= 64: wave 0 holds every row
+    }
+    lds_barrier();
+    FL_STAMP(3);
 
     // backward, top layer first: wgrad of layer l needs dZ_{l+1} and act_l, then dgrad
     // overwrites act_l with dH_l = (dZ_{l+1} W_l) * relu'(act_l).
     for (int l = L - 1; l >= 0; --l) {
-        const float* dz = lds + d.act_off[l + 1];
-        float* act = lds + d.act_off[l];
-        wgrad_layer<RT>(d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act, d.ld[l],
-                        slab + d.w_off[l], slab + d.b_off[l]);
-        __syncthreads();
+        const float* dz = acts + d.act_off[l + 1];
+        float* act = acts + d.act_off[l];
+        wgrad_layer<RT>(d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act, d.ld[l], slab + d.w_off[l],
+                        slab + d.b_off[l]);
+        FL_STAMP(4 + 2 * (L - 1 - l));
         if (l > 0) {
-            dgrad_layer<RT>(params + d.w_off[l], d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act, d.ld[l]);
-            __syncthreads();
+            // dgrad rewrites act_l, which wgrad above reads: barrier first
+            lds_barrier();
+            dgrad_layer<RT>(li + d.iw_off[l], fl_ldw(d.dim[l]), d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act,
+                            d.ld[l]);
+            lds_barrier();
+            FL_STAMP(5 + 2 * (L - 1 - l));
         }
     }
-    if (threadIdx.x == 0) slab[d.P] = lossv;  // wave 0 holds every valid row (R <= 64)
+    FL_STAMP(15);
 }
 
-// Deterministic slab reduction + Adam + StepLR + FedAvg pre-scale.  One thread per
-// element of the comm buffer [P params | world * tail_stride].
-__global__ void __launch_bounds__(256)
+// Slab reduction + Adam + StepLR + FedAvg pre-scale over the parameter image.  Block = 16
+// waves x 64 image entries: wave w sums slabs w, w+16, ... of the matching dense gradient
+// column, the 16 partials are combined in a fixed order (deterministic), then wave 0
+// applies Adam.  Image padding stays exactly 0.  The last block writes this rank's tail.
+#define ADAM_WAVES 16
+__global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
                const FLState* __restrict__ st, int local_step) {
+    __shared__ float part[ADAM_WAVES][64];
     const int last_local_step = (local_step == c.local_steps - 1);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int total = d.P + c.tail_len;
-    if (i >= total) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nparam_blocks = (d.Pimg + 63) / 64;
     const FLState S = *st;
-    if (!S.live) {
-        // past the stop: contribute the (identical on all ranks) global weights from rank 0
-        // only, so the all-reduce returns them bit-exactly.
-        if (last_local_step) comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
+    if (blockIdx.x >= nparam_blocks) {
+        // tail block: this rank's confusion slots are zeroed (fl_eval accumulates into
+        // them), its loss slot gets the summed per-block CE partials
+        for (int j = threadIdx.x; j < c.tail_len; j += blockDim.x) {
+            const int i = d.Pimg + j;
+            if (!S.live) {
+                if (last_local_step) comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
+                continue;
+            }
+            if (!last_local_step) continue;
+            const int k = j / c.tail_stride, e = j - k * c.tail_stride;
+            float val = 0.f;
+            if (k == c.rank && e == c.tail_stride - 1)
+                for (int s = 0; s < c.n_slabs; ++s) val += b.slab[(size_t)s * c.slab_stride + d.P];
+            comm[i] = val;
+        }
         return;
     }
-    if (i < d.P) {
-        float g = 0.f;
-        const float* sp = b.slab + i;
-        int k = 0;
-        for (; k + 4 <= c.n_slabs; k += 4) {
-            const float g0 = sp[(size_t)(k + 0) * c.slab_stride];
-            const float g1 = sp[(size_t)(k + 1) * c.slab_stride];
-            const float g2 = sp[(size_t)(k + 2) * c.slab_stride];
-            const float g3 = sp[(size_t)(k + 3) * c.slab_stride];
+    const int j = blockIdx.x * 64 + lane;  // image index
+    if (!S.live) {
+        // past the stop: rank 0 contributes the (identical) global weights, others 0, so the
+        // all-reduce returns them bit-exactly
+        if (wave == 0 && j < d.Pimg && last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
+        return;
+    }
+    // image index -> dense index (or padding)
+    int di = -1;
+    if (j < d.Pimg) {
+        int l = 0;
+        while (l + 1 < d.L && j >= d.iw_off[l + 1]) ++l;
+        const int K = d.dim[l], N = d.dim[l + 1];
+        if (j < d.ib_off[l]) {
+            const int e = j - d.iw_off[l], ldw = fl_ldw(K);
+            const int n = e / ldw, k = e - n * ldw;
+            if (n < N && k < K) di = d.w_off[l] + n * K + k;
+        } else {
+            const int n = j - d.ib_off[l];
+            if (n < N) di = d.b_off[l] + n;
+        }
+    }
+    float g = 0.f;
+    if (di >= 0) {
+        const float* sp = b.slab + di;
+        int s = wave;
+        for (; s + 3 * ADAM_WAVES < c.n_slabs; s += 4 * ADAM_WAVES) {
+            const float g0 = sp[(size_t)(s)*c.slab_stride];
+            const float g1 = sp[(size_t)(s + ADAM_WAVES) * c.slab_stride];
+            const float g2 = sp[(size_t)(s + 2 * ADAM_WAVES) * c.slab_stride];
+            const float g3 = sp[(size_t)(s + 3 * ADAM_WAVES) * c.slab_stride];
             g += g0; g += g1; g += g2; g += g3;
         }
-        for (; k < c.n_slabs; ++k) g += sp[(size_t)k * c.slab_stride];
-        float p = pin[i];
-        if (c.weight_decay != 0.f) g += c.weight_decay * p;
-        if (c.prox_mu != 0.f) g += c.prox_mu * (p - anchor[i]);
-        // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
-        // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
-        // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
-        const int t = S.cur_round * c.local_steps + local_step + 1;
-        const double lr = c.lr0 * pow(c.gamma, (double)(S.cur_round / c.step_size));
-        const float step_size = (float)(lr / (1.0 - pow(c.beta1, (double)t)));
-        const float bc2_sqrt = (float)sqrt(1.0 - pow(c.beta2, (double)t));
-        float m = b.m[i], v = b.v[i];
-        m = m + c.omb1 * (g - m);
-        v = v * c.beta2f + c.omb2 * g * g;
-        const float denom = sqrtf(v) / bc2_sqrt + c.eps;
-        p = p + (-step_size) * (m / denom);
-        b.m[i] = m; b.v[i] = v;
-        b.local[i] = p;
-        if (last_local_step) comm[i] = p * c.agg_scale;
-    } else if (last_local_step) {
-        // per-rank tail: zero confusion slots (fl_eval accumulates into ours), loss slot
-        const int j = i - d.P;
-        const int k = j / c.tail_stride, e = j - k * c.tail_stride;
-        float val = 0.f;
-        if (k == c.rank && e == c.tail_stride - 1) {
-            float l = 0.f;
-            for (int s = 0; s < c.n_slabs; ++s) l += b.slab[(size_t)s * c.slab_stride + d.P];
-            val = l;
-        }
-        comm[i] = val;
+        for (; s < c.n_slabs; s += ADAM_WAVES) g += sp[(size_t)s * c.slab_stride];
     }
+    part[wave][lane] = g;
+    lds_barrier();
+    if (wave != 0 || j >= d.Pimg) return;
+    if (di < 0) {  // padding: keep the published image padding exactly 0
+        if (last_local_step) comm[j] = 0.f;
+        return;
+    }
+    g = 0.f;
+#pragma unroll
+    for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
+    float p = pin[j];
+    if (c.weight_decay != 0.f) g += c.weight_decay * p;
+    if (c.prox_mu != 0.f) g += c.prox_mu * (p - anchor[j]);
+    // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
+    // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
+    // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
+    const int t = S.cur_round * c.local_steps + local_step + 1;
+    const double lr = c.lr0 * pow(c.gamma, (double)(S.cur_round / c.step_size));
+    const float step_size = (float)(lr / (1.0 - pow(c.beta1, (double)t)));
+    const float bc2_sqrt = (float)sqrt(1.0 - pow(c.beta2, (double)t));
+    float m = b.m[j], v = b.v[j];
+    m = m + c.omb1 * (g - m);
+    v = v * c.beta2f + c.omb2 * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + c.eps;
+    p = p + (-step_size) * (m / denom);
+    b.m[j] = m;
+    b.v[j] = v;
+    b.local[j] = p;
+    if (last_local_step) comm[j] = p * c.agg_scale;
 }
 
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,
@@ -407,30 +595,40 @@ fl_eval_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ par
     const int R = RT * 16;
     const int row0 = blockIdx.x * R;
     const int C = d.dim[d.L];
+    float* acts = lds;
+    float* li = lds + d.img_lds;
+    FL_STAMP(0);
     for (int e = threadIdx.x; e < C * C; e += FL_THREADS) cm_s[e] = 0;
-    stage_rows<RT>(b.X, c.n_rows, d.dim[0], row0, lds + d.act_off[0], d.ld[0]);
-    __syncthreads();
-    forward_block<RT>(d, params, lds);
+    // labels are needed only after the forward pass: issue the load now
+    const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
+    stage_image(d, params, li);
+    stage_rows<RT>(b.X, c.n_rows, d.dim[0], row0, acts + d.act_off[0], d.ld[0]);
+    lds_barrier();
+    FL_STAMP(1);
+    forward_block<RT>(d, acts, li);
+    FL_STAMP(2);
     if (threadIdx.x < R) {
         const int r = threadIdx.x, row = row0 + r;
         if (row < c.n_rows) {
-            const float* zr = lds + d.act_off[d.L] + r * d.ld[d.L];
+            const float* zr = acts + d.act_off[d.L] + r * d.ld[d.L];
             int best = 0;
             float bv = zr[0];
             for (int k = 1; k < C; ++k)
                 if (zr[k] > bv) { bv = zr[k]; best = k; }
-            atomicAdd(&cm_s[b.y[row] * C + best], 1);
+            atomicAdd(&cm_s[ylab * C + best], 1);
         }
     }
-    __syncthreads();
+    lds_barrier();
     for (int e = threadIdx.x; e < C * C; e += FL_THREADS)
         if (cm_s[e]) atomicAdd(&cm_out[e], (float)cm_s[e]);
+    FL_STAMP(15);
 }
 
 __global__ void fl_finalize_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                                    const FLState* __restrict__ st_in, FLState* __restrict__ st_out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (blockIdx.x != 0) return;
     FLState S = finalize_state(d, c, b, pg, *st_in, true);
+    if (threadIdx.x != 0) return;
     S.live = 0;
     *st_out = S;
 }
@@ -469,26 +667,20 @@ __global__ void fl_synth_kernel(float* __restrict__ X, int* __restrict__ y, long
     const uint64_t gid = row_offset + (uint64_t)row;
     float x[32];
     const int cards[8] = {7, 16, 7, 14, 6, 5, 2, 40};
-    for (int f = 0; f < F; f += 4) {
-        const uint4 r4 = philox4x32(gid, (uint32_t)(f >> 2), seed);
-        const uint32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
-        for (int q = 0; q < 4 && f + q < F; ++q) {
-            const int col = f + q;
-            const uint4 r2 = philox4x32(gid, 0x10000u + (uint32_t)col, seed);
-            const float u1 = u01(rr[q]), u2 = u01(r2.x);
-            const float g = sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853f * u2);
-            float val;
-            if (col < 6) {
-                val = g;
-            } else {
-                const int card = cards[(col - 6) & 7];
-                const float code = floorf(u01(r2.y) * card);
-                const float mean = 0.5f * (card - 1), sd = sqrtf((card * card - 1) / 12.f);
-                val = (code - mean) / sd;
-            }
-            x[col] = val;
-            X[(size_t)row * F + col] = val;
+    for (int col = 0; col < F; ++col) {
+        const uint4 r2 = philox4x32(gid, (uint32_t)col, seed);
+        const float u1 = u01(r2.x), u2 = u01(r2.y);
+        float val;
+        if (col < 6) {
+            val = sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2);
+        } else {
+            const int card = cards[(col - 6) & 7];
+            const float code = floorf(u01(r2.z) * card);
+            const float mean = 0.5f * (card - 1), sd = sqrtf((card * card - 1) / 12.f);
+            val = (code - mean) / sd;
         }
+        x[col] = val;
+        X[(size_t)row * F + col] = val;
     }
     float score = 0.f;
     for (int h = 0; h < H; ++h) {
@@ -503,12 +695,13 @@ __global__ void fl_synth_kernel(float* __restrict__ X, int* __restrict__ y, long
 // Launchers
 // ---------------------------------------------------------------------------------------
 static inline int nblocks(int n, int R) { return (n + R - 1) / R; }
+static inline size_t lds_bytes(const MLPDesc& d) { return (size_t)d.lds_floats * sizeof(float); }
 
 template <int RT>
 static hipError_t launch_train_rt(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                                   const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s) {
-    const size_t lds = (size_t)d.lds_floats * sizeof(float);
-    hipLaunchKernelGGL(fl_train_kernel<RT>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, c, b, pg, si, so, ls);
+    hipLaunchKernelGGL(fl_train_kernel<RT>, dim3(c.n_slabs), dim3(FL_THREADS), lds_bytes(d), s, d, c, b, pg, si,
+                       so, ls);
     return hipGetLastError();
 }
 
@@ -517,25 +710,23 @@ hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers&
     switch (c.R) {
         case 16: return launch_train_rt<1>(d, c, b, pg, si, so, ls, s);
         case 32: return launch_train_rt<2>(d, c, b, pg, si, so, ls, s);
-        case 64: return launch_train_rt<4>(d, c, b, pg, si, so, ls, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
                           const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s) {
-    const int total = d.P + c.tail_len;
-    hipLaunchKernelGGL(fl_adam_kernel, dim3((total + 255) / 256), dim3(256), 0, s, d, c, b, pin, anchor,
-                       comm, st, local_step);
+    const int blocks = (d.Pimg + 63) / 64 + 1;
+    hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
+                       local_step);
     return hipGetLastError();
 }
 
 template <int RT>
 static hipError_t launch_eval_rt(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* params,
                                  float* cm, const FLState* st, hipStream_t s) {
-    const size_t lds = (size_t)d.lds_floats * sizeof(float);
-    hipLaunchKernelGGL(fl_eval_kernel<RT>, dim3(nblocks(c.n_rows, RT * 16)), dim3(FL_THREADS), lds, s, d, c, b,
-                       params, cm, st);
+    hipLaunchKernelGGL(fl_eval_kernel<RT>, dim3(nblocks(c.n_rows, RT * 16)), dim3(FL_THREADS), lds_bytes(d), s, d,
+                       c, b, params, cm, st);
     return hipGetLastError();
 }
 
@@ -545,7 +736,6 @@ hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
     switch (c.R) {
         case 16: return launch_eval_rt<1>(d, c, b, params, cm, st, s);
         case 32: return launch_eval_rt<2>(d, c, b, params, cm, st, s);
-        case 64: return launch_eval_rt<4>(d, c, b, params, cm, st, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -559,13 +749,14 @@ hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffe
 hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const int* y, int n_rows,
                                const float* params, float* cm_out, hipStream_t s) {
     FLConfig c = {};
-    c.R = R; c.n_rows = n_rows;
+    c.R = R;
+    c.n_rows = n_rows;
     FLBuffers b = {};
-    b.X = X; b.y = y;
+    b.X = X;
+    b.y = y;
     switch (R) {
         case 16: return launch_eval_rt<1>(d, c, b, params, cm_out, nullptr, s);
         case 32: return launch_eval_rt<2>(d, c, b, params, cm_out, nullptr, s);
-        case 64: return launch_eval_rt<4>(d, c, b, params, cm_out, nullptr, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -583,11 +774,13 @@ hipError_t fl_launch_synth(float* X, int* y, long long n, int F, unsigned long l
 // Allow the LDS-resident kernels to request more than the default dynamic-LDS window
 // (gfx950 has 160 KiB per CU).
 hipError_t fl_set_lds_limit(size_t bytes) {
-    const int b = (int)bytes + 1024;
+    const int b = (int)bytes;
     hipError_t e = hipSuccess;
-#define FL_SET(fn) if (e == hipSuccess) e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, b)
-    FL_SET(fl_train_kernel<1>); FL_SET(fl_train_kernel<2>); FL_SET(fl_train_kernel<4>);
-    FL_SET(fl_eval_kernel<1>); FL_SET(fl_eval_kernel<2>); FL_SET(fl_eval_kernel<4>);
+#define FL_SET(fn)                                                                                      \
+    if (e == hipSuccess)                                                                                \
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, b)
+    FL_SET(fl_train_kernel<1>); FL_SET(fl_train_kernel<2>);
+    FL_SET(fl_eval_kernel<1>); FL_SET(fl_eval_kernel<2>);
 #undef FL_SET
     return e;
 }

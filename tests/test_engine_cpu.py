@@ -1,0 +1,91 @@
+"""TorchRoundEngine (CPU path) vs a literal transcription of the reference [C] client."""
+import numpy as np
+import pytest
+import torch
+
+from fedmi.data.synthetic import make_income_like
+from fedmi.fl.engine import EngineConfig, TorchRoundEngine
+from fedmi.fl.metrics import confusion_matrix, metrics_from_confusion
+from fedmi.models.mlp import (MLPModel, dense_to_image, dict_to_flat, flat_to_dict, image_layout,
+                              image_to_dense, init_flat, param_count, param_layout)
+
+from .reference_oracle import RefClient, fedavg
+
+
+def test_param_layout_matches_reference_named_parameters():
+    from .reference_oracle import RefMLP
+    dims = [14, 50, 200, 2]
+    ref = RefMLP(14, [50, 200], 2)
+    names = [(n, tuple(p.shape)) for n, p in ref.named_parameters()]
+    assert names == [(n, s) for n, s, _ in param_layout(dims)]
+    assert param_count(dims) == 11352 == sum(p.numel() for p in ref.parameters())
+    m = MLPModel(14, [50, 200], 2)
+    assert [n for n, _ in m.named_parameters()] == [n for n, _ in names]
+    # params are views of the flat buffer
+    m.flat.zero_()
+    assert all(float(p.abs().sum()) == 0 for p in m.parameters())
+
+
+@pytest.mark.parametrize("dims", [[14, 50, 200, 2], [14, 7, 3], [5, 33, 17, 9, 4]])
+def test_image_roundtrip(dims):
+    f = init_flat(dims, 3)
+    img = dense_to_image(f, dims)
+    assert img.size == image_layout(dims)[2] and img.size % 4 == 0
+    np.testing.assert_array_equal(image_to_dense(img, dims), f)
+    assert abs(img.sum() - f.sum()) < 1e-3   # padding is zero
+
+
+def test_dict_flat_roundtrip():
+    dims = [14, 50, 200, 2]
+    f = init_flat(dims, 1)
+    np.testing.assert_array_equal(dict_to_flat(flat_to_dict(f, dims), dims), f)
+
+
+def test_single_client_rounds_match_reference():
+    X, y = make_income_like(600, seed=2)
+    dims = [14, 50, 200, 2]
+    flat = init_flat(dims, 0)
+    cfg = EngineConfig(max_rounds=40, early_stop=False)
+    eng = TorchRoundEngine(X, y, 2, cfg, None, flat)
+    ref = RefClient(X, y, [50, 200], 2, flat)
+    for r in range(40):
+        eng.run(1)
+        ref.train_one_epoch()
+        cm = confusion_matrix(y, ref.predictions(), 2)
+        np.testing.assert_allclose(eng.hist.glob[r], list(metrics_from_confusion(cm).values()), atol=1e-12)
+    np.testing.assert_allclose(eng.global_flat(), dict_to_flat(ref.get_weights(), dims), rtol=1e-5, atol=1e-6)
+
+
+def test_fedavg_arithmetic_matches_reference_formula():
+    dims = [14, 8, 2]
+    rng = np.random.RandomState(0)
+    ws = [flat_to_dict(rng.randn(param_count(dims)).astype(np.float32), dims) for _ in range(3)]
+    sizes = [100, 250, 57]
+    ref = dict_to_flat(fedavg(ws, sizes), dims)
+    ours = sum(dict_to_flat(w, dims) * (n / sum(sizes)) for w, n in zip(ws, sizes))
+    np.testing.assert_allclose(ours, ref, rtol=1e-6, atol=1e-7)
+
+
+def test_early_stop_and_lr_schedule_on_real_data():
+    from fedmi.data.tabular import load_tabular
+    ds = load_tabular()
+    dims = [14, 50, 200, 2]
+    eng = TorchRoundEngine(ds.X_train, ds.y_train, 2, EngineConfig(max_rounds=300), None, init_flat(dims, 0))
+    eng.run(300)
+    h = eng.history()
+    assert 120 < h["rounds_run"] < 300 and h["stop_round"] == h["rounds_run"]
+    acc = h["global"][:, 0]
+    assert acc[-1] > 0.82
+    # StepLR(30, 0.5) stepped per round (C:46, C:73)
+    assert abs(eng.optimizer.param_groups[0]["lr"] - 0.004 * 0.5 ** (h["rounds_run"] // 30)) < 1e-12
+
+
+def test_fedprox_local_steps_changes_trajectory():
+    X, y = make_income_like(300, seed=4)
+    dims = [14, 16, 2]
+    a = TorchRoundEngine(X, y, 2, EngineConfig(hidden=(16,), local_steps=3, max_rounds=5, early_stop=False),
+                         None, init_flat(dims, 0))
+    b = TorchRoundEngine(X, y, 2, EngineConfig(hidden=(16,), local_steps=3, prox_mu=0.5, max_rounds=5,
+                                               early_stop=False), None, init_flat(dims, 0))
+    a.run(5); b.run(5)
+    assert not np.allclose(a.global_flat(), b.global_flat())

@@ -1,0 +1,76 @@
+"""BASELINE config 1: multi-client FedAvg on CPU over gloo (world_size 2 and 3)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, rounds, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    torch.set_num_threads(1)
+    from fedmi.data.tabular import load_tabular
+    from fedmi.fl.engine import EngineConfig
+    from fedmi.fl.trainer import FederatedMLPLearning
+    from fedmi.models.mlp import dict_to_flat
+    from fedmi.parallel.comm import Comm
+    comm = Comm(backend="gloo", device="cpu")
+    ds = load_tabular()
+    cfg = EngineConfig(max_rounds=rounds)
+    tr = FederatedMLPLearning(ds.X_train, ds.y_train, comm.rank, comm.size, comm=comm, config=cfg,
+                              mode="correct", backend="torch")
+    # one round step by step (reference API) ...
+    tr.train_one_epoch()
+    local_after = dict_to_flat(tr.get_weights(), tr.engine.dims)
+    m = tr.evaluate_local()
+    tr.federated_averaging(comm)
+    g1 = tr.engine.global_flat()
+    # ... then the fused loop
+    gm = tr.train_and_evaluate(comm, rounds=rounds - 1, verbose=False)
+    test = tr.evaluate_global(ds.X_test, ds.y_test, comm)
+    q.put((rank, len(tr.X_local), local_after, m, g1, tr.engine.global_flat(), gm, test,
+           tr.history()["per_rank"]))
+    comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fedavg_over_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 6, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sizes = [r[1] for r in res]
+    assert sum(sizes) == 8000                       # disjoint IID shards ('correct' mode)
+    # round-1 global = sample-size-weighted mean of the post-step local weights (C:110-116)
+    expect = sum(r[2] * (n / sum(sizes)) for r, n in zip(res, sizes))
+    for r in res:
+        np.testing.assert_allclose(r[4], expect, rtol=1e-5, atol=1e-6)
+    # all ranks end with bit-identical global weights and identical metric histories
+    for r in res[1:]:
+        np.testing.assert_array_equal(r[5], res[0][5])
+        assert r[6] == res[0][6]
+        assert r[7] == res[0][7]
+    # global metrics are the unweighted mean of per-rank local metrics (C:169, Q3)
+    per_rank = res[0][8]
+    np.testing.assert_allclose(np.array(res[0][6]["accuracy"]), per_rank[:, :, 0].mean(axis=1), atol=1e-12)
+    # the per-rank metrics of round 1 match each rank's own evaluate_local()
+    for k, r in enumerate(res):
+        assert abs(per_rank[0, k, 0] - r[3]["accuracy"]) < 1e-12
+    assert res[0][7]["accuracy"] > 0.6

@@ -1,0 +1,41 @@
+"""Per-phase in-kernel timing (s_memrealtime stamps, 10 ns ticks) of the fused kernels.
+
+Train-kernel slots: 0 start, 1 staged, 10+l start of forward layer l, 2 forward done,
+3 CE done, 4.. backward phases, 15 end; 13/14 = s_memtime (core clock) at start / after
+forward, used to report the effective shader clock."""
+import sys, numpy as np, torch
+sys.path.insert(0, ".")
+from fedmi.data.synthetic import make_income_like
+from fedmi.fl.engine import EngineConfig, HipRoundEngine
+from fedmi.models.mlp import init_flat
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 8000
+R = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+hidden = tuple(int(h) for h in sys.argv[3].split(",")) if len(sys.argv) > 3 else (50, 200)
+X, y = make_income_like(rows, seed=1)
+cfg = EngineConfig(hidden=hidden, max_rounds=100, rows_per_block=R, graph_rounds=0, early_stop=False)
+e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *hidden, 2], 0))
+e.run(3)
+nb = (rows + R - 1) // R
+dbg = torch.zeros(nb * 16, dtype=torch.int64, device=e.device)
+order = [0, 1, 10, 11, 12, 2, 3, 4, 5, 6, 7, 8, 9, 15]
+for which, name in ((0, "train"), (2, "eval")):
+    for rep in range(5):
+        dbg.zero_()
+        e.engine.set_debug(dbg.data_ptr())
+        e.engine.launch_one(e.rounds_issued - 1, which, e._stream())
+        e.stream.synchronize()
+        e.engine.set_debug(0)
+    st = dbg.view(nb, 16).cpu().numpy().astype(np.int64)
+    t0 = st[:, 0].min()
+    print(f"{name}: blocks={nb} dispatch spread={(st[:,0].max()-t0)*10/1000:.2f}us "
+          f"total={(st[:,15].max()-t0)*10/1000:.2f}us")
+    if which == 0 and (st[:, 13] > 0).all():
+        cyc = st[:, 14] - st[:, 13]
+        real = (st[:, 2] - st[:, 0]) * 10e-9
+        print(f"   effective shader clock over start..forward: {np.median(cyc / real) / 1e9:.2f} GHz")
+    cols = [i for i in order if (st[:, i] > 0).all()]
+    prev = cols[0]
+    for c in cols[1:]:
+        d = (st[:, c] - st[:, prev]) * 10 / 1000
+        print(f"   phase {prev:2d}->{c:2d}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
+        prev = c
