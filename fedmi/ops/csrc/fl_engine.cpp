@@ -40,6 +40,7 @@ namespace py = pybind11;
     } while (0)
 
 hipError_t fl_set_lds_limit(size_t bytes);  // fl_kernels.hip
+void register_trainer(pybind11::module_& m);  // mlp_trainer.cpp
 
 static inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 template <typename T>
@@ -424,4 +425,5 @@ PYBIND11_MODULE(_fedmi_hip, m) {
     m.def("synth", &synth);
     m.def("device_info", &device_info);
     m.attr("STATE_BYTES") = (int)sizeof(FLState);
+    register_trainer(m);
 }

@@ -1,0 +1,294 @@
+// Native minibatch trainer for T packed MLPs of one architecture (layered path).
+//
+// Serves the scikit-learn-compatible estimator (FL_SkLearn_MLPClassifier_Limitation.py:77-101,
+// hyperparameters_tuning.py:90-91) and the hyperparameter sweep with trial packing: the 9
+// learning rates of one hidden-layer config train together, sharing every minibatch.  One
+// epoch = ceil(n/B) minibatch steps; each step is
+//   gather -> L fused fwd GEMMs (bias+ReLU) -> loss head -> per layer: wgrad GEMM + bias
+//   colsum + dgrad GEMM (ReLU mask) -> step counter -> Adam (+L2 loss term)
+// and the epoch ends with the sklearn tol / n_iter_no_change rule evaluated on the device
+// per trial.  An epoch is captured once into a hipGraph and replayed (the epoch's row
+// permutation is selected by a device counter), so the host issues one launch per epoch.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "gemm_mfma.h"
+#include "mlp_ops.h"
+
+namespace py = pybind11;
+
+#define TR_CHECK(expr)                                                                         \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                                     " at " #expr);                                            \
+    } while (0)
+
+template <typename T>
+static inline T* ptr_of(py::dict& d, const char* k) {
+    return reinterpret_cast<T*>(d[k].cast<uintptr_t>());
+}
+
+class MLPTrainer {
+  public:
+    MLPTrainer(std::vector<int> dims, int T, py::dict cfg, py::dict bufs) : dims_(dims), T_(T) {
+        L_ = (int)dims.size() - 1;
+        if (L_ < 1) throw std::runtime_error("MLPTrainer: need >= 1 layer");
+        int off = 0;
+        for (int l = 0; l < L_; ++l) {
+            w_off_.push_back(off);
+            off += dims[l] * dims[l + 1];
+            b_off_.push_back(off);
+            off += dims[l + 1];
+        }
+        P_ = off;
+        n_ = cfg["n_rows"].cast<int>();
+        B_ = cfg["batch"].cast<int>();
+        head_ = cfg["head"].cast<int>();
+        style_ = cfg["style"].cast<int>();
+        beta1_ = cfg["beta1"].cast<double>();
+        beta2_ = cfg["beta2"].cast<double>();
+        eps_ = cfg["eps"].cast<double>();
+        alpha_ = cfg["alpha"].cast<double>();
+        wd_ = cfg["weight_decay"].cast<double>();
+        mu_ = cfg["mu"].cast<double>();
+        tol_ = cfg["tol"].cast<double>();
+        nic_ = cfg["n_iter_no_change"].cast<int>();
+        max_iter_ = cfg["max_iter"].cast<int>();
+        tol_stop_ = cfg["tol_stop"].cast<int>();
+        X_ = ptr_of<const float>(bufs, "X");
+        y_ = ptr_of<const int>(bufs, "y");
+        perms_ = ptr_of<const int>(bufs, "perms");
+        epoch_ctr_ = ptr_of<int>(bufs, "epoch_ctr");
+        params_ = ptr_of<float>(bufs, "params");
+        grads_ = ptr_of<float>(bufs, "grads");
+        m_ = ptr_of<float>(bufs, "m");
+        v_ = ptr_of<float>(bufs, "v");
+        anchor_ = ptr_of<const float>(bufs, "anchor");
+        wd_mask_ = ptr_of<const unsigned char>(bufs, "wd_mask");
+        lr_ = ptr_of<const double>(bufs, "lr");
+        step_ = ptr_of<long long>(bufs, "step");
+        loss_acc_ = ptr_of<double>(bufs, "loss_acc");
+        best_ = ptr_of<double>(bufs, "best");
+        count_ = ptr_of<int>(bufs, "count");
+        n_iter_ = ptr_of<int>(bufs, "n_iter");
+        active_ = ptr_of<int>(bufs, "active");
+        curve_ = ptr_of<double>(bufs, "curve");
+        xb_ = ptr_of<float>(bufs, "xb");
+        yb_ = ptr_of<int>(bufs, "yb");
+        acts_ = ptr_of<float>(bufs, "acts");    // [L][T][B][maxw]
+        deltas_ = ptr_of<float>(bufs, "deltas");
+        maxw_ = cfg["maxw"].cast<int>();
+    }
+    ~MLPTrainer() { drop_graph(); }
+
+    int P() const { return P_; }
+
+    // One minibatch step on rows perm[epoch][off : off+rows].
+    void step(int off, int rows, hipStream_t s) {
+        GatherArgs ga{X_, dims_[0], y_, perms_, epoch_ctr_, (long long)n_, off, rows, dims_[0], xb_, dims_[0],
+                      nullptr, yb_};
+        TR_CHECK(gather_rows_launch(ga, s));
+        forward(xb_, rows, s, acts_, /*Bstride*/ B_);
+        // loss head
+        const int C = dims_[L_];
+        XentArgs xa{};
+        xa.z = act(L_ - 1); xa.ldz = maxw_; xa.sZ = (long long)B_ * maxw_;
+        xa.y = yb_; xa.idx = nullptr; xa.M = rows; xa.C = C; xa.mode = head_;
+        xa.scale = 1.f / (float)rows;
+        xa.dz = delta(L_ - 1); xa.lddz = maxw_; xa.sDz = (long long)B_ * maxw_;
+        xa.loss_acc = loss_acc_; xa.pred = nullptr; xa.active = active_;
+        TR_CHECK(xent_launch(xa, T_, s));
+        // backward
+        for (int l = L_ - 1; l >= 0; --l) {
+            const int K = dims_[l], N = dims_[l + 1];
+            const float* in = l == 0 ? xb_ : act(l - 1);
+            const long long s_in = l == 0 ? 0 : (long long)B_ * maxw_;
+            const int ld_in = l == 0 ? dims_[0] : maxw_;
+            // wgrad: dW[N][K] = dZ^T (rows x N) . in (rows x K)
+            GemmArgs g{};
+            g.M = N; g.N = K; g.K = rows;
+            g.A = delta(l); g.lda = maxw_; g.sA = (long long)B_ * maxw_;
+            g.B = in; g.ldb = ld_in; g.sB = s_in;
+            g.C = grads_ + w_off_[l]; g.ldc = K; g.sC = P_;
+            g.alpha = 1.f; g.beta = 0.f; g.active = active_;
+            TR_CHECK(gemm_launch(g, 0, 0, 0, GEMM_EPI_NONE, 1, T_, s));
+            TR_CHECK(colsum_launch(delta(l), rows, N, maxw_, grads_ + b_off_[l], 0.f, T_, (long long)B_ * maxw_, P_,
+                                   active_, s));
+            if (l > 0) {
+                // dgrad: dIn[rows][K] = dZ . W[N][K], masked by in > 0 (ReLU)
+                GemmArgs d{};
+                d.M = rows; d.N = K; d.K = N;
+                d.A = delta(l); d.lda = maxw_; d.sA = (long long)B_ * maxw_;
+                d.B = params_ + w_off_[l]; d.ldb = K; d.sB = P_;
+                d.C = delta(l - 1); d.ldc = maxw_; d.sC = (long long)B_ * maxw_;
+                d.mask = act(l - 1); d.ldmask = maxw_; d.sMask = (long long)B_ * maxw_;
+                d.alpha = 1.f; d.beta = 0.f; d.active = active_;
+                TR_CHECK(gemm_launch(d, 0, 1, 0, GEMM_EPI_MASK, 1, T_, s));
+            }
+        }
+        TR_CHECK(step_count_launch(step_, active_, T_, s));
+        AdamArgs aa{};
+        aa.p = params_; aa.m = m_; aa.v = v_; aa.g = grads_; aa.anchor = anchor_; aa.wd_mask = wd_mask_;
+        aa.n = (size_t)P_; aa.style = style_; aa.lr = lr_; aa.beta1 = beta1_; aa.beta2 = beta2_; aa.eps = eps_;
+        // sklearn: coef grads (dW + alpha*W)/batch; torch: weight_decay * p
+        aa.wd = style_ == 1 ? alpha_ / (double)rows : wd_;
+        aa.mu = mu_; aa.step = step_; aa.loss_acc = loss_acc_;
+        aa.l2_coef = style_ == 1 ? 0.5 * alpha_ : 0.0;
+        aa.active = active_; aa.p_bf16 = nullptr;
+        TR_CHECK(adam_launch(aa, T_, s));
+    }
+
+    void epoch(hipStream_t s) {
+        for (int off = 0; off < n_; off += B_) step(off, std::min(B_, n_ - off), s);
+        EpochArgs ea{T_, epoch_ctr_, loss_acc_, best_, count_, n_iter_, active_, curve_, (long long)n_, tol_, nic_,
+                     max_iter_, tol_stop_};
+        TR_CHECK(epoch_end_launch(ea, s));
+    }
+
+    // Run up to n_epochs epochs (graph-replayed), polling the active flags every
+    // `check_every` epochs; returns epochs issued.
+    int run(int n_epochs, uintptr_t stream, int check_every, bool use_graph) {
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        std::vector<int> act(T_);
+        int done = 0;
+        while (done < n_epochs) {
+            const int chunk = std::min(check_every, n_epochs - done);
+            for (int e = 0; e < chunk; ++e) {
+                if (use_graph) {
+                    if (!exec_) capture(s);
+                    TR_CHECK(hipGraphLaunch(exec_, s));
+                } else {
+                    epoch(s);
+                }
+            }
+            done += chunk;
+            TR_CHECK(hipMemcpyAsync(act.data(), active_, sizeof(int) * T_, hipMemcpyDeviceToHost, s));
+            TR_CHECK(hipStreamSynchronize(s));
+            bool any = false;
+            for (int t = 0; t < T_; ++t) any = any || act[t] != 0;
+            if (!any) break;
+        }
+        return done;
+    }
+
+    // Forward pass of all trials over an arbitrary row block (evaluation / predict):
+    // logits of the last layer land in out [T][rows][ld = maxw].
+    void predict_logits(uintptr_t Xp, int rows, uintptr_t ws, uintptr_t stream) {
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        forward(reinterpret_cast<const float*>(Xp), rows, s, reinterpret_cast<float*>(ws), rows, /*gated*/ false);
+    }
+
+  private:
+    float* act(int l) const { return acts_ + (size_t)l * T_ * B_ * maxw_; }
+    float* delta(int l) const { return deltas_ + (size_t)l * T_ * B_ * maxw_; }
+
+    // acts layout [L][T][Bs][maxw]; x shared by all trials (row stride dims[0]).
+    void forward(const float* x, int rows, hipStream_t s, float* acts, int Bs, bool gated = true) {
+        for (int l = 0; l < L_; ++l) {
+            const int K = dims_[l], N = dims_[l + 1];
+            GemmArgs g{};
+            g.M = rows; g.N = N; g.K = K;
+            g.A = l == 0 ? x : acts + (size_t)(l - 1) * T_ * Bs * maxw_;
+            g.lda = l == 0 ? dims_[0] : maxw_;
+            g.sA = l == 0 ? 0 : (long long)Bs * maxw_;
+            g.B = params_ + w_off_[l]; g.ldb = K; g.sB = P_;
+            g.C = acts + (size_t)l * T_ * Bs * maxw_; g.ldc = maxw_; g.sC = (long long)Bs * maxw_;
+            g.bias = params_ + b_off_[l]; g.sBias = P_;
+            g.alpha = 1.f; g.beta = 0.f; g.active = gated ? active_ : nullptr;
+            TR_CHECK(gemm_launch(g, 0, 1, 1, l + 1 < L_ ? GEMM_EPI_BIAS_RELU : GEMM_EPI_BIAS, 1, T_, s));
+        }
+    }
+
+    void capture(hipStream_t s) {
+        drop_graph();
+        TR_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        try {
+            epoch(s);
+        } catch (...) {
+            hipGraph_t g;
+            hipStreamEndCapture(s, &g);
+            if (g) hipGraphDestroy(g);
+            throw;
+        }
+        TR_CHECK(hipStreamEndCapture(s, &graph_));
+        TR_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+    }
+    void drop_graph() {
+        if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
+        if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+    }
+
+    std::vector<int> dims_, w_off_, b_off_;
+    int T_, L_, P_, n_, B_, head_, style_, nic_, max_iter_, tol_stop_, maxw_;
+    double beta1_, beta2_, eps_, alpha_, wd_, mu_, tol_;
+    const float* X_;
+    const int* y_;
+    const int* perms_;
+    int* epoch_ctr_;
+    float *params_, *grads_, *m_, *v_;
+    const float* anchor_;
+    const unsigned char* wd_mask_;
+    const double* lr_;
+    long long* step_;
+    double *loss_acc_, *best_, *curve_;
+    int *count_, *n_iter_, *active_;
+    float* xb_;
+    int* yb_;
+    float *acts_, *deltas_;
+    hipGraph_t graph_ = nullptr;
+    hipGraphExec_t exec_ = nullptr;
+};
+
+// Standalone layered GEMM entry (tests, wide-MLP path): dtype 0 f32 / 1 bf16.
+static void gemm_py(int M, int N, int K, uintptr_t A, int lda, int a_kc, uintptr_t B, int ldb, int b_kc, uintptr_t C,
+                    int ldc, int epi, uintptr_t bias, uintptr_t mask, int ldmask, int mask_bf16, float alpha,
+                    float beta, int dtype, int splits, uintptr_t slab, uintptr_t Cbf16, uintptr_t stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = reinterpret_cast<const void*>(A); g.lda = lda;
+    g.B = reinterpret_cast<const void*>(B); g.ldb = ldb;
+    g.bias = reinterpret_cast<const float*>(bias);
+    g.mask = reinterpret_cast<const void*>(mask); g.ldmask = ldmask; g.mask_bf16 = mask_bf16;
+    g.alpha = alpha;
+    if (splits > 1) {
+        g.C = reinterpret_cast<float*>(slab); g.ldc = ldc; g.beta = 0.f;
+        g.slab_stride = (size_t)M * ldc;
+        TR_CHECK(gemm_launch(g, dtype, a_kc, b_kc, GEMM_EPI_NONE, splits, 1, s));
+        TR_CHECK(splitk_reduce_launch(reinterpret_cast<float*>(slab), (size_t)M * ldc, splits,
+                                      reinterpret_cast<float*>(C), (size_t)M * ldc, beta, s));
+    } else {
+        g.C = reinterpret_cast<float*>(C); g.ldc = ldc; g.beta = beta;
+        g.Cbf16 = reinterpret_cast<void*>(Cbf16);
+        TR_CHECK(gemm_launch(g, dtype, a_kc, b_kc, epi, 1, 1, s));
+    }
+}
+
+static void colsum_py(uintptr_t X, int M, int N, int ld, uintptr_t out, float beta, uintptr_t stream) {
+    TR_CHECK(colsum_launch(reinterpret_cast<const float*>(X), M, N, ld, reinterpret_cast<float*>(out), beta, 1, 0, 0,
+                           nullptr, reinterpret_cast<hipStream_t>(stream)));
+}
+
+static void to_bf16_py(uintptr_t x, uintptr_t y, size_t n, uintptr_t stream) {
+    TR_CHECK(f32_to_bf16_launch(reinterpret_cast<const float*>(x), reinterpret_cast<void*>(y), n,
+                                reinterpret_cast<hipStream_t>(stream)));
+}
+
+void register_trainer(py::module_& m) {
+    py::class_<MLPTrainer>(m, "MLPTrainer")
+        .def(py::init<std::vector<int>, int, py::dict, py::dict>())
+        .def("run", &MLPTrainer::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
+             py::arg("use_graph") = true)
+        .def("predict_logits", &MLPTrainer::predict_logits)
+        .def_property_readonly("P", &MLPTrainer::P);
+    m.def("gemm", &gemm_py);
+    m.def("colsum", &colsum_py);
+    m.def("to_bf16", &to_bf16_py);
+}

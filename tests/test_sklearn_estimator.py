@@ -1,0 +1,113 @@
+"""fedmi MLPClassifier vs scikit-learn (float64 numpy backend: algorithmic parity), the
+[S] limitation (Q8), warm-start fix, packed sweep semantics, and the HIP fp32 backend."""
+import warnings
+
+import numpy as np
+import pytest
+
+from fedmi.data.tabular import load_tabular
+from fedmi.models.sklearn_mlp import MLPClassifier, epoch_permutations, fit_packed
+
+sknn = pytest.importorskip("sklearn.neural_network")
+warnings.filterwarnings("ignore")
+
+
+@pytest.fixture(scope="module")
+def data():
+    ds = load_tabular(with_mean=False)
+    return ds.X_train[:1500], ds.y_train[:1500]
+
+
+@pytest.mark.parametrize("hl,mi", [((30,), 25), ((20, 40), 30), ((8, 8, 8), 20)])
+def test_numpy_backend_matches_sklearn(data, hl, mi):
+    X, y = data
+    a = sknn.MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=0.004, max_iter=mi, random_state=42).fit(X, y)
+    b = MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=0.004, max_iter=mi, random_state=42,
+                      backend="numpy").fit(X, y)
+    assert a.n_iter_ == b.n_iter_
+    for u, v in zip(a.coefs_ + a.intercepts_, b.coefs_ + b.intercepts_):
+        np.testing.assert_allclose(u, v, rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(a.loss_curve_, b.loss_curve_, rtol=1e-10)
+    assert (a.predict(X) == b.predict(X)).all()
+    np.testing.assert_allclose(a.predict_proba(X), b.predict_proba(X), atol=1e-9)
+
+
+def test_multiclass_and_tol_stop_match_sklearn():
+    rng = np.random.RandomState(0)
+    X = rng.randn(400, 5)
+    y = (X[:, 0] > 0).astype(int) + (X[:, 1] > 0.5).astype(int)     # 3 classes
+    a = sknn.MLPClassifier(hidden_layer_sizes=(16,), learning_rate_init=0.01, max_iter=500, tol=1e-3,
+                           random_state=3).fit(X, y)
+    b = MLPClassifier(hidden_layer_sizes=(16,), learning_rate_init=0.01, max_iter=500, tol=1e-3, random_state=3,
+                      backend="numpy").fit(X, y)
+    assert a.n_iter_ == b.n_iter_ < 500          # stopped by the tol / n_iter_no_change rule
+    np.testing.assert_allclose(a.loss_curve_, b.loss_curve_, rtol=1e-9)
+    assert list(a.classes_) == list(b.classes_)
+
+
+def test_partial_fit_then_fit_discards_weights_q8(data):
+    """The [S] limitation: fit() re-initialises, so weights set before it are lost."""
+    X, y = data
+    m = MLPClassifier(hidden_layer_sizes=(10,), max_iter=5, random_state=42, backend="numpy")
+    m.partial_fit(X, y, classes=np.unique(y))
+    m.fit(X, y)
+    ref = [c.copy() for c in m.coefs_]
+    m.coefs_ = [np.zeros_like(c) for c in m.coefs_]           # "apply global weights"
+    m.fit(X, y)
+    for u, v in zip(ref, m.coefs_):
+        np.testing.assert_array_equal(u, v)                     # identical: the averaged weights were discarded
+    w = MLPClassifier(hidden_layer_sizes=(10,), max_iter=5, random_state=42, warm_start=True, backend="numpy")
+    w.fit(X, y)
+    w.coefs_ = [np.zeros_like(c) for c in w.coefs_]
+    w.fit(X, y)
+    assert not all(np.array_equal(u, v) for u, v in zip(ref, w.coefs_))
+
+
+def test_epoch_permutations_follow_sklearn_rng():
+    rs = np.random.RandomState(42)
+    p = epoch_permutations(rs, 10, 3)
+    from sklearn.utils import shuffle
+    rs2 = np.random.RandomState(42)
+    idx = np.arange(10)
+    for e in range(3):
+        idx = shuffle(idx, random_state=rs2)
+        assert (p[e] == idx).all()
+
+
+def test_fit_packed_cpu_equals_individual(data):
+    X, y = data
+    lrs = [0.002, 0.01]
+    packed = [MLPClassifier(hidden_layer_sizes=(12,), learning_rate_init=lr, max_iter=8, random_state=42,
+                            backend="numpy") for lr in lrs]
+    fit_packed(packed, X, y)
+    for lr, e in zip(lrs, packed):
+        s = MLPClassifier(hidden_layer_sizes=(12,), learning_rate_init=lr, max_iter=8, random_state=42,
+                          backend="numpy").fit(X, y)
+        for u, v in zip(s.coefs_, e.coefs_):
+            np.testing.assert_array_equal(u, v)
+
+
+@pytest.mark.gpu
+def test_hip_backend_tracks_float64(data):
+    X, y = data
+    a = MLPClassifier(hidden_layer_sizes=(50, 100), learning_rate_init=0.004, max_iter=15, random_state=42,
+                      backend="numpy").fit(X, y)
+    b = MLPClassifier(hidden_layer_sizes=(50, 100), learning_rate_init=0.004, max_iter=15, random_state=42,
+                      backend="hip").fit(X, y)
+    assert b.n_iter_ == a.n_iter_
+    np.testing.assert_allclose(b.loss_curve_[:5], a.loss_curve_[:5], rtol=2e-4)
+    assert (a.predict(X) == b.predict(X)).mean() > 0.97
+
+
+@pytest.mark.gpu
+def test_hip_packed_equals_single(data):
+    X, y = data
+    lrs = [0.002, 0.005, 0.01]
+    packed = [MLPClassifier(hidden_layer_sizes=(32, 64), learning_rate_init=lr, max_iter=12, random_state=42,
+                            backend="hip") for lr in lrs]
+    fit_packed(packed, X, y)
+    single = MLPClassifier(hidden_layer_sizes=(32, 64), learning_rate_init=0.005, max_iter=12, random_state=42,
+                           backend="hip").fit(X, y)
+    for u, v in zip(single.coefs_, packed[1].coefs_):
+        np.testing.assert_allclose(u, v, rtol=1e-6, atol=1e-7)
+    assert packed[1].n_iter_ == single.n_iter_
