@@ -1,0 +1,178 @@
+"""Wide-MLP federated client (BASELINE config 3: MLP 14-4096-4096-4096-2 on large
+synthetic income-shaped shards, MFMA-GEMM bound).
+
+The fused round engine (``fedmi/fl/engine.py``) keeps a whole small MLP in one workgroup;
+a 33.6 M-parameter model does not fit, so this client runs the same round semantics
+(full-batch local Adam step(s) over the shard + StepLR, local eval, sample-weighted FedAvg)
+layer by layer on the grid-level MFMA GEMMs of ``fedmi/ops/csrc/gemm_mfma.hip``:
+
+* bf16 operands, fp32 accumulation, fp32 master weights / Adam state / gradients;
+* the shard is processed in micro-batches with gradient accumulation (beta = 1 in the
+  wgrad epilogue), which is exactly the full-batch gradient (row-wise scale-up);
+* FedAvg = one RCCL all-reduce per layer bucket of the pre-scaled (n_i / N) fp32 weights;
+  buckets are issued in backward order on a side stream as soon as that layer's Adam
+  update is done, so the all-reduce of the top layers overlaps the update / re-quantisation
+  of the lower ones.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..models.mlp import init_flat, param_layout
+
+
+class WideClient:
+    def __init__(self, X: torch.Tensor, y: torch.Tensor, dims: Sequence[int], comm=None, n_total: Optional[int] = None,
+                 micro_batch: int = 8192, lr: float = 0.004, betas=(0.9, 0.999), eps: float = 1e-8,
+                 step_size: int = 30, gamma: float = 0.5, seed: int = 0, dtype: str = "bf16",
+                 eval_rows: int = 0):
+        from ..ops import native
+        self.m = native()
+        self.dev = X.device
+        self.X, self.y = X.contiguous(), y.to(torch.int32).contiguous()
+        self.n = int(X.shape[0])
+        self.dims = [int(d) for d in dims]
+        self.L = len(self.dims) - 1
+        self.comm = comm
+        self.world = comm.size if comm is not None else 1
+        self.n_total = n_total or self.n * self.world
+        self.agg = self.n / self.n_total
+        self.mb = min(micro_batch, self.n)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.step_size, self.gamma = step_size, gamma
+        self.dtype = 1 if dtype == "bf16" else 0
+        self.eval_rows = eval_rows
+        f32 = dict(dtype=torch.float32, device=self.dev)
+        flat = torch.as_tensor(init_flat(self.dims, seed), **f32)
+        self.layout = param_layout(self.dims)
+        self.params = flat
+        self.grads = torch.zeros_like(flat)
+        self.m_ = torch.zeros_like(flat)
+        self.v_ = torch.zeros_like(flat)
+        self.W = [flat[off:off + int(np.prod(s))].view(*s) for n_, s, off in self.layout[0::2]]
+        self.b = [flat[off:off + int(np.prod(s))].view(*s) for n_, s, off in self.layout[1::2]]
+        self.gW = [self.grads[off:off + int(np.prod(s))].view(*s) for n_, s, off in self.layout[0::2]]
+        self.gb = [self.grads[off:off + int(np.prod(s))].view(*s) for n_, s, off in self.layout[1::2]]
+        gdt = torch.bfloat16 if self.dtype else torch.float32
+        self.Wq = [torch.empty(w.shape, dtype=gdt, device=self.dev) for w in self.W]
+        # activations of one micro-batch: fp32 (masks / loss) + GEMM-operand copies
+        self.h = [torch.empty(self.mb, d, **f32) for d in self.dims[1:]]
+        self.hq = [torch.empty(self.mb, d, dtype=gdt, device=self.dev) for d in self.dims[1:]]
+        self.xq = torch.empty(self.mb, self.dims[0], dtype=gdt, device=self.dev)
+        self.dz = [torch.empty(self.mb, d, **f32) for d in self.dims[1:]]
+        self.dzq = [torch.empty(self.mb, d, dtype=gdt, device=self.dev) for d in self.dims[1:]]
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.dev)
+        self.lr_t = torch.zeros(1, dtype=torch.float64, device=self.dev)
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.round = 0
+        self.stream = torch.cuda.Stream(device=self.dev)
+        self.comm_stream = torch.cuda.Stream(device=self.dev)
+        self._quantize()
+
+    # ------------------------------------------------------------------
+    def _s(self) -> int:
+        return self.stream.cuda_stream
+
+    def _quantize(self):
+        with torch.cuda.stream(self.stream):
+            for w, q in zip(self.W, self.Wq):
+                if self.dtype:
+                    self.m.to_bf16(w.data_ptr(), q.data_ptr(), w.numel(), self._s())
+                else:
+                    q.copy_(w)
+
+    def _forward(self, r0: int, rows: int):
+        m, s = self.m, self._s()
+        x = self.X[r0:r0 + rows]
+        if self.dtype:
+            m.to_bf16(x.data_ptr(), self.xq.data_ptr(), x.numel(), s)
+            inp, ld_in = self.xq, self.dims[0]
+        else:
+            inp, ld_in = x, self.dims[0]
+        for l in range(self.L):
+            K, N = self.dims[l], self.dims[l + 1]
+            epi = 2 if l + 1 < self.L else 1
+            m.gemm(rows, N, K, inp.data_ptr(), ld_in, 1, self.Wq[l].data_ptr(), K, 1, self.h[l].data_ptr(), N, epi,
+                   self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0,
+                   self.hq[l].data_ptr() if self.dtype else 0, s)
+            inp, ld_in = (self.hq[l] if self.dtype else self.h[l]), N
+
+    def local_step(self):
+        """One full-batch Adam step over the whole shard (micro-batched accumulation)."""
+        m, s = self.m, self._s()
+        C = self.dims[-1]
+        with torch.cuda.stream(self.stream):
+            self.loss_acc.zero_()
+            for r0 in range(0, self.n, self.mb):
+                rows = min(self.mb, self.n - r0)
+                self._forward(r0, rows)
+                # loss head: softmax CE, dZ = (p - onehot) / n (full-batch mean)
+                self.m.xent(self.h[-1].data_ptr(), C, self.y[r0:].data_ptr(), rows, C, 0, 1.0 / self.n,
+                            self.dz[-1].data_ptr(), C, self.loss_acc.data_ptr(), s)
+                beta = 0.0 if r0 == 0 else 1.0
+                for l in range(self.L - 1, -1, -1):
+                    K, N = self.dims[l], self.dims[l + 1]
+                    dzl = self.dz[l]
+                    if self.dtype:
+                        m.to_bf16(dzl.data_ptr(), self.dzq[l].data_ptr(), rows * N, s)
+                        dq = self.dzq[l]
+                    else:
+                        dq = dzl
+                    if l == 0:
+                        inp = self.xq if self.dtype else self.X[r0:r0 + rows]
+                    else:
+                        inp = self.hq[l - 1] if self.dtype else self.h[l - 1]
+                    # wgrad (+= over micro-batches): dW[N][K] = dZ^T . in
+                    m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), K, 0, self.gW[l].data_ptr(), K, 0, 0, 0,
+                           0, 0, 1.0, beta, self.dtype, 1, 0, 0, s)
+                    m.colsum(dzl.data_ptr(), rows, N, N, self.gb[l].data_ptr(), beta, s)
+                    if l > 0:
+                        # dgrad with the ReLU mask of the layer input
+                        m.gemm(rows, K, N, dq.data_ptr(), N, 1, self.Wq[l].data_ptr(), K, 0, self.dz[l - 1].data_ptr(),
+                               K, 3, 0, self.h[l - 1].data_ptr(), K, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
+            # torch Adam + StepLR (scalars computed on host: the schedule is known)
+            t = self.round + 1
+            lr = self.lr * self.gamma ** (self.round // self.step_size)
+            self.m.adam_flat(self.params.data_ptr(), self.m_.data_ptr(), self.v_.data_ptr(), self.grads.data_ptr(),
+                             self.params.numel(), lr, self.betas[0], self.betas[1], self.eps, t, s)
+
+    def aggregate(self):
+        """Sample-size-weighted FedAvg: scale by n_i/N, all-reduce per layer bucket (top
+        layer first) on the comm stream, then refresh the bf16 operand copies."""
+        if self.world > 1:
+            self.comm_stream.wait_stream(self.stream)
+            with torch.cuda.stream(self.comm_stream):
+                for (name, shape, off), (bn, bs, boff) in reversed(list(zip(self.layout[0::2], self.layout[1::2]))):
+                    seg = self.params[off:boff + int(np.prod(bs))]
+                    seg.mul_(self.agg)
+                    self.comm.allreduce_(seg)
+            self.stream.wait_stream(self.comm_stream)
+        self._quantize()
+
+    def evaluate(self) -> float:
+        rows = min(self.eval_rows or self.mb, self.n, self.mb)
+        with torch.cuda.stream(self.stream):
+            self._forward(0, rows)
+            pred = self.h[-1][:rows].argmax(dim=1)
+            acc = (pred == self.y[:rows].long()).float().mean()
+        self.stream.synchronize()
+        return float(acc)
+
+    def run_round(self, evaluate: bool = False) -> Optional[float]:
+        self.local_step()
+        acc = self.evaluate() if evaluate else None
+        self.aggregate()
+        self.round += 1
+        return acc
+
+    def loss(self) -> float:
+        self.stream.synchronize()
+        return float(self.loss_acc.item()) / self.n
+
+    @property
+    def flops_per_round(self) -> float:
+        macs = sum(a * b for a, b in zip(self.dims[:-1], self.dims[1:]))
+        return 6.0 * self.n * macs

@@ -46,6 +46,8 @@ struct AdamArgs {
     double l2_coef;                // sklearn: 0.5 * alpha
     const int* active;
     void* p_bf16;                  // optional bf16 shadow [T][n]
+    double lr_scalar;              // used when lr == nullptr
+    long long step_scalar;         // used when step == nullptr
 };
 
 struct EpochArgs {

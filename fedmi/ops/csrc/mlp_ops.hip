@@ -94,8 +94,8 @@ adam_kernel(AdamArgs a) {
             if (a.wd != 0.0) g += (float)a.wd * p;
         }
         if (a.mu != 0.0) g += (float)a.mu * (p - a.anchor[j]);
-        const long long step = a.step[t];
-        const double lr = a.lr[t];
+        const long long step = a.step != nullptr ? a.step[t] : a.step_scalar;
+        const double lr = a.lr != nullptr ? a.lr[t] : a.lr_scalar;
         float m = a.m[j], v = a.v[j];
         if (a.style == 0) {
             m = m + (float)(1.0 - a.beta1) * (g - m);

@@ -281,7 +281,29 @@ static void to_bf16_py(uintptr_t x, uintptr_t y, size_t n, uintptr_t stream) {
                                 reinterpret_cast<hipStream_t>(stream)));
 }
 
+// Single-problem loss head (wide path): softmax CE (mode 0) / sklearn binary (mode 1).
+static void xent_py(uintptr_t z, int ldz, uintptr_t y, int M, int C, int mode, float scale, uintptr_t dz, int lddz,
+                    uintptr_t loss_acc, uintptr_t stream) {
+    XentArgs a{};
+    a.z = reinterpret_cast<const float*>(z); a.ldz = ldz; a.y = reinterpret_cast<const int*>(y);
+    a.M = M; a.C = C; a.mode = mode; a.scale = scale;
+    a.dz = reinterpret_cast<float*>(dz); a.lddz = lddz; a.loss_acc = reinterpret_cast<double*>(loss_acc);
+    TR_CHECK(xent_launch(a, 1, reinterpret_cast<hipStream_t>(stream)));
+}
+
+// Single-problem torch-style Adam over a flat fp32 vector (host-side lr / step).
+static void adam_flat_py(uintptr_t p, uintptr_t m, uintptr_t v, uintptr_t g, size_t n, double lr, double b1, double b2,
+                         double eps, long long t, uintptr_t stream) {
+    AdamArgs a{};
+    a.p = reinterpret_cast<float*>(p); a.m = reinterpret_cast<float*>(m); a.v = reinterpret_cast<float*>(v);
+    a.g = reinterpret_cast<const float*>(g); a.n = n; a.style = 0; a.beta1 = b1; a.beta2 = b2; a.eps = eps;
+    a.lr_scalar = lr; a.step_scalar = t;
+    TR_CHECK(adam_launch(a, 1, reinterpret_cast<hipStream_t>(stream)));
+}
+
 void register_trainer(py::module_& m) {
+    m.def("xent", &xent_py);
+    m.def("adam_flat", &adam_flat_py);
     py::class_<MLPTrainer>(m, "MLPTrainer")
         .def(py::init<std::vector<int>, int, py::dict, py::dict>())
         .def("run", &MLPTrainer::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,

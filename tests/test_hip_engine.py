@@ -1,0 +1,188 @@
+"""HIP kernels of the fused round engine and the layered path vs torch fp32 references."""
+import numpy as np
+import pytest
+import torch
+
+from fedmi.data.synthetic import make_income_like
+from fedmi.fl.early_stop import EarlyStopper
+from fedmi.fl.engine import EngineConfig, HipRoundEngine, TorchRoundEngine
+from fedmi.models.mlp import init_flat
+
+pytestmark = pytest.mark.gpu
+
+DIMS = [14, 50, 200, 2]
+
+
+@pytest.fixture(scope="module")
+def shard():
+    return make_income_like(3000, seed=5)
+
+
+def test_native_extension_loaded():
+    from fedmi.ops import native
+    m = native(build_if_missing=False)
+    assert m.__file__.endswith(".so") and "fedmi/ops" in m.__file__
+    info = m.device_info(0)
+    assert "gfx950" in info["arch"]
+
+
+@pytest.mark.parametrize("R", [16, 32])
+@pytest.mark.parametrize("hidden", [(50, 200), (7,), (33, 17, 9)])
+def test_round_matches_torch(shard, R, hidden):
+    X, y = shard
+    dims = [14, *hidden, 2]
+    flat = init_flat(dims, 1)
+    cfg = EngineConfig(hidden=hidden, max_rounds=20, rows_per_block=R, graph_rounds=0, early_stop=False)
+    hip = HipRoundEngine(X, y, 2, cfg, None, flat)
+    ref = TorchRoundEngine(X, y, 2, cfg, None, flat)
+    hip.run(3)
+    ref.run(3)
+    a, b = hip.global_flat(), ref.global_flat()
+    assert np.abs(a - b).max() / np.abs(b).max() < 2e-5
+    np.testing.assert_allclose(hip.history()["global"], ref.history()["global"], atol=2e-3)
+    np.testing.assert_allclose(hip.history()["loss"], ref.history()["loss"], rtol=1e-4)
+
+
+def test_graph_replay_bitwise_equals_eager(shard):
+    X, y = shard
+    flat = init_flat(DIMS, 2)
+    out = []
+    for g in (0, 8):
+        cfg = EngineConfig(max_rounds=40, graph_rounds=g, early_stop=False)
+        e = HipRoundEngine(X, y, 2, cfg, None, flat)
+        e.run(33)
+        out.append((e.global_flat(), e.history()["global"]))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+def test_device_early_stop_rule_matches_host_rule():
+    from fedmi.data.tabular import load_tabular
+    ds = load_tabular()
+    e = HipRoundEngine(ds.X_train, ds.y_train, 2, EngineConfig(max_rounds=300), None, init_flat(DIMS, 0))
+    e.run(300)
+    h = e.history()
+    assert 100 < h["rounds_run"] < 300 and h["stop_round"] == h["rounds_run"]
+    es = EarlyStopper(10, 1e-4)
+    stop = None
+    for r, v in enumerate(h["global"]):
+        if es.update(v):
+            stop = r + 1
+            break
+    assert stop == h["stop_round"]
+    assert h["global"][-1][0] > 0.82
+
+
+def test_step_api_equals_fused(shard):
+    X, y = shard
+    flat = init_flat(DIMS, 3)
+    cfg = EngineConfig(max_rounds=10, graph_rounds=0, early_stop=False)
+    a = HipRoundEngine(X, y, 2, cfg, None, flat)
+    b = HipRoundEngine(X, y, 2, cfg, None, flat)
+    a.run(4)
+    for _ in range(4):
+        b.step_train()
+        cm = b.step_eval()
+        assert cm.sum() == len(X)
+        b.step_aggregate()
+    b.sync_history()
+    np.testing.assert_array_equal(a.global_flat(), b.global_flat())
+
+
+def test_confusion_eval_matches_torch(shard):
+    X, y = shard
+    flat = init_flat(DIMS, 4)
+    hip = HipRoundEngine(X, y, 2, EngineConfig(max_rounds=4), None, flat)
+    ref = TorchRoundEngine(X, y, 2, EngineConfig(max_rounds=4), None, flat)
+    Xt, yt = make_income_like(777, seed=9)
+    np.testing.assert_array_equal(hip.confusion(Xt, yt, flat=flat), ref.confusion(Xt, yt, flat=flat))
+
+
+def test_local_steps_and_fedprox_match_torch(shard):
+    X, y = shard
+    dims = [14, 16, 2]
+    flat = init_flat(dims, 5)
+    cfg = EngineConfig(hidden=(16,), local_steps=3, prox_mu=0.3, max_rounds=5, early_stop=False, graph_rounds=0)
+    hip = HipRoundEngine(X, y, 2, cfg, None, flat)
+    ref = TorchRoundEngine(X, y, 2, cfg, None, flat)
+    hip.run(3)
+    ref.run(3)
+    a, b = hip.global_flat(), ref.global_flat()
+    assert np.abs(a - b).max() / np.abs(b).max() < 2e-5
+
+
+def test_synthetic_device_generator():
+    from fedmi.ops import native
+    from fedmi.data.synthetic import teacher_weights
+    m = native()
+    dev = torch.device("cuda", 0)
+    n = 200_000
+    X = torch.empty(n, 14, device=dev)
+    yv = torch.empty(n, dtype=torch.int32, device=dev)
+    w1, w2 = teacher_weights()
+    Xs, _ = make_income_like(4096, seed=123)
+    th = float(np.median(np.maximum(Xs @ w1.T, 0.0) @ w2))
+    tw1 = torch.as_tensor(w1, device=dev)
+    tw2 = torch.as_tensor(np.append(w2, th).astype(np.float32), device=dev)
+    m.synth(X.data_ptr(), yv.data_ptr(), n, 14, 7, 0, tw1.data_ptr(), tw2.data_ptr(), w1.shape[0],
+            torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    Xc = X.cpu().numpy()
+    assert np.isfinite(Xc).all()
+    assert abs(Xc[:, :6].mean()) < 0.02 and abs(Xc[:, :6].std() - 1) < 0.02
+    assert 0.35 < yv.float().mean().item() < 0.65
+
+
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_layered_gemm_variants(dtype):
+    from fedmi.ops import native
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(0)
+    M, N, K = 130, 70, 300
+    for epi in (0, 1, 2, 3):
+        for akc, bkc in ((1, 1), (1, 0), (0, 0), (0, 1)):
+            if epi == 3 and not akc:
+                continue
+            Af = torch.randn(M, K, device=dev) if akc else torch.randn(K, M, device=dev)
+            Bf = torch.randn(N, K, device=dev) if bkc else torch.randn(K, N, device=dev)
+            At, Bt = (Af if akc else Af.t()), (Bf.t() if bkc else Bf)
+            bias, mask = torch.randn(N, device=dev), torch.randn(M, N, device=dev)
+            C = torch.zeros(M, N, device=dev)
+            cast = (lambda t: t) if dtype == 0 else (lambda t: t.to(torch.bfloat16))
+            Ain, Bin = cast(Af), cast(Bf)
+            m.gemm(M, N, K, Ain.data_ptr(), Af.shape[1], akc, Bin.data_ptr(), Bf.shape[1], bkc, C.data_ptr(), N,
+                   epi, bias.data_ptr(), mask.data_ptr(), N, 0, 1.0, 0.0, dtype, 1, 0, 0, s)
+            ref = (cast(At).float().double() @ cast(Bt).float().double()).float()
+            if epi in (1, 2):
+                ref = ref + bias
+            if epi == 2:
+                ref = ref.clamp_min(0)
+            if epi == 3:
+                ref = ref * (mask > 0)
+            torch.cuda.synchronize()
+            tol = 5e-6 if dtype == 0 else 1e-2
+            assert ((C - ref).abs().max() / ref.abs().max()).item() < tol
+
+
+def test_wide_client_fp32_matches_torch():
+    from fedmi.fl.wide import WideClient
+    dev = torch.device("cuda", 0)
+    X, y = make_income_like(1500, seed=0)
+    Xt, yt = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
+    c = WideClient(Xt, yt, [14, 64, 48, 2], micro_batch=512, dtype="fp32")
+    ref = torch.nn.Sequential(torch.nn.Linear(14, 64), torch.nn.ReLU(), torch.nn.Linear(64, 48), torch.nn.ReLU(),
+                              torch.nn.Linear(48, 2)).to(dev)
+    with torch.no_grad():
+        for p, w in zip(ref.parameters(), [c.W[0], c.b[0], c.W[1], c.b[1], c.W[2], c.b[2]]):
+            p.copy_(w)
+    opt = torch.optim.Adam(ref.parameters(), lr=0.004)
+    for _ in range(3):
+        c.run_round()
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(Xt), yt.long()).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    flat_ref = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    assert ((c.params - flat_ref).abs().max() / flat_ref.abs().max()).item() < 1e-4
