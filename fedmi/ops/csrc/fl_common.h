@@ -32,6 +32,7 @@ struct MLPDesc {
     int dim[FL_MAX_LAYERS + 1];       // dim[0] = features, dim[L] = classes
     int ld[FL_MAX_LAYERS + 1];        // LDS leading dimension (floats) per activation buffer
     int act_off[FL_MAX_LAYERS + 1];   // LDS float offset of each activation buffer (R rows)
+    int dlt_off[FL_MAX_LAYERS + 1];   // LDS float offset of the backward delta of hidden layer l
     int w_off[FL_MAX_LAYERS];         // dense (reference) offset of W_l
     int b_off[FL_MAX_LAYERS];         // dense offset of b_l
     int P;                            // dense parameter count

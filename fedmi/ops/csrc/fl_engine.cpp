@@ -152,6 +152,11 @@ class FLEngine {
             lds += c_.R * d_.ld[l];
             lds = (lds + 3) & ~3;
         }
+        for (int l = 1; l < L; ++l) {  // backward deltas of the hidden layers
+            d_.dlt_off[l] = lds;
+            lds += c_.R * d_.ld[l];
+            lds = (lds + 3) & ~3;
+        }
         d_.img_lds = lds;
         lds += d_.Pimg;
         d_.lds_floats = lds;

@@ -148,12 +148,14 @@ __device__ void fwd_head_valu(const float* w, int ldw, const float* bias, int K,
     }
 }
 
-// dH[r][i] = (sum_o dZ[r][o] W[o][i]) * (act[r][i] > 0), in place over act.
-// Item = 16-column tile of dH (all R rows); B fragment W[o][i] reused across the RT rows.
+// dH[r][i] = (sum_o dZ[r][o] W[o][i]) * (act[r][i] > 0) -> out (separate buffer, so the
+// same phase can run the layer's wgrad, which reads act).  Item = 16-column tile of dH (all
+// R rows); B fragment W[o][i] reused across the RT rows.  Items are handed out from the
+// LAST wave down, so they pair with the wgrad tiles handed out from wave 0 up.
 template <int RT>
-__device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* dz, int ld_z, float* act,
-                            int ld_a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* dz, int ld_z, const float* act,
+                            int ld_a, float* out) {
+    const int wave = (FL_WAVES - 1) - (threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     const int itiles = (K + 15) >> 4;
     const int ochunks = (N + 15) >> 4;
@@ -194,9 +196,8 @@ __device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* 
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                float* p = act + (rt * 16 + lg * 4 + j) * ld_a + i;
-                const float a = *p;
-                *p = (ivalid && a > 0.f) ? acc[rt][j] : 0.f;
+                const int o = (rt * 16 + lg * 4 + j) * ld_a + i;
+                out[o] = (ivalid && act[o] > 0.f) ? acc[rt][j] : 0.f;
             }
     }
 }
@@ -465,31 +466,30 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
     lds_barrier();
     FL_STAMP(3);
 
-    // backward, top layer first: wgrad of layer l needs dZ_{l+1} and act_l, then dgrad
-    // overwrites act_l with dH_l = (dZ_{l+1} W_l) * relu'(act_l).
+    // backward, top layer first, ONE phase per layer: wgrad_l (reads dZ_{l+1}, act_l) and
+    // dgrad_l (reads dZ_{l+1}, W_l, act_l; writes dH_l into its own buffer) are independent.
     for (int l = L - 1; l >= 0; --l) {
-        const float* dz = acts + d.act_off[l + 1];
-        float* act = acts + d.act_off[l];
+        const float* dz = (l == L - 1) ? acts + d.act_off[L] : acts + d.dlt_off[l + 1];
+        const float* act = acts + d.act_off[l];
         wgrad_layer<RT>(d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act, d.ld[l], slab + d.w_off[l],
                         slab + d.b_off[l]);
-        FL_STAMP(4 + 2 * (L - 1 - l));
-        if (l > 0) {
-            // dgrad rewrites act_l, which wgrad above reads: barrier first
-            lds_barrier();
+        if (l > 0)
             dgrad_layer<RT>(li + d.iw_off[l], fl_ldw(d.dim[l]), d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act,
-                            d.ld[l]);
-            lds_barrier();
-            FL_STAMP(5 + 2 * (L - 1 - l));
-        }
+                            d.ld[l], acts + d.dlt_off[l]);
+        lds_barrier();
+        FL_STAMP(4 + (L - 1 - l));
     }
     FL_STAMP(15);
 }
 
-// Slab reduction + Adam + StepLR + FedAvg pre-scale over the parameter image.  Block = 16
-// waves x 64 image entries: wave w sums slabs w, w+16, ... of the matching dense gradient
-// column, the 16 partials are combined in a fixed order (deterministic), then wave 0
-// applies Adam.  Image padding stays exactly 0.  The last block writes this rank's tail.
+// Slab reduction + Adam + StepLR + FedAvg pre-scale.  Block = 16 waves x 64 DENSE
+// parameters: wave w sums slab rows w, w+16, ... of its 64 columns with 16 rows in flight
+// per lane (one 4-byte load per row would leave ~1 KB in flight per wave: latency bound);
+// the 16 partials are combined in a fixed order (deterministic), then wave 0 applies Adam
+// and writes the result at the parameter's image position.  Image padding is never
+// written (it stays 0 in every buffer).  The last block writes this rank's metric tail.
 #define ADAM_WAVES 16
+#define ADAM_DEPTH 16
 __global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
@@ -497,68 +497,76 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     __shared__ float part[ADAM_WAVES][64];
     const int last_local_step = (local_step == c.local_steps - 1);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nparam_blocks = (d.Pimg + 63) / 64;
+    const int nparam_blocks = (d.P + 63) / 64;
     const FLState S = *st;
     if (blockIdx.x >= nparam_blocks) {
         // tail block: this rank's confusion slots are zeroed (fl_eval accumulates into
-        // them), its loss slot gets the summed per-block CE partials
-        for (int j = threadIdx.x; j < c.tail_len; j += blockDim.x) {
-            const int i = d.Pimg + j;
+        // them); its loss slot gets the per-workgroup CE partials, summed in a fixed order
+        if (!last_local_step) return;
+        float lp = 0.f;
+        for (int s = threadIdx.x; s < c.n_slabs; s += blockDim.x) lp += b.slab[(size_t)s * c.slab_stride + d.P];
+        part[wave][lane] = lp;
+        lds_barrier();
+        if (wave == 0) {
+            float t = 0.f;
+#pragma unroll
+            for (int w = 0; w < ADAM_WAVES; ++w) t += part[w][lane];
+            t = wave_sum(t);
+            part[0][lane] = t;
+        }
+        lds_barrier();
+        const float loss = part[0][0];
+        for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
+            const int i = d.Pimg + jj;
             if (!S.live) {
-                if (last_local_step) comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
+                comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
                 continue;
             }
-            if (!last_local_step) continue;
-            const int k = j / c.tail_stride, e = j - k * c.tail_stride;
-            float val = 0.f;
-            if (k == c.rank && e == c.tail_stride - 1)
-                for (int s = 0; s < c.n_slabs; ++s) val += b.slab[(size_t)s * c.slab_stride + d.P];
-            comm[i] = val;
+            const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
+            comm[i] = (k == c.rank && e == c.tail_stride - 1) ? loss : 0.f;
         }
         return;
     }
-    const int j = blockIdx.x * 64 + lane;  // image index
+    const int di = blockIdx.x * 64 + lane;  // dense index
+    const bool valid = di < d.P;
+    // dense index -> image index
+    int j = 0;
+    if (valid) {
+        int l = 0;
+        while (l + 1 < d.L && di >= d.w_off[l + 1]) ++l;
+        const int K = d.dim[l];
+        if (di < d.b_off[l]) {
+            const int e = di - d.w_off[l];
+            const int n = e / K, k = e - n * K;
+            j = d.iw_off[l] + n * fl_ldw(K) + k;
+        } else {
+            j = d.ib_off[l] + (di - d.b_off[l]);
+        }
+    }
     if (!S.live) {
         // past the stop: rank 0 contributes the (identical) global weights, others 0, so the
         // all-reduce returns them bit-exactly
-        if (wave == 0 && j < d.Pimg && last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
+        if (wave == 0 && valid && last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
         return;
     }
-    // image index -> dense index (or padding)
-    int di = -1;
-    if (j < d.Pimg) {
-        int l = 0;
-        while (l + 1 < d.L && j >= d.iw_off[l + 1]) ++l;
-        const int K = d.dim[l], N = d.dim[l + 1];
-        if (j < d.ib_off[l]) {
-            const int e = j - d.iw_off[l], ldw = fl_ldw(K);
-            const int n = e / ldw, k = e - n * ldw;
-            if (n < N && k < K) di = d.w_off[l] + n * K + k;
-        } else {
-            const int n = j - d.ib_off[l];
-            if (n < N) di = d.b_off[l] + n;
-        }
-    }
     float g = 0.f;
-    if (di >= 0) {
-        const float* sp = b.slab + di;
-        int s = wave;
-        for (; s + 3 * ADAM_WAVES < c.n_slabs; s += 4 * ADAM_WAVES) {
-            const float g0 = sp[(size_t)(s)*c.slab_stride];
-            const float g1 = sp[(size_t)(s + ADAM_WAVES) * c.slab_stride];
-            const float g2 = sp[(size_t)(s + 2 * ADAM_WAVES) * c.slab_stride];
-            const float g3 = sp[(size_t)(s + 3 * ADAM_WAVES) * c.slab_stride];
-            g += g0; g += g1; g += g2; g += g3;
+    {
+        const float* sp = b.slab + (valid ? di : 0);
+        for (int s0 = wave; s0 < c.n_slabs; s0 += ADAM_WAVES * ADAM_DEPTH) {
+            float x[ADAM_DEPTH];
+#pragma unroll
+            for (int u = 0; u < ADAM_DEPTH; ++u) {
+                const int s = s0 + u * ADAM_WAVES;
+                const float v = sp[(size_t)(s < c.n_slabs ? s : 0) * c.slab_stride];  // unpredicated
+                x[u] = s < c.n_slabs ? v : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < ADAM_DEPTH; ++u) g += x[u];
         }
-        for (; s < c.n_slabs; s += ADAM_WAVES) g += sp[(size_t)s * c.slab_stride];
     }
     part[wave][lane] = g;
     lds_barrier();
-    if (wave != 0 || j >= d.Pimg) return;
-    if (di < 0) {  // padding: keep the published image padding exactly 0
-        if (last_local_step) comm[j] = 0.f;
-        return;
-    }
+    if (wave != 0 || !valid) return;
     g = 0.f;
 #pragma unroll
     for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
@@ -716,7 +724,7 @@ hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers&
 
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
                           const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s) {
-    const int blocks = (d.Pimg + 63) / 64 + 1;
+    const int blocks = (d.P + 63) / 64 + 1;
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
                        local_step);
     return hipGetLastError();

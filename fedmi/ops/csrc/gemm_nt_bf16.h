@@ -1,0 +1,19 @@
+// bf16 NT GEMM (gemm_nt_bf16.hip): C = alpha * A[M][K] . B[N][K]^T (+bias, ReLU, mask, +beta*C).
+#pragma once
+#include <hip/hip_runtime.h>
+
+struct NTArgs {
+    int M, N, K;
+    const void* A; int lda;     // bf16 [M][lda]
+    const void* B; int ldb;     // bf16 [N][ldb]
+    float* C; int ldc;          // optional fp32 output
+    void* Cbf16; int ldcb;      // optional bf16 row-major output
+    void* CbT; int ldct;        // optional bf16 transposed output [N][ldct]
+    const float* bias;          // optional [N]
+    const void* mask; int ldmask;  // optional bf16 [M][ldmask]: out = mask > 0 ? v : 0
+    int relu;
+    float alpha, beta;
+};
+
+hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s);
+hipError_t transpose_bf16_launch(const float* in, int R, int C, int ldi, void* out, int ldo, hipStream_t s);

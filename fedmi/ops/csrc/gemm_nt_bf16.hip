@@ -1,0 +1,169 @@
+// High-throughput bf16 "NT" GEMM for the wide-MLP path (gfx950):
+//
+//   C[M][N] = A[M][K] . B[N][K]^T      (both operands k-contiguous, bf16; fp32 accumulate)
+//
+// The wide client (fedmi/fl/wide.py) keeps every operand k-contiguous -- activations and
+// deltas are also written transposed by the epilogues, and W^T is re-quantised after each
+// optimizer step -- so forward (X W^T), dgrad (dY W) and wgrad (dY^T X) are all this
+// kernel.  Structure (CDNA guide §5, "standard MFMA GEMM main loop"):
+//   * 128x128 block tile, BK = 64, 256 threads = 4 waves in 2x2, 64x64 per wave
+//     (4x4 tiles of v_mfma_f32_16x16x32_bf16, 64 fp32 accumulators per lane);
+//   * global -> registers (16-byte loads) for k-tile t+1 issued before the MFMAs of k-tile t,
+//     written to the other LDS buffer after them (T14 split), one barrier per k-tile;
+//   * LDS rows of 128 B with the 16-byte chunk index XOR-swizzled by (row >> 1) & 7, so the
+//     16 rows read by one ds_read_b128 lane group land on 16 distinct bank slots (T2);
+//   * XCD-aware block remap (T1); fused epilogue: alpha, +bias, ReLU, +beta*C, fp32 and/or
+//     bf16 row-major and bf16 transposed outputs.
+// Requires M % 128 == N % 128 == K % 64 == 0 (the host falls back to gemm_mfma.hip).
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "gemm_nt_bf16.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+#define NT_BM 128
+#define NT_BN 128
+#define NT_BK 64
+#define NT_THREADS 256
+
+// byte offset of 16-byte chunk c (0..7) of row r in a [128][64] bf16 LDS tile
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ int xcd_remap_nt(int bid, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+__global__ void __launch_bounds__(NT_THREADS)
+gemm_nt_bf16_kernel(NTArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2][2][NT_BM * NT_BK * 2];  // [buf][A/B]
+    const int mt = g.M / NT_BM, nt = g.N / NT_BN;
+    const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
+    const int m0 = (bid % mt) * NT_BM, n0 = (bid / mt) * NT_BN;
+    const __hip_bfloat16* A = reinterpret_cast<const __hip_bfloat16*>(g.A);
+    const __hip_bfloat16* B = reinterpret_cast<const __hip_bfloat16*>(g.B);
+    const int t = threadIdx.x;
+    const int wave = t >> 6, lane = t & 63;
+    const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+    const int lr = lane & 15, lg = lane >> 4;
+
+    // staging map: 128 rows x 8 chunks of 16 B = 1024 chunks per operand, 4 per thread
+    int srow[4], schunk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int id = t + u * NT_THREADS;
+        srow[u] = id >> 3;
+        schunk[u] = id & 7;
+    }
+    uint4 ra[4], rb[4];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            ra[u] = *reinterpret_cast<const uint4*>(A + (size_t)(m0 + srow[u]) * g.lda + k0 + schunk[u] * 8);
+            rb[u] = *reinterpret_cast<const uint4*>(B + (size_t)(n0 + srow[u]) * g.ldb + k0 + schunk[u] * 8);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            *reinterpret_cast<uint4*>(smem[buf][0] + swz(srow[u], schunk[u])) = ra[u];
+            *reinterpret_cast<uint4*>(smem[buf][1] + swz(srow[u], schunk[u])) = rb[u];
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int ktiles = g.K / NT_BK;
+    for (int kt = 0; kt < ktiles; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < ktiles) gload((kt + 1) * NT_BK);  // in flight during this tile's MFMAs
+        const char* As = smem[cur][0];
+        const char* Bs = smem[cur][1];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {  // two 32-deep MFMA k-steps per 64-deep tile
+            bf16x8 af[4], bf[4];
+            const int chunk = ks * 4 + lg;  // lane group lg holds k = 8*lg .. 8*lg+7 of the step
+#pragma unroll
+            for (int x = 0; x < 4; ++x) af[x] = *reinterpret_cast<const bf16x8*>(As + swz(wm + 16 * x + lr, chunk));
+#pragma unroll
+            for (int y = 0; y < 4; ++y) bf[y] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn + 16 * y + lr, chunk));
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bf[y], acc[x][y], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (kt + 1 < ktiles) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue (C/D map: col = lane&15, row = 4*(lane>>4) + j)
+    __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
+    __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        const int n = n0 + wn + 16 * y + lr;
+        const float bv = g.bias != nullptr ? g.bias[n] : 0.f;
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int mm = m0 + wm + 16 * x + 4 * lg + j;
+                float v = acc[x][y][j] * g.alpha + bv;
+                if (g.relu) v = fmaxf(v, 0.f);
+                if (g.mask != nullptr) {
+                    const __hip_bfloat16 mk = reinterpret_cast<const __hip_bfloat16*>(g.mask)[(size_t)mm * g.ldmask + n];
+                    v = __bfloat162float(mk) > 0.f ? v : 0.f;
+                }
+                if (g.C != nullptr) {
+                    float* cp = g.C + (size_t)mm * g.ldc + n;
+                    if (g.beta != 0.f) v += g.beta * *cp;
+                    *cp = v;
+                }
+                if (Cb != nullptr) Cb[(size_t)mm * g.ldcb + n] = __float2bfloat16(v);
+                if (CbT != nullptr) CbT[(size_t)n * g.ldct + mm] = __float2bfloat16(v);
+            }
+    }
+}
+
+hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
+    if (g.M % NT_BM || g.N % NT_BN || g.K % NT_BK || g.lda % 8 || g.ldb % 8) return hipErrorInvalidValue;
+    const int blocks = (g.M / NT_BM) * (g.N / NT_BN);
+    hipLaunchKernelGGL(gemm_nt_bf16_kernel, dim3(blocks), dim3(NT_THREADS), 0, s, g);
+    return hipGetLastError();
+}
+
+// Transposing bf16 copy: out[c][r] = bf16(in[r][c]) for a [R][C] fp32 matrix (W^T refresh).
+__global__ void transpose_bf16_kernel(const float* __restrict__ in, int R, int Cc, int ldi,
+                                      __hip_bfloat16* __restrict__ out, int ldo) {
+    __shared__ float tile[32][33];
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+    for (int i = ty; i < 32; i += 8) {
+        const int r = r0 + i, c = c0 + tx;
+        tile[i][tx] = (r < R && c < Cc) ? in[(size_t)r * ldi + c] : 0.f;
+    }
+    __syncthreads();
+    for (int i = ty; i < 32; i += 8) {
+        const int c = c0 + i, r = r0 + tx;
+        if (c < Cc && r < R) out[(size_t)c * ldo + r] = __float2bfloat16(tile[tx][i]);
+    }
+}
+
+hipError_t transpose_bf16_launch(const float* in, int R, int C, int ldi, void* out, int ldo, hipStream_t s) {
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, s, in, R, C, ldi,
+                       reinterpret_cast<__hip_bfloat16*>(out), ldo);
+    return hipGetLastError();
+}
