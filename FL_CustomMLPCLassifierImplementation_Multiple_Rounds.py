@@ -21,13 +21,14 @@ import sys
 
 import numpy as np
 
-from fedmi.ckpt.checkpoint import save_checkpoint
+from fedmi.ckpt.checkpoint import resume, save_checkpoint
 from fedmi.data.tabular import DEFAULT_DATASET, DEFAULT_LABEL, load_tabular
 from fedmi.fl.engine import EngineConfig
 from fedmi.fl.trainer import FederatedMLPLearning
 from fedmi.models.mlp import MLPModel  # noqa: F401  (reference symbol)
 from fedmi.obs.console import JsonlWriter
 from fedmi.parallel.comm import get_world
+from fedmi.runtime.fault import parse_fault
 
 
 
@@ -55,7 +56,15 @@ def parse_args(argv=None):
     ap.add_argument("--rows-per-block", type=int, default=32)
     ap.add_argument("--graph-rounds", type=int, default=16)
     ap.add_argument("--jsonl", default=None, help="append per-round metrics as JSON lines")
-    ap.add_argument("--save", default=None, help="checkpoint path (reference weight layout)")
+    ap.add_argument("--save", default=None, help="checkpoint directory written at the end (reference weight layout)")
+    ap.add_argument("--resume", default=None, help="checkpoint directory to continue from (same clients/dims)")
+    ap.add_argument("--fault-inject", default=None, metavar="RANK:ROUND[:raise|exit|hang]",
+                    help="make one client fail at a round (tests the abort path)")
+    ap.add_argument("--watchdog-s", type=float, default=0.0,
+                    help="abort the job if a chunk of rounds stalls this long (0 = off)")
+    ap.add_argument("--debug", action="store_true", help="synchronised phases + NaN/Inf checks every round")
+    ap.add_argument("--profile", type=int, default=0, metavar="N",
+                    help="time the first N rounds per phase with hipEvents (HIP engine)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args(argv)
 
@@ -70,24 +79,35 @@ def main(argv=None):
     cfg = EngineConfig(hidden=tuple(a.hidden), lr=a.lr, step_size=a.step_size, gamma=a.gamma,
                        local_steps=a.local_steps, prox_mu=a.fedprox_mu, early_stop=not a.no_early_stop,
                        patience=a.patience, tolerance=a.tolerance, max_rounds=a.rounds,
-                       rows_per_block=a.rows_per_block, graph_rounds=a.graph_rounds, seed=a.seed)
+                       rows_per_block=a.rows_per_block, graph_rounds=a.graph_rounds, seed=a.seed,
+                       debug=a.debug)
     trainer = FederatedMLPLearning(ds.X_train, ds.y_train, rank, size, comm=comm, hidden_sizes=a.hidden,
                                    mode=a.mode, backend=a.engine, seed=a.seed, config=cfg,
                                    shard_mode=a.partition, alpha=a.alpha)
+    if a.resume:
+        done = resume(a.resume, trainer)
+        if rank == 0:
+            print(f"Resumed from {a.resume} after {done} rounds", flush=True)
+    timings = None
+    if a.profile and hasattr(trainer.engine, "profile"):
+        timings = trainer.engine.profile(a.profile)
+        if rank == 0:
+            print("Phase timings (us/round, first %d rounds): " % a.profile
+                  + ", ".join(f"{k}: {v:.2f}" for k, v in timings.items()), flush=True)
     global_metrics = trainer.train_and_evaluate(comm, rounds=a.rounds, termination_patience=a.patience,
-                                                tolerance=a.tolerance, verbose=not a.quiet)
+                                                tolerance=a.tolerance, verbose=not a.quiet,
+                                                fault=parse_fault(a.fault_inject), watchdog_s=a.watchdog_s)
     if a.mode == "correct":
         test = trainer.evaluate_global(ds.X_test, ds.y_test, comm)
         if rank == 0:
             print("Held-out test metrics of the aggregated model: "
                   + ", ".join(f"{k}: {v:.4f}" for k, v in test.items()), flush=True)
-    if rank == 0:
-        if a.jsonl:
-            w = JsonlWriter(a.jsonl)
-            w.history(trainer.history(), clients=size, script="C")
-            w.close()
-        if a.save:
-            save_checkpoint(a.save, trainer)
+    if rank == 0 and a.jsonl:
+        w = JsonlWriter(a.jsonl)
+        w.history(trainer.history(), clients=size, script="C", timings=timings)
+        w.close()
+    if a.save:
+        save_checkpoint(a.save, trainer)   # collective: every client writes its optimizer state
     comm.close()
     return global_metrics
 

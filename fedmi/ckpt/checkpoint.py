@@ -5,23 +5,28 @@ format: the ``named_parameters()`` dict ``model.{2i}.weight`` [ou
 ``model.{2i}.bias`` fp32 ([C], C:93-94) and, for sklearn, ``coefs_ + intercepts_``
 ([in, out], float64; S:26).  A fedmi checkpoint is a directory with
 
-* ``weights.safetensors`` -- the global model under the reference key names (loadable into
-  a plain ``torch.nn`` model of the reference with ``load_state_dict``),
-* ``optim.safetensors``   -- flat Adam ``exp_avg`` / ``exp_avg_sq`` (these persist across
-  rounds in the reference, Q6) and the local weights,
-* ``meta.json``           -- dims, rounds done, engine config, early-stop state, history.
+* ``weights.safetensors``       -- the global (aggregated) model under the reference key
+  names, loadable into a plain ``torch.nn`` model of the reference with ``load_state_dict``;
+* ``client{r}.safetensors``     -- per client r: local weights and the flat Adam
+  ``exp_avg`` / ``exp_avg_sq`` (they persist across rounds in the reference, Q6);
+* ``meta.json``                 -- dims, rounds done (= StepLR counter and Adam step),
+  engine config, replicated early-stop state and the metric history.
 
-Only safetensors / JSON: nothing in a checkpoint can execute code on load.
+Only safetensors / JSON: nothing in a checkpoint can execute code on load.  The state is
+engine-independent (dense reference layout), so a run checkpointed on the HIP engine
+resumes on the torch engine and vice versa.
 """
 from __future__ import annotations
 
 import json
 import os
-from typing import Dict
+from typing import Dict, Optional
 
 import numpy as np
 
 from ..models.mlp import dict_to_flat, flat_to_dict
+
+FORMAT = "fedmi-ckpt-2"
 
 
 def _st():
@@ -39,43 +44,78 @@ def load_weights(path: str) -> Dict[str, np.ndarray]:
     return dict(load_file(path))
 
 
+def _engine(obj):
+    return obj.engine if hasattr(obj, "engine") else obj
+
+
+def _barrier(eng) -> None:
+    comm = getattr(eng, "comm", None)
+    if comm is not None and getattr(comm, "size", 1) > 1:
+        comm.Barrier()
+
+
 def save_checkpoint(path: str, trainer) -> None:
-    eng = trainer.engine if hasattr(trainer, "engine") else trainer
+    """Collective over the clients: every rank writes its own ``client{r}`` file, rank 0
+    writes the global weights and the metadata."""
+    eng = _engine(trainer)
+    st = eng.portable_state()
     os.makedirs(path, exist_ok=True)
-    sd = eng.state_dict()
-    save_weights(os.path.join(path, "weights.safetensors"), flat_to_dict(sd["params"], eng.dims))
     save_file, _ = _st()
-    optim = {}
-    if "exp_avg" in sd:
-        optim["exp_avg"] = np.asarray(sd["exp_avg"], np.float32)
-        optim["exp_avg_sq"] = np.asarray(sd["exp_avg_sq"], np.float32)
-        optim["local"] = np.asarray(sd["local"], np.float32)
-        optim["device_state"] = np.asarray(sd["state"], np.uint8)
-    if optim:
-        save_file(optim, os.path.join(path, "optim.safetensors"))
-    hist = sd.get("history", {})
-    meta = {
-        "format": "fedmi-ckpt-1",
-        "dims": list(eng.dims),
-        "rounds": int(sd.get("rounds", 0)),
-        "config": eng.cfg.to_dict(),
-        "world": eng.world,
-        "rank": eng.rank,
-        "history": {k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in hist.items()},
-    }
-    if "stopper" in sd:
-        meta["stopper"] = sd["stopper"]
-    with open(os.path.join(path, "meta.json"), "w") as f:
-        json.dump(meta, f)
+    save_file({"local": np.asarray(st["local"], np.float32), "exp_avg": np.asarray(st["exp_avg"], np.float32),
+               "exp_avg_sq": np.asarray(st["exp_avg_sq"], np.float32)},
+              os.path.join(path, f"client{eng.rank}.safetensors"))
+    if eng.rank == 0:
+        save_weights(os.path.join(path, "weights.safetensors"), flat_to_dict(st["global"], eng.dims))
+        hist = st["history"]
+        meta = {
+            "format": FORMAT,
+            "dims": list(eng.dims),
+            "rounds": int(st["rounds"]),
+            "config": eng.cfg.to_dict(),
+            "world": eng.world,
+            "early_stop": st["es"],
+            "history": {k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in hist.items()},
+        }
+        tmp = os.path.join(path, "meta.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(meta, f)
+        os.replace(tmp, os.path.join(path, "meta.json"))
+    _barrier(eng)
 
 
-def load_checkpoint(path: str) -> dict:
+def load_checkpoint(path: str, rank: Optional[int] = None) -> dict:
     with open(os.path.join(path, "meta.json")) as f:
         meta = json.load(f)
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"{path}: unsupported checkpoint format {meta.get('format')!r}")
     w = load_weights(os.path.join(path, "weights.safetensors"))
     out = {"meta": meta, "weights": w, "flat": dict_to_flat(w, meta["dims"])}
-    op = os.path.join(path, "optim.safetensors")
-    if os.path.isfile(op):
-        _, load_file = _st()
-        out["optim"] = dict(load_file(op))
+    if rank is not None:
+        cp = os.path.join(path, f"client{rank}.safetensors")
+        if os.path.isfile(cp):
+            _, load_file = _st()
+            out["client"] = dict(load_file(cp))
     return out
+
+
+def resume(path: str, trainer) -> int:
+    """Restore a run saved by :func:`save_checkpoint` into ``trainer`` (same dims and
+    client count); returns the number of rounds already done."""
+    eng = _engine(trainer)
+    ck = load_checkpoint(path, rank=eng.rank)
+    meta = ck["meta"]
+    if list(meta["dims"]) != list(eng.dims):
+        raise ValueError(f"checkpoint dims {meta['dims']} != model dims {eng.dims}")
+    if int(meta["world"]) != eng.world:
+        raise ValueError(f"checkpoint has {meta['world']} clients, this run has {eng.world}")
+    if "client" not in ck:
+        raise FileNotFoundError(f"{path}: no client{eng.rank}.safetensors")
+    c = ck["client"]
+    h = meta["history"]
+    st = {"rounds": int(meta["rounds"]), "global": ck["flat"], "local": c["local"], "exp_avg": c["exp_avg"],
+          "exp_avg_sq": c["exp_avg_sq"], "es": meta["early_stop"],
+          "history": {"rounds_run": h["rounds_run"], "stop_round": h["stop_round"],
+                      "stop_trigger": h["stop_trigger"], "global": np.asarray(h["global"]),
+                      "per_rank": np.asarray(h["per_rank"]), "loss": np.asarray(h["loss"])}}
+    eng.load_portable_state(st)
+    return st["rounds"]

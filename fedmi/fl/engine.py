@@ -52,6 +52,7 @@ class EngineConfig:
     rows_per_block: int = 32        # R rows per workgroup of the fused kernels
     graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
     seed: int = 0
+    debug: bool = False             # eager, synchronised phases + non-finite checks every round
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -136,6 +137,25 @@ class RoundEngineBase:
 
     def history(self) -> dict:
         return self.hist.as_dict()
+
+    # -- resume (round index, Adam m/v, StepLR counter, early-stop state) --
+    def portable_state(self) -> dict:
+        """Engine-independent resume state (dense reference layout, numpy only).  A state
+        written by one backend loads into the other."""
+        raise NotImplementedError
+
+    def load_portable_state(self, st: dict) -> None:
+        raise NotImplementedError
+
+    def _load_history(self, h: dict) -> None:
+        n = int(h.get("rounds_run", 0))
+        self.hist.rounds_run = n
+        if n:
+            self.hist.glob[:n] = np.asarray(h["global"], dtype=np.float64).reshape(n, 4)
+            self.hist.rank[:n] = np.asarray(h["per_rank"], dtype=np.float64).reshape(n, self.world, 4)
+            self.hist.loss[:n] = np.asarray(h["loss"], dtype=np.float32).reshape(n)
+        self.hist.stop_round = int(h.get("stop_round", -1))
+        self.hist.stop_trigger = int(h.get("stop_trigger", -1))
 
 
 # ---------------------------------------------------------------------------------------
@@ -236,6 +256,9 @@ class TorchRoundEngine(RoundEngineBase):
         return self.stopper.stopped
 
     def _finalize(self, r: int, tail: np.ndarray) -> None:
+        if self.cfg.debug:
+            _check_finite(r, "aggregated weights", self.model.flat.detach())
+            _check_finite(r, "loss/confusion tail", torch.as_tensor(tail))
         tails = tail.reshape(self.world, self.tail_stride)
         C = self.n_classes
         per = [metrics_from_confusion(t[:C * C].reshape(C, C)) for t in tails]
@@ -266,6 +289,52 @@ class TorchRoundEngine(RoundEngineBase):
         return {"params": self.global_flat(), "optimizer": self.optimizer.state_dict(),
                 "scheduler": self.scheduler.state_dict(), "stopper": self.stopper.state_dict(),
                 "rounds": self.rounds_issued, "history": self.hist.as_dict()}
+
+    def portable_state(self) -> dict:
+        params = list(self.model.parameters())
+        m = [self.optimizer.state.get(p, {}).get("exp_avg") for p in params]
+        v = [self.optimizer.state.get(p, {}).get("exp_avg_sq") for p in params]
+        cat = (lambda ts: np.zeros(self.P, np.float32) if ts[0] is None else
+               torch.cat([t.detach().reshape(-1).cpu() for t in ts]).numpy().astype(np.float32))
+        sp = self.stopper
+        return {
+            "rounds": int(self.rounds_issued), "global": self.global_flat(), "local": self.local_flat(),
+            "exp_avg": cat(m), "exp_avg_sq": cat(v),
+            "es": {"count": int(sp.count), "has_prev": sp.prev is not None,
+                   "prev": [0.0] * 4 if sp.prev is None else [float(x) for x in sp.prev],
+                   "stopped": bool(sp.stopped), "stop_round": int(self.hist.stop_round)},
+            "history": self.hist.as_dict(),
+        }
+
+    def load_portable_state(self, st: dict) -> None:
+        r = int(st["rounds"])
+        cfg = self.cfg
+        with torch.no_grad():
+            self.model.flat.copy_(torch.as_tensor(np.asarray(st["global"], np.float32)))
+        self.global_params = self.model.flat.detach().clone()
+        steps = r * int(cfg.local_steps)
+        if steps:
+            off = 0
+            for p in self.model.parameters():
+                n = p.numel()
+                self.optimizer.state[p] = {
+                    "step": torch.tensor(float(steps)),
+                    "exp_avg": torch.as_tensor(np.asarray(st["exp_avg"][off:off + n], np.float32)).view_as(p).clone(),
+                    "exp_avg_sq": torch.as_tensor(np.asarray(st["exp_avg_sq"][off:off + n], np.float32)).view_as(p).clone(),
+                }
+                off += n
+        lr = cfg.lr * cfg.gamma ** (r // cfg.step_size)
+        for g in self.optimizer.param_groups:
+            g["lr"] = lr
+        self.scheduler.last_epoch = r
+        self.scheduler._step_count = r + 1
+        self.scheduler._last_lr = [lr]
+        es = st["es"]
+        self.stopper.count = int(es["count"])
+        self.stopper.prev = np.asarray(es["prev"], np.float64) if es["has_prev"] else None
+        self.stopper.stopped = bool(es["stopped"])
+        self.rounds_issued = r
+        self._load_history(st["history"])
 
 
 # ---------------------------------------------------------------------------------------
@@ -353,8 +422,64 @@ class HipRoundEngine(RoundEngineBase):
     def _stream(self) -> int:
         return self.stream.cuda_stream
 
+    def _issue_debug(self, n: int) -> None:
+        """Debug mode: every phase launched eagerly and synchronised, so a
+        fault is attributed to its kernel, and weights / metric tails checked for NaN/Inf
+        after every local step and every aggregation."""
+        s = self._stream()
+        for _ in range(n):
+            r = self.rounds_issued
+            out = self.params[(r + 1) & 1]
+            self.engine.phase(r, 0, s, None)
+            self.stream.synchronize()
+            _check_finite(r, "local weights after the Adam step", self.local)
+            self.engine.phase(r, 1, s, None)
+            self.stream.synchronize()
+            if self.world > 1:
+                if self._native_comm is not None:
+                    self.engine.phase(r, 2, s, self._native_comm)
+                else:
+                    with torch.cuda.stream(self.stream):
+                        self.comm.allreduce_(out)
+            self.stream.synchronize()
+            _check_finite(r, "aggregated weights / metric tails", out)
+            self.rounds_issued += 1
+
+    def profile(self, n: int) -> Dict[str, float]:
+        """Run ``n`` live rounds eagerly with hipEvents around each phase; returns mean
+        microseconds of local step (train + Adam kernels), eval, all-reduce and round."""
+        s = self._stream()
+        names = ("train", "eval", "allreduce")
+        acc = dict.fromkeys(names + ("round",), 0.0)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        n = min(n, self.cfg.max_rounds - self.rounds_issued)
+        for _ in range(n):
+            r = self.rounds_issued
+            ev[0].record(self.stream)
+            self.engine.phase(r, 0, s, None)
+            ev[1].record(self.stream)
+            self.engine.phase(r, 1, s, None)
+            ev[2].record(self.stream)
+            if self.world > 1:
+                if self._native_comm is not None:
+                    self.engine.phase(r, 2, s, self._native_comm)
+                else:
+                    with torch.cuda.stream(self.stream):
+                        self.comm.allreduce_(self.params[(r + 1) & 1])
+            ev[3].record(self.stream)
+            self.stream.synchronize()
+            for i, k in enumerate(names):
+                acc[k] += 1e3 * ev[i].elapsed_time(ev[i + 1])
+            acc["round"] += 1e3 * ev[0].elapsed_time(ev[3])
+            self.rounds_issued += 1
+        self.sync_history()
+        return {k + "_us": v / max(n, 1) for k, v in acc.items()}
+
     def _issue(self, n: int) -> None:
         """Issue rounds [rounds_issued, rounds_issued + n) on the current stream."""
+        if self.cfg.debug:
+            self._issue_debug(n)
+            return
         s = self._stream()
         r0 = self.rounds_issued
         g = int(self.cfg.graph_rounds)
@@ -472,12 +597,65 @@ class HipRoundEngine(RoundEngineBase):
         self.stream.synchronize()
         return cm.cpu().numpy().reshape(self.n_classes, self.n_classes).astype(np.int64)
 
+    def portable_state(self) -> dict:
+        self.sync_history()
+        r = self.rounds_issued
+        st = self._read_state((r + 1) & 1)   # the finalized copy (sync_history folded round r-1)
+        return {
+            "rounds": int(r), "global": self.global_flat(), "local": self.local_flat(),
+            "exp_avg": image_to_dense(self.mom.cpu().numpy(), self.dims),
+            "exp_avg_sq": image_to_dense(self.vel.cpu().numpy(), self.dims),
+            "es": {"count": int(st["count"]), "has_prev": bool(st["has_prev"]),
+                   "prev": [float(x) for x in st["prev"]], "stopped": bool(st["stopped"]),
+                   "stop_round": int(st["stop_round"])},
+            "history": self.hist.as_dict(),
+        }
+
+    def load_portable_state(self, st: dict) -> None:
+        r = int(st["rounds"])
+        if r > self.cfg.max_rounds:
+            raise ValueError(f"checkpoint has {r} rounds > max_rounds {self.cfg.max_rounds}")
+        self.stream.synchronize()
+        dev = self.device
+        img = lambda a: torch.as_tensor(dense_to_image(np.asarray(a, np.float32), self.dims), device=dev)
+        with torch.cuda.stream(self.stream):
+            self.params[r & 1][:self.Pimg].copy_(img(st["global"]))
+            self.local.copy_(img(st["local"]))
+            self.mom.copy_(img(st["exp_avg"]))
+            self.vel.copy_(img(st["exp_avg_sq"]))
+            es = st["es"]
+            rec = np.zeros(1, dtype=_STATE_DTYPE)
+            rec["next_round"] = r
+            rec["finalized"] = r
+            rec["cur_round"] = r - 1
+            rec["count"] = int(es["count"])
+            rec["has_prev"] = int(bool(es["has_prev"]))
+            rec["prev"] = np.asarray(es["prev"], np.float64)
+            rec["stopped"] = int(bool(es["stopped"]))
+            rec["stop_round"] = int(es["stop_round"])
+            self.state[r & 1].copy_(torch.as_tensor(rec.view(np.uint8).copy()).to(dev))
+            self._load_history(st["history"])
+            n = self.hist.rounds_run
+            if n:
+                self.h_global[:n * 4].copy_(torch.as_tensor(self.hist.glob[:n].reshape(-1), device=dev))
+                self.h_rank[:n * self.world * 4].copy_(torch.as_tensor(self.hist.rank[:n].reshape(-1), device=dev))
+                self.h_loss[:n].copy_(torch.as_tensor(self.hist.loss[:n], device=dev))
+        self.stream.synchronize()
+        self.rounds_issued = r
+        self._stopped_seen = bool(st["es"]["stopped"])
+
     def state_dict(self) -> dict:
         self.stream.synchronize()
         return {"params": self.global_flat(), "local": self.local_flat(),
                 "exp_avg": image_to_dense(self.mom.cpu().numpy(), self.dims),
                 "exp_avg_sq": image_to_dense(self.vel.cpu().numpy(), self.dims), "rounds": self.rounds_issued,
                 "state": self.state[self.rounds_issued & 1].cpu().numpy(), "history": self.hist.as_dict()}
+
+
+def _check_finite(r: int, what: str, t: torch.Tensor) -> None:
+    if not bool(torch.isfinite(t).all()):
+        bad = int((~torch.isfinite(t)).sum())
+        raise FloatingPointError(f"round {r}: {bad} non-finite values in {what}")
 
 
 class _ShapeOnly:

@@ -90,28 +90,45 @@ class FederatedMLPLearning:
         self.global_weights = flat_to_dict(self.engine.global_flat(), self.engine.dims)
 
     def train_and_evaluate(self, comm=None, rounds: int = 5, termination_patience: int = 10,
-                           tolerance: float = 1e-4, verbose: bool = True, chunk: int = 64):
+                           tolerance: float = 1e-4, verbose: bool = True, chunk: int = 64,
+                           fault=None, watchdog_s: float = 0.0):
         """Multi-round FedAvg with early stopping (C:122-207).  Returns the reference's
-        ``global_metrics`` dict of per-round lists."""
+        ``global_metrics`` dict of per-round lists.
+
+        ``fault`` (:class:`fedmi.runtime.FaultSpec`) injects a failure on one client at a
+        given round; ``watchdog_s`` > 0 aborts the job when a chunk of rounds (kernels +
+        all-reduces) stalls that long, e.g. because a peer died inside a collective."""
+        from ..runtime.watchdog import Watchdog
         eng = self.engine
+        comm = comm if comm is not None else self.comm
         if (termination_patience != eng.cfg.patience or tolerance != eng.cfg.tolerance) and eng.rounds_issued:
             raise RuntimeError("early-stop parameters must be set before the first round")
         eng.cfg.patience = termination_patience
         eng.cfg.tolerance = tolerance
         printed = eng.hist.rounds_run
+        abort = (comm.Abort if comm is not None and hasattr(comm, "Abort") else (lambda: None))
+        wd = Watchdog(watchdog_s, abort, rank=self.rank)
         try:
-            left = rounds
+            left = rounds - eng.rounds_issued
             while left > 0 and not eng.stopped:
                 n = min(chunk, left)
-                eng.run(n)
+                if fault is not None and fault.applies(self.rank):
+                    to_fault = fault.round - eng.rounds_issued
+                    if to_fault <= 0:
+                        fault.trigger(self.rank, eng.rounds_issued)
+                    n = min(n, to_fault)
+                with wd.guard(f"rounds {eng.rounds_issued}..{eng.rounds_issued + n - 1}"):
+                    eng.run(n)
                 left -= n
                 if verbose and self.rank == 0:
                     printed = print_history(eng.history(), termination_patience, start=printed)
         except Exception as e:  # reference C:203-205
             print(f"Rank {self.rank} encountered an error: {e}", flush=True)
-            if comm is not None and hasattr(comm, "Abort"):
+            if comm is not None and hasattr(comm, "Abort") and getattr(comm, "size", 1) > 1:
                 comm.Abort()
             raise
+        finally:
+            wd.close()
         self.global_weights = flat_to_dict(eng.global_flat(), eng.dims)
         return eng.hist.global_metrics_dict()
 

@@ -57,19 +57,29 @@ class WideClient:
         self.gW = [self.grads[off:off + int(np.prod(s))].view(*s) for n_, s, off in self.layout[0::2]]
         self.gb = [self.grads[off:off + int(np.prod(s))].view(*s) for n_, s, off in self.layout[1::2]]
         gdt = torch.bfloat16 if self.dtype else torch.float32
-        self.Wq = [torch.empty(w.shape, dtype=gdt, device=self.dev) for w in self.W]
-        # activations of one micro-batch: fp32 (masks / loss) + GEMM-operand copies
-        self.h = [torch.empty(self.mb, d, **f32) for d in self.dims[1:]]
-        self.hq = [torch.empty(self.mb, d, dtype=gdt, device=self.dev) for d in self.dims[1:]]
-        self.xq = torch.empty(self.mb, self.dims[0], dtype=gdt, device=self.dev)
-        self.dz = [torch.empty(self.mb, d, **f32) for d in self.dims[1:]]
-        self.dzq = [torch.empty(self.mb, d, dtype=gdt, device=self.dev) for d in self.dims[1:]]
-        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.dev)
-        self.lr_t = torch.zeros(1, dtype=torch.float64, device=self.dev)
-        self.step_t = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        dev = self.dev
+        mb, dims = self.mb, self.dims
+        self.Wq = [torch.empty(w.shape, dtype=gdt, device=dev) for w in self.W]
+        # W^T copies: B operand of the NT dgrad GEMM (hidden layers that take the NT path)
+        self.WqT = [torch.empty(w.shape[1], w.shape[0], dtype=gdt, device=dev) if self.dtype else None
+                    for w in self.W]
+        # activations / deltas of one micro-batch: row-major GEMM operands + transposed
+        # (k = rows contiguous) copies for the NT weight-gradient GEMMs
+        self.hq = [torch.empty(mb, d, dtype=gdt, device=dev) for d in dims[1:-1]]
+        self.hT = [torch.empty(d, mb, dtype=gdt, device=dev) for d in dims[1:-1]]
+        self.dzq = [torch.empty(mb, d, dtype=gdt, device=dev) for d in dims[1:]]
+        self.dzT = [torch.empty(d, mb, dtype=gdt, device=dev) for d in dims[1:-1]]
+        self.xq = torch.empty(mb, dims[0], dtype=gdt, device=dev)
+        self.scratch = torch.empty(mb * max(dims[1:]), **f32)  # fp32 epilogue target of the generic GEMM
+        self.logits = torch.empty(mb, dims[-1], **f32)
+        self.dz_out = torch.empty(mb, dims[-1], **f32)
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         self.round = 0
-        self.stream = torch.cuda.Stream(device=self.dev)
-        self.comm_stream = torch.cuda.Stream(device=self.dev)
+        self.stream = torch.cuda.Stream(device=dev)
+        self.comm_stream = torch.cuda.Stream(device=dev)
+        self.nt_calls = 0
+        # transposed (k = rows) operands need 16-byte aligned rows of the micro-batch buffers
+        self._t_ok = bool(self.dtype) and mb % 128 == 0
         self._quantize()
 
     # ------------------------------------------------------------------
@@ -78,61 +88,125 @@ class WideClient:
 
     def _quantize(self):
         with torch.cuda.stream(self.stream):
-            for w, q in zip(self.W, self.Wq):
+            for l, (w, q) in enumerate(zip(self.W, self.Wq)):
                 if self.dtype:
                     self.m.to_bf16(w.data_ptr(), q.data_ptr(), w.numel(), self._s())
+                    if self.WqT[l] is not None:
+                        N, K = w.shape
+                        self.m.transpose_bf16(w.data_ptr(), N, K, K, self.WqT[l].data_ptr(), N, self._s())
                 else:
                     q.copy_(w)
 
-    def _forward(self, r0: int, rows: int):
-        m, s = self.m, self._s()
+    @staticmethod
+    def _nt_ok(M: int, N: int, K: int) -> bool:
+        return M % 128 == 0 and N % 128 == 0 and K % 64 == 0
+
+    def _forward(self, r0: int, rows: int, keep_t: bool = True):
+        """Forward of one micro-batch.  Hidden layers write bf16 row-major (next layer's A
+        operand, ReLU mask) and, when training, bf16 transposed (wgrad B operand)."""
+        m, s, mb = self.m, self._s(), self.mb
         x = self.X[r0:r0 + rows]
         if self.dtype:
             m.to_bf16(x.data_ptr(), self.xq.data_ptr(), x.numel(), s)
-            inp, ld_in = self.xq, self.dims[0]
+            inp = self.xq
         else:
-            inp, ld_in = x, self.dims[0]
+            inp = x
         for l in range(self.L):
             K, N = self.dims[l], self.dims[l + 1]
-            epi = 2 if l + 1 < self.L else 1
-            m.gemm(rows, N, K, inp.data_ptr(), ld_in, 1, self.Wq[l].data_ptr(), K, 1, self.h[l].data_ptr(), N, epi,
-                   self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0,
-                   self.hq[l].data_ptr() if self.dtype else 0, s)
-            inp, ld_in = (self.hq[l] if self.dtype else self.h[l]), N
+            if l + 1 == self.L:  # logits head: fp32 output for the loss
+                m.gemm(rows, N, K, inp.data_ptr(), K, 1, self.Wq[l].data_ptr(), K, 1, self.logits.data_ptr(), N, 1,
+                       self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
+                break
+            hq = self.hq[l]
+            hT = self.hT[l].data_ptr() if (keep_t and self.dtype) else 0
+            if self._t_ok and self._nt_ok(rows, N, K):
+                m.gemm_nt(rows, N, K, inp.data_ptr(), K, self.Wq[l].data_ptr(), K, 0, 0, hq.data_ptr(), N, hT, mb,
+                          self.b[l].data_ptr(), 0, 0, 1, 1.0, 0.0, s)
+                self.nt_calls += 1
+            else:
+                m.gemm(rows, N, K, inp.data_ptr(), K, 1, self.Wq[l].data_ptr(), K, 1, self.scratch.data_ptr(), N, 2,
+                       self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0,
+                       hq.data_ptr() if self.dtype else 0, s)
+                if self.dtype:
+                    if hT:
+                        m.transpose_bf16(self.scratch.data_ptr(), rows, N, N, hT, mb, s)
+                else:
+                    hq[:rows].copy_(self.scratch[:rows * N].view(rows, N))
+            inp = hq
+
+    def _backward(self, r0: int, rows: int, beta: float):
+        m, s, mb, L = self.m, self._s(), self.mb, self.L
+        C = self.dims[-1]
+        # output layer (N = classes): tiny GEMMs on the generic kernel
+        K = self.dims[L - 1]
+        dzo = self.dzq[L - 1]
+        if self.dtype:
+            m.to_bf16(self.dz_out.data_ptr(), dzo.data_ptr(), rows * C, s)
+        else:
+            dzo[:rows].copy_(self.dz_out[:rows])
+        h_in = self.hq[L - 2] if L >= 2 else (self.xq if self.dtype else self.X[r0:r0 + rows])
+        m.gemm(C, K, rows, dzo.data_ptr(), C, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0, 0,
+               1.0, beta, self.dtype, 1, 0, 0, s)
+        m.colsum(self.dz_out.data_ptr(), rows, C, C, self.gb[L - 1].data_ptr(), beta, s)
+        if L >= 2:
+            # dgrad into the last hidden layer (K = C: bandwidth-bound), ReLU-masked
+            m.gemm(rows, K, C, dzo.data_ptr(), C, 1, self.Wq[L - 1].data_ptr(), K, 0, self.scratch.data_ptr(), K, 3, 0,
+                   self.hq[L - 2].data_ptr(), K, 1 if self.dtype else 0, 1.0, 0.0, self.dtype, 1, 0,
+                   self.dzq[L - 2].data_ptr() if self.dtype else 0, s)
+            if self.dtype:
+                m.transpose_bf16(self.scratch.data_ptr(), rows, K, K, self.dzT[L - 2].data_ptr(), mb, s)
+            else:
+                self.dzq[L - 2][:rows].copy_(self.scratch[:rows * K].view(rows, K))
+        # hidden layers, top down
+        for l in range(L - 2, -1, -1):
+            K, N = self.dims[l], self.dims[l + 1]
+            dq = self.dzq[l]
+            if l == 0:
+                inp = self.xq if self.dtype else self.X[r0:r0 + rows]
+            else:
+                inp = self.hq[l - 1]
+            # wgrad (+= over micro-batches): dW[N][K] = dZ^T . in;  bias: row sums of dZ^T
+            if self._t_ok and l > 0 and self._nt_ok(N, K, rows):
+                m.gemm_nt(N, K, rows, self.dzT[l].data_ptr(), mb, self.hT[l - 1].data_ptr(), mb,
+                          self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, beta, s)
+                self.nt_calls += 1
+            else:
+                m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), K, 0, self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0,
+                       1.0, beta, self.dtype, 1, 0, 0, s)
+            if self.dtype and rows % 8 == 0 and mb % 8 == 0:
+                m.rowsum_bf16(self.dzT[l].data_ptr(), N, rows, mb, self.gb[l].data_ptr(), beta, s)
+            else:
+                dzf = dq[:rows].float()
+                m.colsum(dzf.data_ptr(), rows, N, N, self.gb[l].data_ptr(), beta, s)
+            if l == 0:
+                break
+            # dgrad: dIn[rows][K] = dZ . W, masked by in > 0
+            if self._t_ok and self._nt_ok(rows, K, N):
+                m.gemm_nt(rows, K, N, dq.data_ptr(), N, self.WqT[l].data_ptr(), N, 0, 0, self.dzq[l - 1].data_ptr(), K,
+                          self.dzT[l - 1].data_ptr(), mb, 0, self.hq[l - 1].data_ptr(), K, 0, 1.0, 0.0, s)
+                self.nt_calls += 1
+            else:
+                m.gemm(rows, K, N, dq.data_ptr(), N, 1, self.Wq[l].data_ptr(), K, 0, self.scratch.data_ptr(), K, 3, 0,
+                       self.hq[l - 1].data_ptr(), K, 1 if self.dtype else 0, 1.0, 0.0, self.dtype, 1, 0,
+                       self.dzq[l - 1].data_ptr() if self.dtype else 0, s)
+                if self.dtype:
+                    m.transpose_bf16(self.scratch.data_ptr(), rows, K, K, self.dzT[l - 1].data_ptr(), mb, s)
+                else:
+                    self.dzq[l - 1][:rows].copy_(self.scratch[:rows * K].view(rows, K))
 
     def local_step(self):
         """One full-batch Adam step over the whole shard (micro-batched accumulation)."""
-        m, s = self.m, self._s()
         C = self.dims[-1]
+        s = self._s()
         with torch.cuda.stream(self.stream):
             self.loss_acc.zero_()
             for r0 in range(0, self.n, self.mb):
                 rows = min(self.mb, self.n - r0)
                 self._forward(r0, rows)
                 # loss head: softmax CE, dZ = (p - onehot) / n (full-batch mean)
-                self.m.xent(self.h[-1].data_ptr(), C, self.y[r0:].data_ptr(), rows, C, 0, 1.0 / self.n,
-                            self.dz[-1].data_ptr(), C, self.loss_acc.data_ptr(), s)
-                beta = 0.0 if r0 == 0 else 1.0
-                for l in range(self.L - 1, -1, -1):
-                    K, N = self.dims[l], self.dims[l + 1]
-                    dzl = self.dz[l]
-                    if self.dtype:
-                        m.to_bf16(dzl.data_ptr(), self.dzq[l].data_ptr(), rows * N, s)
-                        dq = self.dzq[l]
-                    else:
-                        dq = dzl
-                    if l == 0:
-                        inp = self.xq if self.dtype else self.X[r0:r0 + rows]
-                    else:
-                        inp = self.hq[l - 1] if self.dtype else self.h[l - 1]
-                    # wgrad (+= over micro-batches): dW[N][K] = dZ^T . in
-                    m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), K, 0, self.gW[l].data_ptr(), K, 0, 0, 0,
-                           0, 0, 1.0, beta, self.dtype, 1, 0, 0, s)
-                    m.colsum(dzl.data_ptr(), rows, N, N, self.gb[l].data_ptr(), beta, s)
-                    if l > 0:
-                        # dgrad with the ReLU mask of the layer input
-                        m.gemm(rows, K, N, dq.data_ptr(), N, 1, self.Wq[l].data_ptr(), K, 0, self.dz[l - 1].data_ptr(),
-                               K, 3, 0, self.h[l - 1].data_ptr(), K, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
+                self.m.xent(self.logits.data_ptr(), C, self.y[r0:].data_ptr(), rows, C, 0, 1.0 / self.n,
+                            self.dz_out.data_ptr(), C, self.loss_acc.data_ptr(), s)
+                self._backward(r0, rows, 0.0 if r0 == 0 else 1.0)
             # torch Adam + StepLR (scalars computed on host: the schedule is known)
             t = self.round + 1
             lr = self.lr * self.gamma ** (self.round // self.step_size)
@@ -155,8 +229,8 @@ class WideClient:
     def evaluate(self) -> float:
         rows = min(self.eval_rows or self.mb, self.n, self.mb)
         with torch.cuda.stream(self.stream):
-            self._forward(0, rows)
-            pred = self.h[-1][:rows].argmax(dim=1)
+            self._forward(0, rows, keep_t=False)
+            pred = self.logits[:rows].argmax(dim=1)
             acc = (pred == self.y[:rows].long()).float().mean()
         self.stream.synchronize()
         return float(acc)

@@ -167,3 +167,30 @@ hipError_t transpose_bf16_launch(const float* in, int R, int C, int ldi, void* o
                        reinterpret_cast<__hip_bfloat16*>(out), ldo);
     return hipGetLastError();
 }
+
+// Bias gradient from a transposed bf16 delta: out[n] (+)= sum_r dT[n][r], one wave per row,
+// 16-byte loads, fixed-order reduction (deterministic across runs).
+__global__ void __launch_bounds__(256) rowsum_bf16_kernel(const __hip_bfloat16* __restrict__ dT, int Nrows, int M,
+                                                          int ld, float* __restrict__ out, float beta) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= Nrows) return;
+    const __hip_bfloat16* p = dT + (size_t)row * ld;
+    float acc = 0.f;
+    for (int c = lane * 8; c < M; c += 512) {
+        const uint4 u = *reinterpret_cast<const uint4*>(p + c);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc += __uint_as_float(w[j] << 16) + __uint_as_float(w[j] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) out[row] = beta != 0.f ? beta * out[row] + acc : acc;
+}
+
+hipError_t rowsum_bf16_launch(const void* dT, int Nrows, int M, int ld, float* out, float beta, hipStream_t s) {
+    if (M % 8 || ld % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rowsum_bf16_kernel, dim3((Nrows + 3) / 4), dim3(256), 0, s,
+                       reinterpret_cast<const __hip_bfloat16*>(dT), Nrows, M, ld, out, beta);
+    return hipGetLastError();
+}

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "gemm_mfma.h"
+#include "gemm_nt_bf16.h"
 #include "mlp_ops.h"
 
 namespace py = pybind11;
@@ -301,7 +302,37 @@ static void adam_flat_py(uintptr_t p, uintptr_t m, uintptr_t v, uintptr_t g, siz
     TR_CHECK(adam_launch(a, 1, reinterpret_cast<hipStream_t>(stream)));
 }
 
+// bf16 NT GEMM (gemm_nt_bf16.hip): C = alpha * A[M][K] . B[N][K]^T with fused epilogue.
+static void gemm_nt_py(int M, int N, int K, uintptr_t A, int lda, uintptr_t B, int ldb, uintptr_t C, int ldc,
+                       uintptr_t Cbf16, int ldcb, uintptr_t CbT, int ldct, uintptr_t bias, uintptr_t mask, int ldmask,
+                       int relu, float alpha, float beta, uintptr_t stream) {
+    NTArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = reinterpret_cast<const void*>(A); g.lda = lda;
+    g.B = reinterpret_cast<const void*>(B); g.ldb = ldb;
+    g.C = reinterpret_cast<float*>(C); g.ldc = ldc;
+    g.Cbf16 = reinterpret_cast<void*>(Cbf16); g.ldcb = ldcb;
+    g.CbT = reinterpret_cast<void*>(CbT); g.ldct = ldct;
+    g.bias = reinterpret_cast<const float*>(bias);
+    g.mask = reinterpret_cast<const void*>(mask); g.ldmask = ldmask;
+    g.relu = relu; g.alpha = alpha; g.beta = beta;
+    TR_CHECK(gemm_nt_bf16_launch(g, reinterpret_cast<hipStream_t>(stream)));
+}
+
+static void transpose_bf16_py(uintptr_t in, int R, int C, int ldi, uintptr_t out, int ldo, uintptr_t stream) {
+    TR_CHECK(transpose_bf16_launch(reinterpret_cast<const float*>(in), R, C, ldi, reinterpret_cast<void*>(out), ldo,
+                                   reinterpret_cast<hipStream_t>(stream)));
+}
+
+static void rowsum_bf16_py(uintptr_t dT, int Nrows, int M, int ld, uintptr_t out, float beta, uintptr_t stream) {
+    TR_CHECK(rowsum_bf16_launch(reinterpret_cast<const void*>(dT), Nrows, M, ld, reinterpret_cast<float*>(out), beta,
+                                reinterpret_cast<hipStream_t>(stream)));
+}
+
 void register_trainer(py::module_& m) {
+    m.def("gemm_nt", &gemm_nt_py);
+    m.def("transpose_bf16", &transpose_bf16_py);
+    m.def("rowsum_bf16", &rowsum_bf16_py);
     m.def("xent", &xent_py);
     m.def("adam_flat", &adam_flat_py);
     py::class_<MLPTrainer>(m, "MLPTrainer")

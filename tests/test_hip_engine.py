@@ -7,6 +7,7 @@ from fedmi.data.synthetic import make_income_like
 from fedmi.fl.early_stop import EarlyStopper
 from fedmi.fl.engine import EngineConfig, HipRoundEngine, TorchRoundEngine
 from fedmi.models.mlp import init_flat
+from fedmi.ops import native
 
 pytestmark = pytest.mark.gpu
 
@@ -186,3 +187,105 @@ def test_wide_client_fp32_matches_torch():
     torch.cuda.synchronize()
     flat_ref = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
     assert ((c.params - flat_ref).abs().max() / flat_ref.abs().max()).item() < 1e-4
+
+
+def test_gemm_nt_bf16_epilogues():
+    """bf16 NT GEMM vs an fp32 torch reference of the same (bf16-rounded) operands."""
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(0)
+    M, N, K = 256, 384, 320
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    B = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    ref = A.float() @ B.float().t()
+    # bias + ReLU -> bf16 row-major + bf16 transposed
+    Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    CbT = torch.empty(N, M, dtype=torch.bfloat16, device=dev)
+    m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, CbT.data_ptr(), M,
+              bias.data_ptr(), 0, 0, 1, 1.0, 0.0, s)
+    r1 = (ref + bias).clamp_min(0)
+    torch.cuda.synchronize()
+    assert ((Cb.float() - r1).abs().max() / r1.abs().max()).item() < 1e-2
+    assert torch.equal(CbT, Cb.t())
+    # fp32 accumulate (beta = 1) with mask
+    mask = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    C0 = torch.randn(M, N, device=dev)
+    C = C0.clone()
+    m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, C.data_ptr(), N, 0, 0, 0, 0, 0,
+              mask.data_ptr(), N, 0, 0.5, 1.0, s)
+    r2 = torch.where(mask.float() > 0, 0.5 * ref, torch.zeros_like(ref)) + C0
+    torch.cuda.synchronize()
+    assert ((C - r2).abs().max() / r2.abs().max()).item() < 1e-5
+
+
+def test_rowsum_and_transpose_bf16():
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    X = torch.randn(200, 136, device=dev)
+    XT = torch.empty(136, 200, dtype=torch.bfloat16, device=dev)
+    m.transpose_bf16(X.data_ptr(), 200, 136, 136, XT.data_ptr(), 200, s)
+    out = torch.full((136,), 2.0, device=dev)
+    m.rowsum_bf16(XT.data_ptr(), 136, 200, 200, out.data_ptr(), 1.0, s)
+    torch.cuda.synchronize()
+    assert torch.equal(XT, X.t().to(torch.bfloat16))
+    ref = XT.float().sum(dim=1) + 2.0
+    assert (out - ref).abs().max().item() < 1e-4
+
+
+def test_wide_client_bf16_nt_path_tracks_torch():
+    from fedmi.fl.wide import WideClient
+    dev = torch.device("cuda", 0)
+    X, y = make_income_like(1536, seed=1)
+    Xt, yt = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
+    c = WideClient(Xt, yt, [14, 256, 256, 2], micro_batch=512, dtype="bf16")
+    ref = torch.nn.Sequential(torch.nn.Linear(14, 256), torch.nn.ReLU(), torch.nn.Linear(256, 256), torch.nn.ReLU(),
+                              torch.nn.Linear(256, 2)).to(dev)
+    with torch.no_grad():
+        for p, w in zip(ref.parameters(), [c.W[0], c.b[0], c.W[1], c.b[1], c.W[2], c.b[2]]):
+            p.copy_(w)
+    opt = torch.optim.Adam(ref.parameters(), lr=0.004)
+    for _ in range(3):
+        c.run_round()
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(Xt), yt.long()).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    assert c.nt_calls > 0
+    flat_ref = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    # bf16 operands: the Adam trajectory follows fp32 torch to within a few lr-steps of drift
+    err = ((c.params - flat_ref).abs().max() / flat_ref.abs().max()).item()
+    assert err < 5e-2
+
+
+def test_hip_resume_is_exact_and_portable(tmp_path):
+    from fedmi.ckpt.checkpoint import resume, save_checkpoint
+    X, y = make_income_like(2000, seed=7)
+    dims = [14, 50, 200, 2]
+
+    def mk(backend_cls, **kw):
+        cfg = EngineConfig(max_rounds=80, patience=4, tolerance=1e-3, graph_rounds=4)
+        return backend_cls(X, y, 2, cfg, None, init_flat(dims, 9), **kw)
+
+    full = mk(HipRoundEngine)
+    full.run(50)
+    a = mk(HipRoundEngine)
+    a.run(17)
+    save_checkpoint(str(tmp_path), a)
+    b = mk(HipRoundEngine)
+    assert resume(str(tmp_path), b) == 17
+    b.run(33)
+    hf, hb = full.history(), b.history()
+    assert hf["rounds_run"] == hb["rounds_run"] and hf["stop_round"] == hb["stop_round"]
+    np.testing.assert_array_equal(hf["global"], hb["global"])
+    np.testing.assert_array_equal(full.global_flat(), b.global_flat())
+    # HIP checkpoint -> torch engine: continues on the same trajectory (fp32 rounding only)
+    t = mk(TorchRoundEngine)
+    resume(str(tmp_path), t)
+    t.run(5)
+    c = mk(HipRoundEngine)
+    resume(str(tmp_path), c)
+    c.run(5)
+    np.testing.assert_allclose(t.global_flat(), c.global_flat(), rtol=1e-4, atol=1e-5)

@@ -1,17 +1,46 @@
-"""Wide-MLP client: correctness vs torch (small dims) + throughput (4096 wide)."""
-import sys, time, numpy as np, torch
+"""Wide-MLP client: correctness vs torch (small dims) + NT GEMM and 4096-wide round throughput."""
+import sys, time, torch
 sys.path.insert(0, ".")
 from fedmi.fl.wide import WideClient
 from fedmi.data.synthetic import make_income_like
+from fedmi.ops import native
+
 dev = torch.device("cuda", 0)
-X, y = make_income_like(3000, seed=0)
+m = native()
+s = torch.cuda.current_stream().cuda_stream
+# raw NT GEMM throughput at the wide-layer shapes
+for (M, N, K) in [(16384, 4096, 4096), (4096, 4096, 16384), (8192, 8192, 8192)]:
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    B = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    for _ in range(3):
+        m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, 0, 0, 0, 0, 0, 0, 1.0, 0.0, s)
+    torch.cuda.synchronize()
+    n = 20
+    t = time.time()
+    for _ in range(n):
+        m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, 0, 0, 0, 0, 0, 0, 1.0, 0.0, s)
+    torch.cuda.synchronize()
+    dt = (time.time() - t) / n
+    tt = time.time()
+    for _ in range(n):
+        Ct = A @ B.t()
+    torch.cuda.synchronize()
+    dtt = (time.time() - tt) / n
+    print(f"gemm_nt {M}x{N}x{K}: {dt*1e3:.3f} ms {2*M*N*K/dt/1e12:.1f} TF/s | torch(hipBLASLt) {2*M*N*K/dtt/1e12:.1f} TF/s",
+          flush=True)
+
+X, y = make_income_like(4096, seed=0)
 Xt = torch.as_tensor(X, device=dev); yt = torch.as_tensor(y, device=dev)
-for dt in ("fp32", "bf16"):
-    c = WideClient(Xt, yt, [14, 64, 48, 2], micro_batch=1024, dtype=dt)
-    ref = torch.nn.Sequential(torch.nn.Linear(14, 64), torch.nn.ReLU(), torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 2)).to(dev)
+for dt_, dims in (("fp32", [14, 64, 48, 2]), ("bf16", [14, 64, 48, 2]), ("bf16", [14, 256, 256, 2])):
+    c = WideClient(Xt, yt, dims, micro_batch=1024, dtype=dt_)
+    layers = []
+    for a, b in zip(dims[:-1], dims[1:]):
+        layers += [torch.nn.Linear(a, b), torch.nn.ReLU()]
+    ref = torch.nn.Sequential(*layers[:-1]).to(dev)
     with torch.no_grad():
-        for p, (w) in zip([ref[0].weight, ref[0].bias, ref[2].weight, ref[2].bias, ref[4].weight, ref[4].bias],
-                          [c.W[0], c.b[0], c.W[1], c.b[1], c.W[2], c.b[2]]):
+        ws = [t for pair in zip(c.W, c.b) for t in pair]
+        for p, w in zip(ref.parameters(), ws):
             p.copy_(w)
     opt = torch.optim.Adam(ref.parameters(), lr=0.004)
     for r in range(5):
@@ -20,7 +49,8 @@ for dt in ("fp32", "bf16"):
     torch.cuda.synchronize()
     flat_ref = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
     err = ((c.params - flat_ref).abs().max() / flat_ref.abs().max()).item()
-    print(f"{dt}: 5 rounds rel weight err vs torch fp32 {err:.2e}, loss {c.loss():.4f}", flush=True)
+    print(f"{dt_} {dims}: 5 rounds rel weight err vs torch fp32 {err:.2e}, loss {c.loss():.4f}, nt_calls {c.nt_calls}",
+          flush=True)
 rows = 1 << 17
 Xw = torch.randn(rows, 14, device=dev); yw = torch.randint(0, 2, (rows,), device=dev)
 c = WideClient(Xw, yw, [14, 4096, 4096, 4096, 2], micro_batch=16384, dtype="bf16")
@@ -28,4 +58,5 @@ c.run_round(); torch.cuda.synchronize()
 t = time.time(); n = 3
 for _ in range(n): c.run_round()
 torch.cuda.synchronize(); dt = (time.time() - t) / n
-print(f"wide bf16: rows={rows} {dt*1e3:.1f} ms/round, {c.flops_per_round/dt/1e12:.1f} TFLOP/s, {rows/dt/1e6:.2f} M samples/s", flush=True)
+print(f"wide bf16: rows={rows} {dt*1e3:.1f} ms/round, {c.flops_per_round/dt/1e12:.1f} TFLOP/s, "
+      f"{rows/dt/1e6:.2f} M samples/s", flush=True)
