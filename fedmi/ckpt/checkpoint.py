@@ -45,7 +45,8 @@ def load_weights(path: str) -> Dict[str, np.ndarray]:
 
 
 def _engine(obj):
-    return obj.engine if hasattr(obj, "engine") else obj
+    """Round engine of a trainer (``FederatedMLPLearning.engine``) or the engine itself."""
+    return obj if hasattr(obj, "portable_state") else obj.engine
 
 
 def _barrier(eng) -> None:

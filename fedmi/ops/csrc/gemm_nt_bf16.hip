@@ -8,8 +8,8 @@
 // kernel.  Structure (CDNA guide §5, "standard MFMA GEMM main loop"):
 //   * 128x128 block tile, BK = 64, 256 threads = 4 waves in 2x2, 64x64 per wave
 //     (4x4 tiles of v_mfma_f32_16x16x32_bf16, 64 fp32 accumulators per lane);
-//   * global -> registers (16-byte loads) for k-tile t+1 issued before the MFMAs of k-tile t,
-//     written to the other LDS buffer after them (T14 split), one barrier per k-tile;
+//   * operands staged global -> LDS by 16-byte LDS-DMA (global_load_lds_dwordx4: no VGPR
+//     round trip); double-buffered variant issues tile k+1's DMA before tile k's MFMAs;
 //   * LDS rows of 128 B with the 16-byte chunk index XOR-swizzled by (row >> 1) & 7, so the
 //     16 rows read by one ds_read_b128 lane group land on 16 distinct bank slots (T2);
 //   * XCD-aware block remap (T1); fused epilogue: alpha, +bias, ReLU, +beta*C, fp32 and/or
@@ -37,9 +37,21 @@ __device__ __forceinline__ int xcd_remap_nt(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// One 16-byte global -> LDS DMA per lane (global_load_lds_dwordx4).  The LDS destination is
+// wave-uniform base + lane * 16, so the swizzle lives in the per-lane GLOBAL address.
+__device__ __forceinline__ void glds16(const void* src, char* lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_base, 16, 0, 0);
+}
+
+// DB = 0: one LDS buffer (32 KiB), two barriers per K-step, ~3 blocks/CU hide the DMA.
+// DB = 1: two LDS buffers (64 KiB), the DMA of tile k+1 overlaps the MFMAs of tile k.
+template <int DB>
 __global__ void __launch_bounds__(NT_THREADS)
 gemm_nt_bf16_kernel(NTArgs g) {
-    __shared__ __attribute__((aligned(16))) char smem[2][2][NT_BM * NT_BK * 2];  // [buf][A/B]
+    __shared__ __attribute__((aligned(16))) char smem[(DB + 1) * 2 * NT_BM * NT_BK * 2];
+    constexpr int TILE = NT_BM * NT_BK * 2;  // bytes per operand tile
     const int mt = g.M / NT_BM, nt = g.N / NT_BN;
     const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
     const int m0 = (bid % mt) * NT_BM, n0 = (bid / mt) * NT_BN;
@@ -50,27 +62,23 @@ gemm_nt_bf16_kernel(NTArgs g) {
     const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
     const int lr = lane & 15, lg = lane >> 4;
 
-    // staging map: 128 rows x 8 chunks of 16 B = 1024 chunks per operand, 4 per thread
-    int srow[4], schunk[4];
+    // DMA map: wave w issues 1-KiB pieces q = 4w + i (rows 8q .. 8q+7) of each operand;
+    // lane l lands at LDS row 8q + l/8, physical chunk l%8 = logical chunk (l%8) ^ f(row).
+    const __hip_bfloat16* srcA[4];
+    const __hip_bfloat16* srcB[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int id = t + u * NT_THREADS;
-        srow[u] = id >> 3;
-        schunk[u] = id & 7;
+    for (int i = 0; i < 4; ++i) {
+        const int row = 8 * (4 * wave + i) + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        srcA[i] = A + (size_t)(m0 + row) * g.lda + c * 8;
+        srcB[i] = B + (size_t)(n0 + row) * g.ldb + c * 8;
     }
-    uint4 ra[4], rb[4];
-    auto gload = [&](int k0) {
+    auto dma = [&](int k0, int buf) {
+        char* base = smem + buf * 2 * TILE;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            ra[u] = *reinterpret_cast<const uint4*>(A + (size_t)(m0 + srow[u]) * g.lda + k0 + schunk[u] * 8);
-            rb[u] = *reinterpret_cast<const uint4*>(B + (size_t)(n0 + srow[u]) * g.ldb + k0 + schunk[u] * 8);
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            *reinterpret_cast<uint4*>(smem[buf][0] + swz(srow[u], schunk[u])) = ra[u];
-            *reinterpret_cast<uint4*>(smem[buf][1] + swz(srow[u], schunk[u])) = rb[u];
+        for (int i = 0; i < 4; ++i) {
+            glds16(srcA[i] + k0, base + (4 * wave + i) * 1024);
+            glds16(srcB[i] + k0, base + TILE + (4 * wave + i) * 1024);
         }
     };
 
@@ -80,15 +88,9 @@ gemm_nt_bf16_kernel(NTArgs g) {
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    const int ktiles = g.K / NT_BK;
-    for (int kt = 0; kt < ktiles; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < ktiles) gload((kt + 1) * NT_BK);  // in flight during this tile's MFMAs
-        const char* As = smem[cur][0];
-        const char* Bs = smem[cur][1];
+    auto compute = [&](int buf) {
+        const char* As = smem + buf * 2 * TILE;
+        const char* Bs = As + TILE;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {  // two 32-deep MFMA k-steps per 64-deep tile
             bf16x8 af[4], bf[4];
@@ -105,8 +107,25 @@ gemm_nt_bf16_kernel(NTArgs g) {
                     acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bf[y], acc[x][y], 0, 0, 0);
             __builtin_amdgcn_s_setprio(0);
         }
-        if (kt + 1 < ktiles) lstore(cur ^ 1);
-        __syncthreads();
+    };
+
+    const int ktiles = g.K / NT_BK;
+    if (DB) {
+        dma(0, 0);
+        for (int kt = 0; kt < ktiles; ++kt) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // tile kt visible to all waves; buffer (kt+1)&1 no longer read
+            if (kt + 1 < ktiles) dma((kt + 1) * NT_BK, (kt + 1) & 1);
+            compute(kt & 1);
+        }
+    } else {
+        for (int kt = 0; kt < ktiles; ++kt) {
+            dma(kt * NT_BK, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            compute(0);
+            __syncthreads();
+        }
     }
 
     // epilogue (C/D map: col = lane&15, row = 4*(lane>>4) + j)
@@ -138,10 +157,16 @@ gemm_nt_bf16_kernel(NTArgs g) {
     }
 }
 
+static int g_nt_variant = 1;
+void gemm_nt_set_variant(int v) { g_nt_variant = v; }
+
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
     if (g.M % NT_BM || g.N % NT_BN || g.K % NT_BK || g.lda % 8 || g.ldb % 8) return hipErrorInvalidValue;
     const int blocks = (g.M / NT_BM) * (g.N / NT_BN);
-    hipLaunchKernelGGL(gemm_nt_bf16_kernel, dim3(blocks), dim3(NT_THREADS), 0, s, g);
+    if (g_nt_variant == 0)
+        hipLaunchKernelGGL(gemm_nt_bf16_kernel<0>, dim3(blocks), dim3(NT_THREADS), 0, s, g);
+    else
+        hipLaunchKernelGGL(gemm_nt_bf16_kernel<1>, dim3(blocks), dim3(NT_THREADS), 0, s, g);
     return hipGetLastError();
 }
 

@@ -331,6 +331,7 @@ static void rowsum_bf16_py(uintptr_t dT, int Nrows, int M, int ld, uintptr_t out
 
 void register_trainer(py::module_& m) {
     m.def("gemm_nt", &gemm_nt_py);
+    m.def("gemm_nt_set_variant", &gemm_nt_set_variant);
     m.def("transpose_bf16", &transpose_bf16_py);
     m.def("rowsum_bf16", &rowsum_bf16_py);
     m.def("xent", &xent_py);

@@ -8,27 +8,34 @@ from fedmi.ops import native
 dev = torch.device("cuda", 0)
 m = native()
 s = torch.cuda.current_stream().cuda_stream
-# raw NT GEMM throughput at the wide-layer shapes
-for (M, N, K) in [(16384, 4096, 4096), (4096, 4096, 16384), (8192, 8192, 8192)]:
-    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
-    B = torch.randn(N, K, device=dev).to(torch.bfloat16)
-    Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+# raw NT GEMM throughput at the wide-layer shapes (random operands), both main-loop variants
+def bench(fn, n=20):
     for _ in range(3):
-        m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, 0, 0, 0, 0, 0, 0, 1.0, 0.0, s)
+        fn()
     torch.cuda.synchronize()
-    n = 20
     t = time.time()
     for _ in range(n):
-        m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, 0, 0, 0, 0, 0, 0, 1.0, 0.0, s)
+        fn()
     torch.cuda.synchronize()
-    dt = (time.time() - t) / n
-    tt = time.time()
-    for _ in range(n):
-        Ct = A @ B.t()
-    torch.cuda.synchronize()
-    dtt = (time.time() - tt) / n
-    print(f"gemm_nt {M}x{N}x{K}: {dt*1e3:.3f} ms {2*M*N*K/dt/1e12:.1f} TF/s | torch(hipBLASLt) {2*M*N*K/dtt/1e12:.1f} TF/s",
-          flush=True)
+    return (time.time() - t) / n
+
+
+for (M, N, K) in [(16384, 4096, 4096), (4096, 4096, 16384), (8192, 8192, 8192)]:
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    ref = A @ B.t()
+    dtt = bench(lambda: A @ B.t())
+    line = f"gemm_nt {M}x{N}x{K}: torch(hipBLASLt) {2*M*N*K/dtt/1e12:.0f} TF/s"
+    for v in (0, 1):
+        m.gemm_nt_set_variant(v)
+        f = lambda: m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, 0, 0, 0, 0, 0, 0,
+                              1.0, 0.0, s)
+        dt = bench(f)
+        err = ((Cb.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+        line += f" | v{v} {dt*1e3:.3f} ms {2*M*N*K/dt/1e12:.0f} TF/s err {err:.1e}"
+    print(line, flush=True)
+m.gemm_nt_set_variant(1)
 
 X, y = make_income_like(4096, seed=0)
 Xt = torch.as_tensor(X, device=dev); yt = torch.as_tensor(y, device=dev)
