@@ -53,6 +53,8 @@ def parse_args(argv=None):
     ap.add_argument("--device", default="auto")
     ap.add_argument("--backend", default="auto", help="comm backend: rccl | nccl | gloo")
     ap.add_argument("--engine", default="auto", help="hip | torch")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="MFMA operand type of the fused HIP kernels (fp32 accumulate either way)")
     ap.add_argument("--rows-per-block", type=int, default=32)
     ap.add_argument("--graph-rounds", type=int, default=16)
     ap.add_argument("--jsonl", default=None, help="append per-round metrics as JSON lines")
@@ -80,7 +82,7 @@ def main(argv=None):
                        local_steps=a.local_steps, prox_mu=a.fedprox_mu, early_stop=not a.no_early_stop,
                        patience=a.patience, tolerance=a.tolerance, max_rounds=a.rounds,
                        rows_per_block=a.rows_per_block, graph_rounds=a.graph_rounds, seed=a.seed,
-                       debug=a.debug)
+                       debug=a.debug, dtype=a.dtype)
     trainer = FederatedMLPLearning(ds.X_train, ds.y_train, rank, size, comm=comm, hidden_sizes=a.hidden,
                                    mode=a.mode, backend=a.engine, seed=a.seed, config=cfg,
                                    shard_mode=a.partition, alpha=a.alpha)

@@ -66,13 +66,13 @@ def synth_shard(n_rows: int, rank: int, device, seed: int = 7):
     return X, y
 
 
-def rounds_to_target(comm, targets=(0.80, 0.83), max_rounds=300):
+def rounds_to_target(comm, targets=(0.80, 0.83), max_rounds=300, dtype="fp32"):
     """Reference-compat convergence on the real CSV at this client count (untimed)."""
     from fedmi.data.tabular import load_tabular
     from fedmi.fl.engine import EngineConfig
     from fedmi.fl.trainer import FederatedMLPLearning
     ds = load_tabular()
-    cfg = EngineConfig(max_rounds=max_rounds, graph_rounds=16)
+    cfg = EngineConfig(max_rounds=max_rounds, graph_rounds=16, dtype=dtype)
     tr = FederatedMLPLearning(ds.X_train, ds.y_train, comm.rank, comm.size, comm=comm, config=cfg,
                               mode="compat", seed=0)
     tr.train_and_evaluate(comm, rounds=max_rounds, verbose=False)
@@ -97,6 +97,8 @@ def main(argv=None):
     ap.add_argument("--rows-per-block", type=int, default=32)
     ap.add_argument("--graph-rounds", type=int, default=16)
     ap.add_argument("--backend", default="rccl", choices=["rccl", "nccl"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="MFMA operand type of the fused kernels (fp32 accumulate, fp32 master weights)")
     ap.add_argument("--no-convergence", action="store_true")
     a = ap.parse_args(argv)
 
@@ -113,7 +115,7 @@ def main(argv=None):
     X, y = synth_shard(a.rows_per_client, comm.rank, dev)
     dims = [14, *a.hidden, 2]
     cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=a.warmup + a.steps + 8, early_stop=False,
-                       rows_per_block=a.rows_per_block, graph_rounds=a.graph_rounds)
+                       rows_per_block=a.rows_per_block, graph_rounds=a.graph_rounds, dtype=a.dtype)
     eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank),
                          n_total=a.rows_per_client * N)
 
@@ -140,7 +142,7 @@ def main(argv=None):
     assert h["rounds_run"] == a.warmup + a.steps, h["rounds_run"]
     samples = a.rows_per_client * N * a.steps
     value = samples / dt
-    rtt = None if a.no_convergence else rounds_to_target(comm)
+    rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype)
     if comm.rank == 0:
         rec = {
             "metric": METRIC,
@@ -153,7 +155,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": value / (ref_per_client(N) * N),
-            "dtype": "fp32",
+            "dtype": a.dtype,
             "data": f"synthetic income-shaped (device Philox), {a.rows_per_client} rows/client; random-init weights",
             "config": {"model": f"MLP {'-'.join(map(str, dims))} (reference [C])",
                        "global_batch": a.rows_per_client * N, "seq_len": 1,

@@ -53,6 +53,7 @@ class EngineConfig:
     graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
     seed: int = 0
     debug: bool = False             # eager, synchronised phases + non-finite checks every round
+    dtype: str = "fp32"             # MFMA operand type of the fused kernels: 'fp32' | 'bf16'
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -65,6 +66,12 @@ def _metric_mode_id(mode: str) -> int:
     if mode not in ("mean", "pooled"):
         raise ValueError(f"metric_mode must be 'mean' or 'pooled', got {mode!r}")
     return 0 if mode == "mean" else 1
+
+
+def _dtype_id(dtype: str) -> int:
+    if dtype not in ("fp32", "bf16"):
+        raise ValueError(f"dtype must be 'fp32' or 'bf16', got {dtype!r}")
+    return 0 if dtype == "fp32" else 1
 
 
 class _History:
@@ -396,6 +403,7 @@ class HipRoundEngine(RoundEngineBase):
             "eps": float(cfg.eps), "weight_decay": float(cfg.weight_decay), "prox_mu": float(cfg.prox_mu),
             "early_stop": bool(cfg.early_stop), "patience": int(cfg.patience), "atol": float(cfg.tolerance),
             "rtol": float(cfg.rtol), "max_rounds": mr, "metric_mode": _metric_mode_id(cfg.metric_mode),
+            "dtype": _dtype_id(cfg.dtype),
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(), "slab": self.slab.data_ptr(),

@@ -43,6 +43,24 @@ struct MLPDesc {
     int lds_floats;                   // LDS floats needed per block
 };
 
+// bf16 LDS layout of the fused kernels (fl_kernels_bf16.hip).  All offsets are BYTES into
+// the dynamic LDS window.  Every fan-in dimension is padded to kp = roundup32(dim) (one
+// v_mfma_f32_16x16x32_bf16 k-step per 32) and rows are kp + 8 elements apart, i.e. 16-byte
+// aligned and an odd number of 16-byte slots, so the 16 rows of a ds_read_b128 lane group
+// hit 16 distinct bank slots.  W_l has kp[l+1] rows (the dgrad contraction runs over its
+// padded fan-out), activations / deltas have R rows.  Transposed operands (wgrad over rows,
+// dgrad over W's rows) are read with ds_read_b64_tr_b16 from the same images.
+struct MLPDescB {
+    int kp[FL_MAX_LAYERS + 1];        // roundup32(dim[l])
+    int lda[FL_MAX_LAYERS + 1];       // kp[l] + 8: row stride (elements) of act_l, D_l, and W_l rows
+    int w_off[FL_MAX_LAYERS];         // W_l  bf16 [kp[l+1]][lda[l]]
+    int bias_off[FL_MAX_LAYERS];      // b_l  fp32 [kp[l+1]] (zero padded)
+    int act_off[FL_MAX_LAYERS + 1];   // act_l bf16 [R][lda[l]]   (l < L)
+    int dlt_off[FL_MAX_LAYERS + 1];   // D_l  bf16 [R][lda[l]]    (1 <= l <= L): dLoss/dz_l
+    int logit_off;                    // fp32 [R][16] classifier logits
+    int lds_bytes;
+};
+
 struct FLConfig {
     int R;              // rows per workgroup (16 or 32)
     int n_rows;         // local training rows
@@ -117,6 +135,13 @@ hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                               const float* pg, const FLState* st_in, FLState* st_out,
                               hipStream_t s);
+// bf16-operand variants (fp32 accumulate, fp32 master weights / slab / Adam state).
+hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                                const float* pg, const FLState* st_in, FLState* st_out, int local_step,
+                                hipStream_t s);
+hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                               const float* params, float* comm, const FLState* st, hipStream_t s);
+hipError_t fl_set_lds_limit_bf16(size_t bytes);
 // Stand-alone forward + confusion on an arbitrary row set (held-out evaluation).
 hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const int* y, int n_rows,
                                const float* params, float* cm_out, hipStream_t s);

@@ -160,9 +160,17 @@ class FLEngine {
         d_.img_lds = lds;
         lds += d_.Pimg;
         d_.lds_floats = lds;
-        if ((size_t)lds * 4 > 150 * 1024)
-            throw std::runtime_error("FLEngine: activations exceed LDS; use a smaller R or the layered path");
-        HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));
+        dtype_ = cfg.contains("dtype") ? cfg["dtype"].cast<int>() : 0;
+        if (dtype_ == 0) {
+            if ((size_t)lds * 4 > 150 * 1024)
+                throw std::runtime_error("FLEngine: activations exceed LDS; use a smaller R or the layered path");
+            HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));
+        } else {
+            build_bf16_layout();
+            if (e_.lds_bytes > 150 * 1024)
+                throw std::runtime_error("FLEngine(bf16): model exceeds LDS; use a smaller R or the layered path");
+            HIP_CHECK(fl_set_lds_limit_bf16((size_t)e_.lds_bytes));
+        }
 
         c_.n_rows = cfg["n_rows"].cast<int>();
         c_.inv_n = 1.0f / (float)c_.n_rows;
@@ -271,9 +279,9 @@ class FLEngine {
         float* pg = pbuf_[r & 1];
         float* cb = pbuf_[(r + 1) & 1];
         FLState* so = st_[(r + 1) & 1];
-        if (which == 0) HIP_CHECK(fl_launch_train(d_, c_, b_, pg, so, so, 1, s));
+        if (which == 0) launch_train(pg, so, so, 1, s);
         else if (which == 1) HIP_CHECK(fl_launch_adam(d_, c_, b_, b_.local, pg, cb, so, 1, s));
-        else HIP_CHECK(fl_launch_eval(d_, c_, b_, b_.local, cb, so, s));
+        else launch_eval(b_.local, cb, so, s);
     }
 
     // Per-kernel device time (us, averaged over `iters` back-to-back launches, hipEvents)
@@ -299,9 +307,9 @@ class FLEngine {
             out[name] = 1e3 * ms / iters;
         };
         const int ls = 1;
-        timeit("train", [&] { HIP_CHECK(fl_launch_train(d_, c_, b_, pg, so, so, ls, s)); });
+        timeit("train", [&] { launch_train(pg, so, so, ls, s); });
         timeit("adam", [&] { HIP_CHECK(fl_launch_adam(d_, c_, b_, b_.local, pg, cb, so, ls, s)); });
-        timeit("eval", [&] { HIP_CHECK(fl_launch_eval(d_, c_, b_, b_.local, cb, so, s)); });
+        timeit("eval", [&] { launch_eval(b_.local, cb, so, s); });
         HIP_CHECK(hipEventDestroy(e0));
         HIP_CHECK(hipEventDestroy(e1));
         return out;
@@ -329,7 +337,8 @@ class FLEngine {
         o["ib_off"] = ib;
         o["ld"] = ld;
         o["dims"] = dims;
-        o["lds_bytes"] = d_.lds_floats * 4;
+        o["lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : e_.lds_bytes;
+        o["dtype"] = dtype_;
         o["slab_stride"] = c_.slab_stride;
         o["n_slabs"] = c_.n_slabs;
         o["tail_off"] = c_.tail_off;
@@ -341,18 +350,43 @@ class FLEngine {
     }
 
   private:
+    // bf16 LDS layout (fl_common.h MLPDescB), byte offsets, 16-byte aligned pieces
+    void build_bf16_layout() {
+        std::memset(&e_, 0, sizeof(e_));
+        const int L = d_.L, R = c_.R;
+        for (int l = 0; l <= L; ++l) {
+            e_.kp[l] = (d_.dim[l] + 31) & ~31;
+            e_.lda[l] = e_.kp[l] + 8;
+        }
+        int off = 0;
+        auto take = [&](int bytes) { const int o = off; off += (bytes + 15) & ~15; return o; };
+        for (int l = 0; l < L; ++l) e_.act_off[l] = take(R * e_.lda[l] * 2);
+        for (int l = 1; l <= L; ++l) e_.dlt_off[l] = take(R * e_.lda[l] * 2);
+        e_.logit_off = take(R * 16 * 4);
+        for (int l = 0; l < L; ++l) e_.w_off[l] = take(e_.kp[l + 1] * e_.lda[l] * 2);
+        for (int l = 0; l < L; ++l) e_.bias_off[l] = take(e_.kp[l + 1] * 4);
+        e_.lds_bytes = off;
+    }
+    void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s) {
+        if (dtype_ == 0) HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s));
+        else HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s));
+    }
+    void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
+        if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
+        else HIP_CHECK(fl_launch_eval_bf16(d_, e_, c_, b_, params, comm, st, s));
+    }
     void issue_train(int r, hipStream_t s) {
         float* pg = pbuf_[r & 1];
         float* cb = pbuf_[(r + 1) & 1];
         FLState* si = st_[r & 1];
         FLState* so = st_[(r + 1) & 1];
         for (int ls = 0; ls < c_.local_steps; ++ls) {
-            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, ls == 0 ? si : so, so, ls, s));
+            launch_train(pg, ls == 0 ? si : so, so, ls, s);
             HIP_CHECK(fl_launch_adam(d_, c_, b_, ls == 0 ? pg : b_.local, pg, cb, so, ls, s));
         }
     }
     void issue_eval(int r, hipStream_t s) {
-        HIP_CHECK(fl_launch_eval(d_, c_, b_, b_.local, pbuf_[(r + 1) & 1], st_[(r + 1) & 1], s));
+        launch_eval(b_.local, pbuf_[(r + 1) & 1], st_[(r + 1) & 1], s);
     }
     void issue_allreduce(int r, hipStream_t s, RcclComm* comm) {
         if (comm != nullptr && c_.world > 1)
@@ -371,6 +405,8 @@ class FLEngine {
     }
 
     MLPDesc d_;
+    MLPDescB e_;
+    int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
     FLConfig c_;
     FLBuffers b_;
     float* pbuf_[2];

@@ -22,24 +22,10 @@
 // while the current one is multiplied.  The skinny classifier head (C outputs) runs on the
 // VALU with a fixed-order split-K shuffle reduction.
 #include "fl_common.h"
+#include "fl_device.h"
 #include <math.h>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-#define FL_THREADS 512
-#define FL_WAVES (FL_THREADS / 64)
-
-// In-kernel phase stamps (100 MHz s_memrealtime) for profiling; off unless b.dbg is set.
-#define FL_STAMP(i)                                                                            \
-    do {                                                                                       \
-        if (b.dbg != nullptr && threadIdx.x == 0)                                              \
-            b.dbg[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime();                   \
-    } while (0)
-
-// Workgroup barrier that orders LDS only.  __syncthreads() also waits vmcnt(0), which puts
-// every in-flight global store (the per-block gradient slab) and load on the critical path
-// of each phase; the phases here only hand data to each other through LDS.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ f32x4 mfma_f32(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -292,104 +278,6 @@ __device__ void forward_block(const MLPDesc& d, float* acts, const float* li, un
                                d.ld[l + 1], l + 1 < d.L);
         lds_barrier();
     }
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-// ---------------------------------------------------------------------------------------
-// Metrics + early stopping on the device (reference C:85-90, C:165-195).
-// ---------------------------------------------------------------------------------------
-
-// Accuracy + weighted precision / recall / F1 (zero_division=0) of a confusion matrix given
-// by an accessor cmv(t, p) (sklearn semantics, fedmi/fl/metrics.py).  No local arrays: the
-// accessor is re-read per class so nothing spills to scratch.
-template <typename CM>
-__device__ void metrics_from_cm(CM cmv, int C, double out[4]) {
-    double total = 0, tp_sum = 0;
-    for (int t = 0; t < C; ++t)
-        for (int p = 0; p < C; ++p) {
-            const double x = cmv(t, p);
-            total += x;
-            if (t == p) tp_sum += x;
-        }
-    if (total <= 0) { out[0] = out[1] = out[2] = out[3] = 0; return; }
-    double prec = 0, rec = 0, f1 = 0;
-    for (int t = 0; t < C; ++t) {
-        double support = 0, pred = 0;
-        for (int p = 0; p < C; ++p) { support += cmv(t, p); pred += cmv(p, t); }
-        const double tp = cmv(t, t);
-        const double w = support / total;
-        const double pc = pred > 0 ? tp / pred : 0.0;
-        const double rc = support > 0 ? tp / support : 0.0;
-        const double den = 2 * tp + (pred - tp) + (support - tp);
-        const double fc = den > 0 ? 2 * tp / den : 0.0;
-        prec += w * pc; rec += w * rc; f1 += w * fc;
-    }
-    out[0] = tp_sum / total; out[1] = prec; out[2] = rec; out[3] = f1;
-}
-
-// Fold the previous round's all-reduced tails into the state.  Executed by one full wave:
-// lane k computes client k's metrics, lane 0 combines them in rank order (the reference's
-// np.mean order) and applies the early-stop rule.  Returns the new state in lane 0.
-__device__ FLState finalize_state(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
-                                  const float* pg, FLState S, bool write_hist) {
-    const int lane = threadIdx.x & 63;
-    if (!S.stopped && S.next_round > S.finalized) {
-        const int r = S.next_round - 1;
-        const int C = d.dim[d.L];
-        const float* tails = pg + c.tail_off;
-        double mk[4] = {0, 0, 0, 0};
-        double lk = 0;
-        if (lane < c.world) {
-            const float* cm = tails + lane * c.tail_stride;
-            metrics_from_cm([&](int t, int p) { return (double)cm[t * C + p]; }, C, mk);
-            lk = (double)cm[C * C];
-            if (write_hist && r < c.max_rounds)
-                for (int q = 0; q < 4; ++q) b.hist_rank[((size_t)r * c.world + lane) * 4 + q] = mk[q];
-        }
-        double mean[4] = {0, 0, 0, 0};
-        double loss = 0;
-        for (int k = 0; k < c.world; ++k) {
-            for (int q = 0; q < 4; ++q) mean[q] += __shfl(mk[q], k, 64);
-            loss += __shfl(lk, k, 64);
-        }
-        if (lane != 0) return S;
-        if (c.metric_mode == 0) {
-            for (int q = 0; q < 4; ++q) mean[q] /= (double)c.world;
-        } else {
-            metrics_from_cm(
-                [&](int t, int p) {
-                    double x = 0;
-                    for (int k = 0; k < c.world; ++k) x += (double)tails[k * c.tail_stride + t * C + p];
-                    return x;
-                },
-                C, mean);
-        }
-        if (write_hist && r < c.max_rounds) {
-            for (int q = 0; q < 4; ++q) b.hist_global[(size_t)r * 4 + q] = mean[q];
-            b.hist_loss[r] = (float)(loss / (double)c.world);
-        }
-        if (c.es_enabled) {
-            bool close = S.has_prev != 0;
-            if (close)
-                for (int q = 0; q < 4; ++q)
-                    close = close && (fabs(mean[q] - S.prev[q]) <= c.atol + c.rtol * fabs(S.prev[q]));
-            if (close) {
-                S.count -= 1;
-                if (S.count == 0) { S.stopped = 1; S.stop_round = S.next_round; }
-            } else {
-                for (int q = 0; q < 4; ++q) S.prev[q] = mean[q];
-                S.has_prev = 1;
-                S.count = c.patience;
-            }
-        }
-        S.finalized = S.next_round;
-    }
-    return S;
 }
 
 // ---------------------------------------------------------------------------------------

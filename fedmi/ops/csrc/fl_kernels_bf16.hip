@@ -1,0 +1,415 @@
+// bf16-operand fused round kernels for gfx950 (BASELINE config 2: "3-layer MLP bf16").
+//
+// Same round structure, state machine, slab and Adam kernel as the fp32 path
+// (fl_kernels.hip); only the per-workgroup GEMM work changes:
+//
+//   * the fp32 parameter image (global, all-reduced in fp32) is converted to a bf16 LDS image
+//     while staging; activations and deltas live in LDS as bf16, accumulation is fp32 and the
+//     weight gradients written to the slab are fp32 (fp32 master weights + Adam state);
+//   * all GEMMs run on v_mfma_f32_16x16x32_bf16 (16x the fp32 MFMA rate per FLOP):
+//       fwd    z  = act . W^T      A = act rows (ds_read_b128), B = W rows (ds_read_b128)
+//       dgrad  D  = D' . W         A = D' rows (ds_read_b128), B = W^T  via ds_read_b64_tr_b16
+//       wgrad  dW = D'^T . act     A = D'^T, B = act^T, both via ds_read_b64_tr_b16 (K = rows)
+//     so no transposed copy of any operand is ever stored: the hardware transpose read
+//     serves the column-wise uses of the same row-major images;
+//   * with R = 16 rows per workgroup the row contraction of wgrad is 16 deep and uses
+//     v_mfma_f32_16x16x16_bf16 (one transposed read per operand).
+//
+// Reference semantics: forward/backward of MLPModel + CrossEntropyLoss
+// (FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:12-25, 63-73), evaluation C:75-91.
+#include "fl_common.h"
+#include "fl_device.h"
+#include <math.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_ptr;
+
+// fp32 -> bf16 bits, round to nearest even (finite inputs)
+__device__ __forceinline__ uint32_t bf16_bits(float x) {
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) { return bf16_bits(a) | (bf16_bits(b) << 16); }
+
+__device__ __forceinline__ bf16x8 ld128(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group passes &M[r0+q][c0+4p]; lane i of the
+// group receives M[r0+0..3][c0+i].
+__device__ __forceinline__ bf16x4 ld_tr(const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_ptr)(p));
+}
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
+    return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+__device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------
+// Staging
+// ---------------------------------------------------------------------------------------
+// fp32 global image (fl_common.h layout) -> bf16 LDS image (MLPDescB layout), 8 elements
+// (two float4 loads, one 16-byte LDS store) per item; padding comes out zero.
+__device__ void stage_image_bf16(const MLPDesc& d, const MLPDescB& e, const float* __restrict__ params,
+                                 char* lds) {
+    for (int l = 0; l < d.L; ++l) {
+        const int K = d.dim[l], N = d.dim[l + 1];
+        const int K16 = (K + 15) & ~15, N16 = (N + 15) & ~15;
+        const int ldw = fl_ldw(K);
+        const int nch = e.kp[l] >> 3, nrows = e.kp[l + 1];
+        const float* src0 = params + d.iw_off[l];
+        char* dst0 = lds + e.w_off[l];
+        for (int it = threadIdx.x; it < nrows * nch; it += FL_THREADS) {
+            const int n = it / nch, ch = it - n * nch;
+            const bool ok = n < N16 && 8 * ch < K16;
+            const float4* src = reinterpret_cast<const float4*>(src0 + (ok ? n * ldw + 8 * ch : 0));
+            const float4 lo = src[0], hi = src[1];  // unpredicated loads, selected below
+            uint4 v;
+            v.x = ok ? pack_bf16x2(lo.x, lo.y) : 0u;
+            v.y = ok ? pack_bf16x2(lo.z, lo.w) : 0u;
+            v.z = ok ? pack_bf16x2(hi.x, hi.y) : 0u;
+            v.w = ok ? pack_bf16x2(hi.z, hi.w) : 0u;
+            *reinterpret_cast<uint4*>(dst0 + (n * e.lda[l] + 8 * ch) * 2) = v;
+        }
+        float* bias = reinterpret_cast<float*>(lds + e.bias_off[l]);
+        const float* bsrc = params + d.ib_off[l];
+        for (int n = threadIdx.x; n < nrows; n += FL_THREADS) {
+            const float v = bsrc[n < N16 ? n : 0];
+            bias[n] = n < N16 ? v : 0.f;
+        }
+    }
+}
+
+template <int RT>
+__device__ void stage_rows_bf16(const float* __restrict__ X, int n_rows, int F, int row0, char* act, int kp,
+                                int lda) {
+    uint16_t* a = reinterpret_cast<uint16_t*>(act);
+    for (int idx = threadIdx.x; idx < RT * 16 * kp; idx += FL_THREADS) {
+        const int r = idx / kp, k = idx - r * kp;
+        const int row = row0 + r;
+        const bool ok = row < n_rows && k < F;
+        const float v = X[(size_t)(ok ? row : 0) * F + (ok ? k : 0)];
+        a[r * lda + k] = ok ? (uint16_t)bf16_bits(v) : (uint16_t)0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// GEMM phases (operand maps of v_mfma_f32_16x16x32_bf16: lane l holds A[l&15][8(l>>4)+j]
+// and B[8(l>>4)+j][l&15]; C/D col l&15, row 4(l>>4)+j)
+// ---------------------------------------------------------------------------------------
+
+// z = act_l . W_l^T + b_l; hidden layers: ReLU -> bf16 act_{l+1} (all kp[l+1] columns, the
+// padding comes out 0); last layer: fp32 logits [R][16].
+template <int RT>
+__device__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lr = lane & 15, lg = lane >> 4;
+    const bool last = (l + 1 == d.L);
+    const int ntiles = last ? ((d.dim[d.L] + 15) >> 4) : (e.kp[l + 1] >> 4);
+    const int ksteps = e.kp[l] >> 5;
+    const int lda = e.lda[l];
+    const char* W = lds + e.w_off[l];
+    const char* act = lds + e.act_off[l];
+    const float* bias = reinterpret_cast<const float*>(lds + e.bias_off[l]);
+    for (int nt = wave; nt < ntiles; nt += FL_WAVES) {
+        const char* wrow = W + ((nt * 16 + lr) * lda + 8 * lg) * 2;
+        const char* arow = act + (lr * lda + 8 * lg) * 2;
+        f32x4 acc[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < ksteps; ++ks) {
+            const bf16x8 bv = ld128(wrow + ks * 64);
+            bf16x8 av[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) av[rt] = ld128(arow + rt * 16 * lda * 2 + ks * 64);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(av[rt], bv, acc[rt]);
+        }
+        const int n = nt * 16 + lr;
+        const float b = bias[n];
+        if (last) {
+            float* z = reinterpret_cast<float*>(lds + e.logit_off);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) z[(rt * 16 + 4 * lg + j) * 16 + n] = acc[rt][j] + b;
+        } else {
+            uint16_t* out = reinterpret_cast<uint16_t*>(lds + e.act_off[l + 1]);
+            const int ldo = e.lda[l + 1];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    out[(rt * 16 + 4 * lg + j) * ldo + n] = (uint16_t)bf16_bits(fmaxf(acc[rt][j] + b, 0.f));
+        }
+    }
+}
+
+// dW_l[o][i] = sum_r D_{l+1}[r][o] act_l[r][i] (fp32 -> slab, dense [N][K]);
+// gb_l[o] = sum_r D_{l+1}[r][o].  Both operands are read transposed (K = rows).
+template <int RT>
+__device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, const char* lds,
+                                 float* __restrict__ gW, float* __restrict__ gb) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lr = lane & 15, lg = lane >> 4, lq = lr >> 2, lp = lr & 3;
+    const int K = d.dim[l], N = d.dim[l + 1];
+    const int otiles = (N + 15) >> 4, itiles = (K + 15) >> 4;
+    const int ldd = e.lda[l + 1], lda = e.lda[l];
+    const char* D = lds + e.dlt_off[l + 1];
+    const char* act = lds + e.act_off[l];
+    for (int t = wave; t < otiles * itiles; t += FL_WAVES) {
+        const int ot = t / itiles, it = t - ot * itiles;
+        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (RT == 2) {
+            const int r0 = 8 * lg + lq;
+            const char* pa = D + (r0 * ldd + ot * 16 + 4 * lp) * 2;
+            const char* pb = act + (r0 * lda + it * 16 + 4 * lp) * 2;
+            const bf16x8 a = cat8(ld_tr(pa), ld_tr(pa + 4 * ldd * 2));
+            const bf16x8 b = cat8(ld_tr(pb), ld_tr(pb + 4 * lda * 2));
+            acc = mfma32(a, b, acc);
+        } else {
+            const int r0 = 4 * lg + lq;
+            const bf16x4 a = ld_tr(D + (r0 * ldd + ot * 16 + 4 * lp) * 2);
+            const bf16x4 b = ld_tr(act + (r0 * lda + it * 16 + 4 * lp) * 2);
+            acc = mfma16(a, b, acc);
+        }
+        const int i = it * 16 + lr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int o = ot * 16 + 4 * lg + j;
+            if (i < K && o < N) gW[o * K + i] = acc[j];
+        }
+    }
+    const uint16_t* Dh = reinterpret_cast<const uint16_t*>(D);
+    for (int o = threadIdx.x; o < N; o += FL_THREADS) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int r = 0; r < RT * 16; r += 2) {
+            s0 += bf16_to_f32(Dh[r * ldd + o]);
+            s1 += bf16_to_f32(Dh[(r + 1) * ldd + o]);
+        }
+        gb[o] = s0 + s1;
+    }
+}
+
+// D_l[r][i] = (sum_o D_{l+1}[r][o] W_l[o][i]) * (act_l[r][i] > 0), all kp[l] columns.
+// B = W_l^T through transposed reads of the row-major W image.  Items from the last wave
+// down (pairs with wgrad's tiles handed out from wave 0 up).
+template <int RT>
+__device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds) {
+    const int wave = (FL_WAVES - 1) - (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int lr = lane & 15, lg = lane >> 4, lq = lr >> 2, lp = lr & 3;
+    const int itiles = e.kp[l] >> 4;
+    const int osteps = e.kp[l + 1] >> 5;
+    const int ldd = e.lda[l + 1], lda = e.lda[l];
+    const char* Dn = lds + e.dlt_off[l + 1];
+    const char* W = lds + e.w_off[l];
+    const uint16_t* act = reinterpret_cast<const uint16_t*>(lds + e.act_off[l]);
+    uint16_t* out = reinterpret_cast<uint16_t*>(lds + e.dlt_off[l]);
+    for (int it = wave; it < itiles; it += FL_WAVES) {
+        f32x4 acc[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const char* pw = W + ((8 * lg + lq) * lda + it * 16 + 4 * lp) * 2;
+        const char* pa = Dn + (lr * ldd + 8 * lg) * 2;
+        for (int os = 0; os < osteps; ++os) {
+            const char* pwk = pw + 32 * os * lda * 2;
+            const bf16x8 bv = cat8(ld_tr(pwk), ld_tr(pwk + 4 * lda * 2));
+            bf16x8 av[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) av[rt] = ld128(pa + rt * 16 * ldd * 2 + os * 64);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(av[rt], bv, acc[rt]);
+        }
+        const int i = it * 16 + lr;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int o = (rt * 16 + 4 * lg + j) * lda + i;
+                out[o] = act[o] != 0 && !(act[o] & 0x8000u) ? (uint16_t)bf16_bits(acc[rt][j]) : (uint16_t)0;
+            }
+    }
+}
+
+template <int RT>
+__device__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg) {
+    for (int l = 0; l < d.L; ++l) {
+        if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
+        fwd_layer_bf16<RT>(d, e, l, lds);
+        lds_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------------------
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
+                     const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    __shared__ FLState S_sh;
+    FL_STAMP(0);
+    if (threadIdx.x < 64) {  // wave 0: round bookkeeping while the other waves stage
+        FLState S0 = *st_in;
+        if (local_step == 0) {
+            S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
+            if (threadIdx.x == 0) {
+                S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
+                if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
+                if (blockIdx.x == 0) *st_out = S0;
+            }
+        }
+        if (threadIdx.x == 0) S_sh = S0;
+    }
+    const float* params = (local_step == 0) ? pg : b.local;
+    const int R = RT * 16;
+    const int row0 = blockIdx.x * R;
+    const int L = d.L;
+    const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
+    stage_image_bf16(d, e, params, lds);
+    stage_rows_bf16<RT>(b.X, c.n_rows, d.dim[0], row0, lds + e.act_off[0], e.kp[0], e.lda[0]);
+    lds_barrier();
+    FL_STAMP(1);
+    if (!S_sh.live) return;
+    float* slab = b.slab + (size_t)blockIdx.x * c.slab_stride;
+    forward_block_bf16<RT>(d, e, lds, b.dbg);
+    FL_STAMP(2);
+
+    // softmax cross-entropy (mean over the shard): D_L = (softmax - onehot) / n, bf16
+    const int C = d.dim[L];
+    const float* z = reinterpret_cast<const float*>(lds + e.logit_off);
+    uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
+    const int ldL = e.lda[L];
+    float lossv = 0.f;
+    if (threadIdx.x < R) {
+        const int r = threadIdx.x, row = row0 + r;
+        const float* zr = z + r * 16;
+        uint16_t* dr = DL + r * ldL;
+        if (row < c.n_rows) {
+            const int y = ylab;
+            float mx = zr[0];
+            for (int k = 1; k < C; ++k) mx = fmaxf(mx, zr[k]);
+            float se = 0.f;
+            for (int k = 0; k < C; ++k) se += expf(zr[k] - mx);
+            const float lse = mx + logf(se);
+            lossv = (lse - zr[y]) * c.inv_n;
+            for (int k = 0; k < C; ++k) {
+                const float p = expf(zr[k] - mx) / se;
+                dr[k] = (uint16_t)bf16_bits((p - (k == y ? 1.f : 0.f)) * c.inv_n);
+            }
+        } else {
+            for (int k = 0; k < C; ++k) dr[k] = 0;
+        }
+        for (int k = C; k < e.kp[L]; ++k) dr[k] = 0;
+    }
+    if (threadIdx.x < 64) {
+        lossv = wave_sum(lossv);
+        if (threadIdx.x == 0) slab[d.P] = lossv;
+    }
+    lds_barrier();
+    FL_STAMP(3);
+
+    // backward, top layer first, one phase per layer (wgrad_l and dgrad_l are independent)
+    for (int l = L - 1; l >= 0; --l) {
+        wgrad_layer_bf16<RT>(d, e, l, lds, slab + d.w_off[l], slab + d.b_off[l]);
+        if (l > 0) dgrad_layer_bf16<RT>(d, e, l, lds);
+        lds_barrier();
+        FL_STAMP(4 + (L - 1 - l));
+    }
+    FL_STAMP(15);
+}
+
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ params,
+                    float* __restrict__ cm_out, const FLState* __restrict__ st) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    __shared__ int cm_s[FL_MAX_CLASSES * FL_MAX_CLASSES];
+    if (st != nullptr && !st->live) return;
+    const int R = RT * 16;
+    const int row0 = blockIdx.x * R;
+    const int C = d.dim[d.L];
+    FL_STAMP(0);
+    for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
+    const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
+    stage_image_bf16(d, e, params, lds);
+    stage_rows_bf16<RT>(b.X, c.n_rows, d.dim[0], row0, lds + e.act_off[0], e.kp[0], e.lda[0]);
+    lds_barrier();
+    FL_STAMP(1);
+    forward_block_bf16<RT>(d, e, lds, nullptr);
+    FL_STAMP(2);
+    if (threadIdx.x < R) {
+        const int r = threadIdx.x, row = row0 + r;
+        if (row < c.n_rows) {
+            const float* zr = reinterpret_cast<const float*>(lds + e.logit_off) + r * 16;
+            int best = 0;
+            float bv = zr[0];
+            for (int k = 1; k < C; ++k)
+                if (zr[k] > bv) { bv = zr[k]; best = k; }
+            atomicAdd(&cm_s[ylab * C + best], 1);
+        }
+    }
+    lds_barrier();
+    for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
+        if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
+    FL_STAMP(15);
+}
+
+// ---------------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------------
+hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                                const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s) {
+    switch (c.R) {
+        case 16:
+            hipLaunchKernelGGL(fl_train_bf16_kernel<1>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
+                               pg, si, so, ls);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
+                               pg, si, so, ls);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                               const float* params, float* comm, const FLState* st, hipStream_t s) {
+    float* cm = comm + c.tail_off + c.rank * c.tail_stride;
+    const int blocks = (c.n_rows + c.R - 1) / c.R;
+    switch (c.R) {
+        case 16:
+            hipLaunchKernelGGL(fl_eval_bf16_kernel<1>, dim3(blocks), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
+                               params, cm, st);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_eval_bf16_kernel<2>, dim3(blocks), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
+                               params, cm, st);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t fl_set_lds_limit_bf16(size_t bytes) {
+    const int v = (int)bytes;
+    hipError_t r = hipSuccess;
+#define FLB_SET(fn)                                                                                     \
+    if (r == hipSuccess)                                                                                \
+    r = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, v)
+    FLB_SET(fl_train_bf16_kernel<1>); FLB_SET(fl_train_bf16_kernel<2>);
+    FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>);
+#undef FLB_SET
+    return r;
+}

@@ -305,3 +305,36 @@ def test_hip_debug_mode_and_profile():
     g = HipRoundEngine(X, y, 2, cfg, None, bad)
     with pytest.raises(FloatingPointError):
         g.run(1)
+
+
+@pytest.mark.parametrize("R", [16, 32])
+@pytest.mark.parametrize("hidden", [(50, 200), (7,), (33, 17, 9)])
+def test_bf16_engine_tracks_fp32_oracle(R, hidden):
+    """bf16 MFMA operands (fp32 accumulate / master weights): one round's update matches the
+    fp32 torch oracle to bf16 precision, and training tracks it over many rounds."""
+    X, y = make_income_like(3000, seed=5)
+    dims = [14, *hidden, 2]
+    flat = init_flat(dims, 3)
+    mk = lambda cls, **kw: cls(X, y, 2, EngineConfig(hidden=hidden, max_rounds=60, early_stop=False,
+                                                      rows_per_block=R, **kw), None, flat)
+    hb = mk(HipRoundEngine, dtype="bf16")
+    ref = mk(TorchRoundEngine)
+    hb.run(1)
+    ref.run(1)
+    d0 = flat
+    upd_b, upd_r = hb.global_flat() - d0, ref.global_flat() - d0
+    # Adam's first step is ~lr * sign(g): compare update directions
+    agree = np.mean(np.sign(upd_b) == np.sign(upd_r))
+    assert agree > 0.97, agree
+    hb.run(59)
+    ref.run(59)
+    acc_b, acc_r = hb.history()["global"][:, 0], ref.history()["global"][:, 0]
+    assert abs(acc_b[-1] - acc_r[-1]) < 0.02, (acc_b[-1], acc_r[-1])
+    assert abs(hb.history()["loss"][-1] - ref.history()["loss"][-1]) < 0.02
+
+
+def test_bf16_engine_layout_fits_two_blocks_per_cu():
+    X, y = make_income_like(500, seed=1)
+    e = HipRoundEngine(X, y, 2, EngineConfig(rows_per_block=16, dtype="bf16"), None, init_flat([14, 50, 200, 2], 0))
+    lay = e.engine.layout()
+    assert lay["dtype"] == 1 and lay["lds_bytes"] <= 80 * 1024, lay["lds_bytes"]

@@ -11,8 +11,10 @@ from fedmi.models.mlp import init_flat
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 8000
 R = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 hidden = tuple(int(h) for h in sys.argv[3].split(",")) if len(sys.argv) > 3 else (50, 200)
+dtype = sys.argv[4] if len(sys.argv) > 4 else "fp32"
 X, y = make_income_like(rows, seed=1)
-cfg = EngineConfig(hidden=hidden, max_rounds=100, rows_per_block=R, graph_rounds=0, early_stop=False)
+cfg = EngineConfig(hidden=hidden, max_rounds=100, rows_per_block=R, graph_rounds=0, early_stop=False,
+                   dtype=dtype)
 e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *hidden, 2], 0))
 e.run(3)
 nb = (rows + R - 1) // R
