@@ -4,7 +4,7 @@ One process per GPU, each GPU one federated client (the reference's mpiexec rank
 *step* is one full federated round exactly as the reference runs it
 (``FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:130-201``): a full-batch
 forward/backward + Adam step + StepLR step on the client's shard (MLP 14->50->200->2,
-fp32), local evaluation of the post-step model on the shard (forward + argmax + weighted
+bf16 MFMA operands with fp32 accumulation and fp32 master weights / Adam state by default, --dtype fp32 for exact-fp32 kernels), local evaluation of the post-step model on the shard (forward + argmax + weighted
 metrics), and the sample-size-weighted FedAvg of all clients' weights (one RCCL
 all-reduce; per-round metrics and the early-stop state ride in the same collective).
 
@@ -97,7 +97,7 @@ def main(argv=None):
     ap.add_argument("--rows-per-block", type=int, default=32)
     ap.add_argument("--graph-rounds", type=int, default=16)
     ap.add_argument("--backend", default="rccl", choices=["rccl", "nccl"])
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+    ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"],
                     help="MFMA operand type of the fused kernels (fp32 accumulate, fp32 master weights)")
     ap.add_argument("--no-convergence", action="store_true")
     a = ap.parse_args(argv)

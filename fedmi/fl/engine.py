@@ -590,6 +590,7 @@ class HipRoundEngine(RoundEngineBase):
         self.stream.synchronize()
         self.params[self.rounds_issued & 1][:self.Pimg].copy_(torch.as_tensor(dense_to_image(flat, self.dims)))
         torch.cuda.current_stream(self.device).synchronize()
+        self.engine.invalidate()
 
     def confusion(self, X=None, y=None, flat=None) -> np.ndarray:
         Xt = self.X if X is None else torch.as_tensor(np.ascontiguousarray(X, np.float32), device=self.device)
@@ -649,6 +650,7 @@ class HipRoundEngine(RoundEngineBase):
                 self.h_rank[:n * self.world * 4].copy_(torch.as_tensor(self.hist.rank[:n].reshape(-1), device=dev))
                 self.h_loss[:n].copy_(torch.as_tensor(self.hist.loss[:n], device=dev))
         self.stream.synchronize()
+        self.engine.invalidate()
         self.rounds_issued = r
         self._stopped_seen = bool(st["es"]["stopped"])
 

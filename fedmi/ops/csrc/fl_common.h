@@ -58,6 +58,9 @@ struct MLPDescB {
     int act_off[FL_MAX_LAYERS + 1];   // act_l bf16 [R][lda[l]]   (l < L)
     int dlt_off[FL_MAX_LAYERS + 1];   // D_l  bf16 [R][lda[l]]    (1 <= l <= L): dLoss/dz_l
     int logit_off;                    // fp32 [R][16] classifier logits
+    int item_base[FL_MAX_LAYERS + 1]; // packing: prefix sums of the 8-element items of each W_l
+    int param_off;                    // start of the parameter region (all W_l then all b_l):
+    int param_bytes;                  // it is stored pre-packed in global memory and staged by a copy
     int lds_bytes;
 };
 
@@ -120,6 +123,8 @@ struct FLBuffers {
     double* hist_rank;    // [max_rounds, world, 4]
     float* hist_loss;     // [max_rounds] mean CE over clients
     unsigned long long* dbg;  // optional [blocks, 16] s_memrealtime phase stamps (profiling)
+    char* pk_global;    // bf16 mode: packed LDS-layout image of the round's input weights
+    char* pk_local;     // bf16 mode: packed LDS-layout image of the local (post-Adam) weights
 };
 
 // Launchers (fl_kernels.hip). `pg` = image the round trains from (the previous round's
@@ -129,7 +134,8 @@ hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers&
                            int local_step, hipStream_t s);
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* pin, const float* anchor, float* comm,
-                          const FLState* st, int local_step, hipStream_t s);
+                          const FLState* st, int local_step, hipStream_t s,
+                          const MLPDescB* e = nullptr);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
@@ -138,10 +144,12 @@ hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffe
 // bf16-operand variants (fp32 accumulate, fp32 master weights / slab / Adam state).
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                 const float* pg, const FLState* st_in, FLState* st_out, int local_step,
-                                hipStream_t s);
+                                hipStream_t s, bool stage_local = false);
 hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_set_lds_limit_bf16(size_t bytes);
+// fp32 parameter image -> packed bf16 LDS-layout parameter region (MLPDescB)
+hipError_t fl_launch_pack_bf16(const MLPDesc& d, const MLPDescB& e, const float* params, char* out, hipStream_t s);
 // Stand-alone forward + confusion on an arbitrary row set (held-out evaluation).
 hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const int* y, int n_rows,
                                const float* params, float* cm_out, hipStream_t s);

@@ -215,9 +215,19 @@ class FLEngine {
         pbuf_[1] = as_ptr<float>(bufs["params1"].cast<uintptr_t>());
         st_[0] = as_ptr<FLState>(bufs["state0"].cast<uintptr_t>());
         st_[1] = as_ptr<FLState>(bufs["state1"].cast<uintptr_t>());
+        if (dtype_ == 1) {
+            // packed bf16 parameter regions; padding stays zero forever
+            HIP_CHECK(hipMalloc(&pk_, 2 * (size_t)e_.param_bytes));
+            HIP_CHECK(hipMemset(pk_, 0, 2 * (size_t)e_.param_bytes));
+            b_.pk_global = pk_;
+            b_.pk_local = pk_ + e_.param_bytes;
+        }
     }
 
-    ~FLEngine() { drop_graph(); }
+    ~FLEngine() {
+        drop_graph();
+        if (pk_) hipFree(pk_);
+    }
 
     // Issue rounds [r0, r0 + n): three kernels (+1 train/adam pair per extra local step)
     // and, when a communicator is attached and world > 1, one all-reduce per round.
@@ -270,6 +280,9 @@ class FLEngine {
 
     int graph_rounds() const { return graph_rounds_; }
 
+    // The host wrote the global weights (set_weights / resume): the next round repacks them.
+    void invalidate() { need_pack_ = true; }
+
     // Enable (ptr != 0) / disable in-kernel phase stamps: [blocks, 16] uint64 buffer.
     void set_debug(uintptr_t ptr) { b_.dbg = as_ptr<unsigned long long>(ptr); }
 
@@ -280,7 +293,7 @@ class FLEngine {
         float* cb = pbuf_[(r + 1) & 1];
         FLState* so = st_[(r + 1) & 1];
         if (which == 0) launch_train(pg, so, so, 1, s);
-        else if (which == 1) HIP_CHECK(fl_launch_adam(d_, c_, b_, b_.local, pg, cb, so, 1, s));
+        else if (which == 1) launch_adam(b_.local, pg, cb, so, 1, s);
         else launch_eval(b_.local, cb, so, s);
     }
 
@@ -308,7 +321,7 @@ class FLEngine {
         };
         const int ls = 1;
         timeit("train", [&] { launch_train(pg, so, so, ls, s); });
-        timeit("adam", [&] { HIP_CHECK(fl_launch_adam(d_, c_, b_, b_.local, pg, cb, so, ls, s)); });
+        timeit("adam", [&] { launch_adam(b_.local, pg, cb, so, ls, s); });
         timeit("eval", [&] { launch_eval(b_.local, cb, so, s); });
         HIP_CHECK(hipEventDestroy(e0));
         HIP_CHECK(hipEventDestroy(e1));
@@ -363,13 +376,31 @@ class FLEngine {
         for (int l = 0; l < L; ++l) e_.act_off[l] = take(R * e_.lda[l] * 2);
         for (int l = 1; l <= L; ++l) e_.dlt_off[l] = take(R * e_.lda[l] * 2);
         e_.logit_off = take(R * 16 * 4);
+        e_.param_off = off;
         for (int l = 0; l < L; ++l) e_.w_off[l] = take(e_.kp[l + 1] * e_.lda[l] * 2);
         for (int l = 0; l < L; ++l) e_.bias_off[l] = take(e_.kp[l + 1] * 4);
+        e_.param_bytes = off - e_.param_off;
         e_.lds_bytes = off;
+        e_.item_base[0] = 0;
+        for (int l = 0; l < L; ++l) e_.item_base[l + 1] = e_.item_base[l] + e_.kp[l + 1] * (e_.kp[l] >> 3);
     }
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s) {
-        if (dtype_ == 0) HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s));
-        else HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s));
+        if (dtype_ == 0) {
+            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s));
+        } else {
+            // the round's input weights -> packed bf16 image.  With one client the FedAvg
+            // output IS the local model (agg_scale = 1), which the Adam kernel already packed,
+            // so the pack is needed only after host-side weight changes; later local steps
+            // stage the Adam-packed local image too.
+            const bool solo = c_.world == 1 && c_.agg_scale == 1.0f && !need_pack_;
+            if (ls == 0 && !solo) HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
+            need_pack_ = false;
+            HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo));
+        }
+    }
+    void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
+                     hipStream_t s) {
+        HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr));
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
@@ -382,7 +413,7 @@ class FLEngine {
         FLState* so = st_[(r + 1) & 1];
         for (int ls = 0; ls < c_.local_steps; ++ls) {
             launch_train(pg, ls == 0 ? si : so, so, ls, s);
-            HIP_CHECK(fl_launch_adam(d_, c_, b_, ls == 0 ? pg : b_.local, pg, cb, so, ls, s));
+            launch_adam(ls == 0 ? pg : b_.local, pg, cb, so, ls, s);
         }
     }
     void issue_eval(int r, hipStream_t s) {
@@ -407,6 +438,8 @@ class FLEngine {
     MLPDesc d_;
     MLPDescB e_;
     int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
+    char* pk_ = nullptr;
+    bool need_pack_ = true;  // host changed the global weights: repack before the next round
     FLConfig c_;
     FLBuffers b_;
     float* pbuf_[2];
@@ -460,6 +493,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("graph_rounds", &FLEngine::graph_rounds)
         .def("time_kernels", &FLEngine::time_kernels)
         .def("set_debug", &FLEngine::set_debug)
+        .def("invalidate", &FLEngine::invalidate)
         .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);

@@ -381,7 +381,7 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
 __global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
-               const FLState* __restrict__ st, int local_step) {
+               const FLState* __restrict__ st, int local_step, MLPDescB e, int pack) {
     __shared__ float part[ADAM_WAVES][64];
     const int last_local_step = (local_step == c.local_steps - 1);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -417,18 +417,22 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     }
     const int di = blockIdx.x * 64 + lane;  // dense index
     const bool valid = di < d.P;
-    // dense index -> image index
-    int j = 0;
+    // dense index -> image index (and, in bf16 mode, -> packed bf16 LDS-layout position)
+    int j = 0, pk = 0;
+    bool is_bias = false;
     if (valid) {
         int l = 0;
         while (l + 1 < d.L && di >= d.w_off[l + 1]) ++l;
         const int K = d.dim[l];
         if (di < d.b_off[l]) {
-            const int e = di - d.w_off[l];
-            const int n = e / K, k = e - n * K;
+            const int q = di - d.w_off[l];
+            const int n = q / K, k = q - n * K;
             j = d.iw_off[l] + n * fl_ldw(K) + k;
+            pk = e.w_off[l] - e.param_off + (n * e.lda[l] + k) * 2;
         } else {
             j = d.ib_off[l] + (di - d.b_off[l]);
+            pk = e.bias_off[l] - e.param_off + (di - d.b_off[l]) * 4;
+            is_bias = true;
         }
     }
     if (!S.live) {
@@ -476,6 +480,14 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     b.m[j] = m;
     b.v[j] = v;
     b.local[j] = p;
+    if (pack) {
+        if (is_bias) {
+            *reinterpret_cast<float*>(b.pk_local + pk) = p;
+        } else {
+            const uint32_t u = __float_as_uint(p);
+            *reinterpret_cast<uint16_t*>(b.pk_local + pk) = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+        }
+    }
     if (last_local_step) comm[j] = p * c.agg_scale;
 }
 
@@ -611,10 +623,13 @@ hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers&
 }
 
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
-                          const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s) {
+                          const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s,
+                          const MLPDescB* e) {
     const int blocks = (d.P + 63) / 64 + 1;
+    MLPDescB ee = {};
+    if (e != nullptr) ee = *e;
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
-                       local_step);
+                       local_step, ee, e != nullptr ? 1 : 0);
     return hipGetLastError();
 }
 

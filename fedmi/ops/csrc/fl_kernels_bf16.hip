@@ -56,36 +56,48 @@ __device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
 // ---------------------------------------------------------------------------------------
 // Staging
 // ---------------------------------------------------------------------------------------
-// fp32 global image (fl_common.h layout) -> bf16 LDS image (MLPDescB layout), 8 elements
-// (two float4 loads, one 16-byte LDS store) per item; padding comes out zero.
-__device__ void stage_image_bf16(const MLPDesc& d, const MLPDescB& e, const float* __restrict__ params,
-                                 char* lds) {
-    for (int l = 0; l < d.L; ++l) {
-        const int K = d.dim[l], N = d.dim[l + 1];
-        const int K16 = (K + 15) & ~15, N16 = (N + 15) & ~15;
-        const int ldw = fl_ldw(K);
-        const int nch = e.kp[l] >> 3, nrows = e.kp[l + 1];
-        const float* src0 = params + d.iw_off[l];
-        char* dst0 = lds + e.w_off[l];
-        for (int it = threadIdx.x; it < nrows * nch; it += FL_THREADS) {
-            const int n = it / nch, ch = it - n * nch;
-            const bool ok = n < N16 && 8 * ch < K16;
-            const float4* src = reinterpret_cast<const float4*>(src0 + (ok ? n * ldw + 8 * ch : 0));
-            const float4 lo = src[0], hi = src[1];  // unpredicated loads, selected below
-            uint4 v;
-            v.x = ok ? pack_bf16x2(lo.x, lo.y) : 0u;
-            v.y = ok ? pack_bf16x2(lo.z, lo.w) : 0u;
-            v.z = ok ? pack_bf16x2(hi.x, hi.y) : 0u;
-            v.w = ok ? pack_bf16x2(hi.z, hi.w) : 0u;
-            *reinterpret_cast<uint4*>(dst0 + (n * e.lda[l] + 8 * ch) * 2) = v;
+// fp32 global image (fl_common.h layout) -> packed bf16 parameter region (MLPDescB layout,
+// W_l then b_l, byte offsets relative to param_off).  One thread per 8-element item (two
+// float4 loads, one 16-byte store); rows/columns of padding come out zero.
+__global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restrict__ params, char* __restrict__ out) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    const int total = e.item_base[d.L];
+    if (id < total) {
+        int l = 0;
+#pragma unroll
+        for (int q = 1; q < FL_MAX_LAYERS; ++q) l += (q < d.L && id >= e.item_base[q]) ? 1 : 0;
+        const int loc = id - e.item_base[l];
+        const int nch = e.kp[l] >> 3;
+        const int n = loc / nch, ch = loc - n * nch;
+        const int K16 = (d.dim[l] + 15) & ~15, N16 = (d.dim[l + 1] + 15) & ~15;
+        const bool ok = n < N16 && 8 * ch < K16;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (ok) {
+            const float4* src = reinterpret_cast<const float4*>(params + d.iw_off[l] + n * fl_ldw(d.dim[l]) + 8 * ch);
+            const float4 lo = src[0], hi = src[1];
+            v = make_uint4(pack_bf16x2(lo.x, lo.y), pack_bf16x2(lo.z, lo.w), pack_bf16x2(hi.x, hi.y),
+                           pack_bf16x2(hi.z, hi.w));
         }
-        float* bias = reinterpret_cast<float*>(lds + e.bias_off[l]);
-        const float* bsrc = params + d.ib_off[l];
-        for (int n = threadIdx.x; n < nrows; n += FL_THREADS) {
-            const float v = bsrc[n < N16 ? n : 0];
-            bias[n] = n < N16 ? v : 0.f;
-        }
+        *reinterpret_cast<uint4*>(out + e.w_off[l] - e.param_off + (n * e.lda[l] + 8 * ch) * 2) = v;
+        return;
     }
+    int bid = id - total;
+    for (int l = 0; l < d.L; ++l) {
+        if (bid < e.kp[l + 1]) {
+            const int N16 = (d.dim[l + 1] + 15) & ~15;
+            reinterpret_cast<float*>(out + e.bias_off[l] - e.param_off)[bid] = bid < N16 ? params[d.ib_off[l] + bid] : 0.f;
+            return;
+        }
+        bid -= e.kp[l + 1];
+    }
+}
+
+// Stage the packed parameter region: a straight 16-byte copy (the padding is already zero).
+__device__ __forceinline__ void stage_params_bf16(const MLPDescB& e, const char* __restrict__ packed, char* lds) {
+    const uint4* src = reinterpret_cast<const uint4*>(packed);
+    uint4* dst = reinterpret_cast<uint4*>(lds + e.param_off);
+    const int n16 = e.param_bytes >> 4;
+    for (int i = threadIdx.x; i < n16; i += FL_THREADS) dst[i] = src[i];
 }
 
 template <int RT>
@@ -255,7 +267,8 @@ __device__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* ld
 template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
-                     const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step) {
+                     const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
+                     int stage_local) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
@@ -276,8 +289,18 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     const int row0 = blockIdx.x * R;
     const int L = d.L;
     const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
-    stage_image_bf16(d, e, params, lds);
+    stage_params_bf16(e, (local_step == 0 && !stage_local) ? b.pk_global : b.pk_local, lds);
+    FL_STAMP(8);
     stage_rows_bf16<RT>(b.X, c.n_rows, d.dim[0], row0, lds + e.act_off[0], e.kp[0], e.lda[0]);
+    {   // padding columns [C, kp[L]) of D_L never change: zero them here, off the CE's path
+        const int C = d.dim[L], padc = e.kp[L] - d.dim[L];
+        uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
+        for (int i = threadIdx.x; i < R * padc; i += FL_THREADS) {
+            const int r = i / padc;
+            DL[r * e.lda[L] + C + (i - r * padc)] = 0;
+        }
+    }
+    FL_STAMP(9);
     lds_barrier();
     FL_STAMP(1);
     if (!S_sh.live) return;
@@ -310,7 +333,6 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
         } else {
             for (int k = 0; k < C; ++k) dr[k] = 0;
         }
-        for (int k = C; k < e.kp[L]; ++k) dr[k] = 0;
     }
     if (threadIdx.x < 64) {
         lossv = wave_sum(lossv);
@@ -342,8 +364,10 @@ fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float*
     FL_STAMP(0);
     for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
     const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
-    stage_image_bf16(d, e, params, lds);
+    stage_params_bf16(e, params == b.local ? b.pk_local : b.pk_global, lds);
+    FL_STAMP(8);
     stage_rows_bf16<RT>(b.X, c.n_rows, d.dim[0], row0, lds + e.act_off[0], e.kp[0], e.lda[0]);
+    FL_STAMP(9);
     lds_barrier();
     FL_STAMP(1);
     forward_block_bf16<RT>(d, e, lds, nullptr);
@@ -369,15 +393,16 @@ fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float*
 // Launchers
 // ---------------------------------------------------------------------------------------
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
-                                const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s) {
+                                const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
+                                bool stage_local) {
     switch (c.R) {
         case 16:
             hipLaunchKernelGGL(fl_train_bf16_kernel<1>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
-                               pg, si, so, ls);
+                               pg, si, so, ls, stage_local ? 1 : 0);
             break;
         case 32:
             hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
-                               pg, si, so, ls);
+                               pg, si, so, ls, stage_local ? 1 : 0);
             break;
         default: return hipErrorInvalidValue;
     }
@@ -399,6 +424,14 @@ hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConf
             break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t fl_launch_pack_bf16(const MLPDesc& d, const MLPDescB& e, const float* params, char* out, hipStream_t s) {
+    int bias_items = 0;
+    for (int l = 0; l < d.L; ++l) bias_items += e.kp[l + 1];
+    const int n = e.item_base[d.L] + bias_items;
+    hipLaunchKernelGGL(fl_pack_bf16_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, e, params, out);
     return hipGetLastError();
 }
 

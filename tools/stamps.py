@@ -19,7 +19,7 @@ e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *hidden, 2], 0))
 e.run(3)
 nb = (rows + R - 1) // R
 dbg = torch.zeros(nb * 16, dtype=torch.int64, device=e.device)
-order = [0, 1, 10, 11, 12, 2, 3, 4, 5, 6, 7, 15]
+order = [0, 8, 9, 1, 10, 11, 12, 2, 3, 4, 5, 6, 7, 15]
 for which, name in ((0, "train"), (2, "eval")):
     for rep in range(5):
         dbg.zero_()
