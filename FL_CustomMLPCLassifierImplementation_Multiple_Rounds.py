@@ -55,7 +55,7 @@ def parse_args(argv=None):
     ap.add_argument("--engine", default="auto", help="hip | torch")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
                     help="MFMA operand type of the fused HIP kernels (fp32 accumulate either way)")
-    ap.add_argument("--rows-per-block", type=int, default=32)
+    ap.add_argument("--rows-per-block", type=int, default=0, help="rows per workgroup: 16 | 32 | 0 = auto")
     ap.add_argument("--graph-rounds", type=int, default=16)
     ap.add_argument("--jsonl", default=None, help="append per-round metrics as JSON lines")
     ap.add_argument("--save", default=None, help="checkpoint directory written at the end (reference weight layout)")

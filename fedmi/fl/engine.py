@@ -49,7 +49,7 @@ class EngineConfig:
     rtol: float = 1e-5
     max_rounds: int = 300
     metric_mode: str = "mean"       # 'mean' (C:169) | 'pooled' (S:130)
-    rows_per_block: int = 32        # R rows per workgroup of the fused kernels
+    rows_per_block: int = 0         # R rows per workgroup of the fused kernels (16 | 32; 0 = auto)
     graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
     seed: int = 0
     debug: bool = False             # eager, synchronised phases + non-finite checks every round
@@ -356,7 +356,11 @@ class HipRoundEngine(RoundEngineBase):
     """Device-resident client.  ``X``/``y`` may be numpy arrays (uploaded once) or CUDA
     tensors already on the device (e.g. from the synthetic generator)."""
 
-    def __init__(self, X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None, device=None):
+    def __init__(self, X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None, device=None,
+                 comm_buffers=None):
+        """``comm_buffers``: optional pair of float32 device views of length
+        :meth:`comm_len` to use as the double-buffered FedAvg buffers (trial packing shares one
+        all-reduce between engines by handing each a slice of one allocation)."""
         from ..ops import native
         self.m = native()
         if device is None:
@@ -372,19 +376,25 @@ class HipRoundEngine(RoundEngineBase):
         f32 = dict(dtype=torch.float32, device=dev)
         self.X = (X if isinstance(X, torch.Tensor) else torch.as_tensor(np.ascontiguousarray(X, np.float32))).to(**f32).contiguous()
         self.y = (y if isinstance(y, torch.Tensor) else torch.as_tensor(np.asarray(y))).to(dtype=torch.int32, device=dev).contiguous()
-        R = int(cfg.rows_per_block)
-        self.R = R
-        n_slabs = (self.n_local + R - 1) // R
+        # rows per workgroup: 0 = auto (32 when the model's LDS image fits, else 16)
+        R_try = [32, 16] if int(cfg.rows_per_block) == 0 else [int(cfg.rows_per_block)]
+        R = R_try[0]
         slab_stride = ((self.P + 1) + 3) & ~3
         # device parameter buffers use the padded image layout (fl_common.h)
         self.Pimg = image_layout(self.dims)[2]
         comm_len = self.Pimg + self.world * self.tail_stride
-        self.params = [torch.zeros(comm_len, **f32), torch.zeros(comm_len, **f32)]
+        if comm_buffers is None:
+            self.params = [torch.zeros(comm_len, **f32), torch.zeros(comm_len, **f32)]
+        else:
+            self.params = list(comm_buffers)
+            for t in self.params:
+                if t.numel() != comm_len or t.dtype != torch.float32 or t.device != dev:
+                    raise ValueError("comm_buffers must be two float32 views of comm_len() on the engine device")
+                t.zero_()
         self.params[0][:self.Pimg] = torch.as_tensor(dense_to_image(init_flat, self.dims))
         self.local = self.params[0][:self.Pimg].clone()
         self.mom = torch.zeros(self.Pimg, **f32)
         self.vel = torch.zeros(self.Pimg, **f32)
-        self.slab = torch.zeros(n_slabs * slab_stride, **f32)
         sb = self.m.STATE_BYTES
         assert sb == _STATE_DTYPE.itemsize, (sb, _STATE_DTYPE.itemsize)
         init = np.zeros(1, dtype=_STATE_DTYPE)
@@ -406,14 +416,24 @@ class HipRoundEngine(RoundEngineBase):
             "dtype": _dtype_id(cfg.dtype),
         }
         bufs = {
-            "X": self.X.data_ptr(), "y": self.y.data_ptr(), "slab": self.slab.data_ptr(),
+            "X": self.X.data_ptr(), "y": self.y.data_ptr(),
             "local": self.local.data_ptr(), "m": self.mom.data_ptr(), "v": self.vel.data_ptr(),
             "hist_global": self.h_global.data_ptr(), "hist_rank": self.h_rank.data_ptr(),
             "hist_loss": self.h_loss.data_ptr(), "params0": self.params[0].data_ptr(),
             "params1": self.params[1].data_ptr(), "state0": self.state[0].data_ptr(),
             "state1": self.state[1].data_ptr(),
         }
-        self.engine = self.m.FLEngine(self.dims, ecfg, bufs)
+        for i, R in enumerate(R_try):
+            self.slab = torch.zeros(((self.n_local + R - 1) // R) * slab_stride, **f32)
+            ecfg["R"] = R
+            bufs["slab"] = self.slab.data_ptr()
+            try:
+                self.engine = self.m.FLEngine(self.dims, ecfg, bufs)
+                break
+            except RuntimeError as err:
+                if "LDS" not in str(err) or i + 1 == len(R_try):
+                    raise
+        self.R = R
         self.layout = self.engine.layout()
         iw, ib, _ = image_layout(self.dims)
         if (self.layout["Pimg"], list(self.layout["iw_off"]), list(self.layout["ib_off"])) != (self.Pimg, iw, ib):
@@ -666,6 +686,12 @@ def _check_finite(r: int, what: str, t: torch.Tensor) -> None:
     if not bool(torch.isfinite(t).all()):
         bad = int((~torch.isfinite(t)).sum())
         raise FloatingPointError(f"round {r}: {bad} non-finite values in {what}")
+
+
+def comm_len(dims: Sequence[int], world: int) -> int:
+    """Floats in one FedAvg buffer of the HIP engine: parameter image + per-rank tails."""
+    n_classes = int(dims[-1])
+    return image_layout(list(dims))[2] + world * (n_classes * n_classes + 1)
 
 
 class _ShapeOnly:

@@ -1,0 +1,157 @@
+"""Federated hyperparameter sweep over the round engine with concurrent trials per GPU
+(BASELINE config 5: "8 clients x {lr, local_epochs, hidden_dim} grid, concurrent trials
+packed per GPU").
+
+The reference's sweep ([H], ``hyperparameters_tuning.py:68-132``) is sklearn-based and
+strictly sequential: each of its 90 trials is fitted, averaged and scored before the next
+starts (SURVEY §2.5 "Trial parallelism: no").  Here a *trial* is a full multi-round FedAvg
+run of the [C] workload (``FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:122-207``)
+with its own hidden sizes, learning rate and local steps per round, and a
+:class:`FedTrialGroup` runs K trials concurrently on every GPU:
+
+* each trial is a fused :class:`~fedmi.fl.engine.HipRoundEngine` on its own HIP stream, so
+  the small per-trial kernels of different trials overlap on the CUs;
+* all trials' FedAvg buffers are slices of ONE device allocation, so a round of all K
+  trials costs one all-reduce (the per-trial weights, metric tails and early-stop inputs
+  ride together), instead of K latency-bound collectives;
+* each trial keeps its own device-side early-stop state; a stopped trial's rounds are exact
+  no-ops inside the shared collective.
+
+On CPU (gloo plumbing config) trials fall back to :class:`~fedmi.fl.engine.TorchRoundEngine`
+run one after another with their own all-reduces.
+"""
+from __future__ import annotations
+
+import itertools
+from dataclasses import dataclass, field, replace
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..fl.engine import EngineConfig, HipRoundEngine, TorchRoundEngine, comm_len
+from ..fl.metrics import METRIC_NAMES
+from ..models.mlp import init_flat
+
+DEFAULT_HIDDEN: Tuple[Tuple[int, ...], ...] = ((50, 200), (100, 50), (50, 400))
+DEFAULT_LRS: Tuple[float, ...] = (0.002, 0.004, 0.01)
+DEFAULT_LOCAL_STEPS: Tuple[int, ...] = (1, 2)
+
+
+@dataclass
+class FedTrial:
+    hidden: Tuple[int, ...]
+    lr: float
+    local_steps: int
+    history: dict = field(default_factory=dict, repr=False)
+
+    @property
+    def final(self) -> Dict[str, float]:
+        g = self.history.get("global")
+        if g is None or len(g) == 0:
+            return {k: float("nan") for k in METRIC_NAMES}
+        return {k: float(g[-1][i]) for i, k in enumerate(METRIC_NAMES)}
+
+    @property
+    def rounds_run(self) -> int:
+        return int(self.history.get("rounds_run", 0))
+
+
+def grid(hidden: Sequence[Sequence[int]] = DEFAULT_HIDDEN, lrs: Sequence[float] = DEFAULT_LRS,
+         local_steps: Sequence[int] = DEFAULT_LOCAL_STEPS) -> List[FedTrial]:
+    return [FedTrial(tuple(int(x) for x in h), float(lr), int(ls))
+            for h, lr, ls in itertools.product(hidden, lrs, local_steps)]
+
+
+class FedTrialGroup:
+    """K federated trials on this client's shard, advanced in lock-step rounds."""
+
+    def __init__(self, X, y, n_classes: int, trials: Sequence[FedTrial], comm, base: EngineConfig,
+                 n_total: Optional[int] = None, backend: str = "auto", seed: int = 0):
+        self.trials = list(trials)
+        self.comm = comm
+        self.world = comm.size if comm is not None else 1
+        rank = comm.rank if comm is not None else 0
+        if backend == "auto":
+            backend = "hip" if torch.cuda.is_available() and (comm is None or comm.device.type == "cuda") else "torch"
+        self.backend = backend
+        F = int(X.shape[1])
+        self.engines = []
+        self.buffers = None
+        cfgs = [replace(base, hidden=t.hidden, lr=t.lr, local_steps=t.local_steps) for t in self.trials]
+        flats = [init_flat([F, *t.hidden, n_classes], seed * 1000003 + rank) for t in self.trials]
+        if backend == "hip":
+            dev = comm.device if comm is not None else torch.device("cuda", torch.cuda.current_device())
+            lens = [comm_len([F, *t.hidden, n_classes], self.world) for t in self.trials]
+            offs = np.concatenate([[0], np.cumsum([(n + 63) & ~63 for n in lens])]).astype(np.int64)
+            self.buffers = [torch.zeros(int(offs[-1]), dtype=torch.float32, device=dev) for _ in range(2)]
+            for i, (cfg, flat) in enumerate(zip(cfgs, flats)):
+                views = (self.buffers[0][offs[i]:offs[i] + lens[i]], self.buffers[1][offs[i]:offs[i] + lens[i]])
+                self.engines.append(HipRoundEngine(X, y, n_classes, cfg, comm, flat, n_total=n_total, device=dev,
+                                                   comm_buffers=views))
+            self.stream = torch.cuda.Stream(device=dev)
+            self._native = comm.native if (comm is not None and self.world > 1) else None
+        elif backend == "torch":
+            for cfg, flat in zip(cfgs, flats):
+                self.engines.append(TorchRoundEngine(X, y, n_classes, cfg, comm, flat, n_total=n_total))
+        else:
+            raise ValueError(f"unknown backend {backend!r}")
+        self.rounds_issued = 0
+
+    def _round_hip(self, r: int) -> None:
+        # fork: every trial's train/adam/eval on its own stream
+        for e in self.engines:
+            e.stream.wait_stream(self.stream)
+            e.engine.run_local(r, e._stream())
+        # join + one all-reduce over all trials' buffers
+        for e in self.engines:
+            self.stream.wait_stream(e.stream)
+        if self.world > 1:
+            buf = self.buffers[(r + 1) & 1]
+            with torch.cuda.stream(self.stream):
+                if self._native is not None:
+                    self._native.allreduce_f32(buf.data_ptr(), buf.numel(), self.stream.cuda_stream)
+                else:
+                    self.comm.allreduce_(buf)
+        for e in self.engines:
+            e.rounds_issued = r + 1
+
+    def run(self, n_rounds: int) -> None:
+        """Run ``n_rounds`` rounds of every trial (trials that stopped early idle)."""
+        n_rounds = min(n_rounds, min(e.cfg.max_rounds for e in self.engines) - self.rounds_issued)
+        if self.backend == "hip":
+            for r in range(self.rounds_issued, self.rounds_issued + n_rounds):
+                self._round_hip(r)
+            self.stream.synchronize()
+            for e in self.engines:
+                e.stream.wait_stream(self.stream)
+                e.sync_history()
+        else:
+            for e in self.engines:
+                e.run(n_rounds)
+        self.rounds_issued += n_rounds
+        for t, e in zip(self.trials, self.engines):
+            t.history = e.history()
+
+    def best(self, key: str = "accuracy") -> FedTrial:
+        i = METRIC_NAMES.index(key)
+        return max(self.trials, key=lambda t: (t.history["global"][-1][i] if t.rounds_run else -1.0))
+
+
+def run_fed_sweep(X_local, y_local, n_classes: int, comm, trials: Sequence[FedTrial], rounds: int = 50,
+                  trials_per_gpu: int = 6, base: Optional[EngineConfig] = None, n_total: Optional[int] = None,
+                  backend: str = "auto", seed: int = 0, on_group=None) -> Tuple[FedTrial, List[FedTrial]]:
+    """Run ``trials`` in groups of ``trials_per_gpu`` concurrent trials; returns (best, all)."""
+    base = base or EngineConfig()
+    base = replace(base, max_rounds=max(base.max_rounds, rounds))
+    done: List[FedTrial] = []
+    for g0 in range(0, len(trials), trials_per_gpu):
+        group = FedTrialGroup(X_local, y_local, n_classes, trials[g0:g0 + trials_per_gpu], comm, base,
+                              n_total=n_total, backend=backend, seed=seed)
+        group.run(rounds)
+        done.extend(group.trials)
+        if on_group is not None:
+            on_group(group)
+    i = METRIC_NAMES.index("accuracy")
+    best = max(done, key=lambda t: (t.history["global"][-1][i] if t.rounds_run else -1.0))
+    return best, done

@@ -10,7 +10,13 @@ Defaults to ``balanced_income_data.csv`` / ``income`` with ``StandardScaler(with
 On a GPU the 9 learning rates of each hidden config train as one packed job
 (``fedmi.hpo.sweep``).  ``--hidden`` / ``--lrs`` narrow the grid.
 
+``--federated`` switches to the round-engine sweep of BASELINE config 5 (``fedmi.hpo.fed_sweep``):
+a {hidden} x {lr} x {local steps per round} grid of multi-round FedAvg trials of the [C]
+workload, ``--trials-per-gpu`` of them running concurrently on every GPU and sharing one
+all-reduce per round.
+
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 hyperparameters_tuning.py
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 hyperparameters_tuning.py --federated --rounds 50
 """
 from __future__ import annotations
 
@@ -41,7 +47,14 @@ def main(argv=None):
     ap.add_argument("--no-pack", action="store_true", help="fit trials one by one")
     ap.add_argument("--quiet", action="store_true", help="only print the best result")
     ap.add_argument("--json", default=None, help="write all trial results here (rank 0)")
+    ap.add_argument("--federated", action="store_true",
+                    help="round-engine sweep over hidden x lr x local steps (BASELINE config 5)")
+    ap.add_argument("--local-steps", type=int, nargs="+", default=None, help="--federated: local steps grid")
+    ap.add_argument("--trials-per-gpu", type=int, default=6, help="--federated: concurrent trials per GPU")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32", help="--federated: engine MFMA dtype")
     a = ap.parse_args(argv)
+    if a.federated:
+        return federated_main(a)
     comm = get_world(backend="gloo" if a.device == "cpu" else "auto", device=a.device)
     rank = comm.Get_rank()
     ds = load_tabular(a.data, label=a.label, with_mean=False)
@@ -86,6 +99,40 @@ def main(argv=None):
                             "n_iter": r.n_iter} for r in results] + [{"wall_s": wall}], f)
     comm.close()
     return best, results
+
+
+def federated_main(a):
+    """BASELINE config 5: federated {hidden, lr, local steps} sweep with packed trials."""
+    from fedmi.fl.engine import EngineConfig
+    from fedmi.hpo.fed_sweep import DEFAULT_HIDDEN, DEFAULT_LOCAL_STEPS, DEFAULT_LRS, grid, run_fed_sweep
+    comm = get_world(backend="gloo" if a.device == "cpu" else "auto", device=a.device)
+    rank, size = comm.Get_rank(), comm.Get_size()
+    ds = load_tabular(a.data, label=a.label, with_mean=True)
+    X_local, y_local = split_data(ds.X_train, ds.y_train, rank, size, mode="iid", seed=0)
+    hidden = ast.literal_eval(a.hidden) if a.hidden else DEFAULT_HIDDEN
+    trials = grid(hidden, tuple(a.lrs) if a.lrs else DEFAULT_LRS,
+                  tuple(a.local_steps) if a.local_steps else DEFAULT_LOCAL_STEPS)
+    rounds = a.rounds if a.rounds > 1 else 50
+    base = EngineConfig(max_rounds=rounds, dtype=a.dtype, graph_rounds=0)
+    t0 = time.time()
+    best, done = run_fed_sweep(X_local, y_local, 2, comm, trials, rounds=rounds, trials_per_gpu=a.trials_per_gpu,
+                               base=base, backend="torch" if a.device == "cpu" else "auto")
+    wall = time.time() - t0
+    if rank == 0:
+        for t in done:
+            if not a.quiet:
+                print(f"Trial hidden={t.hidden} lr={t.lr} local_steps={t.local_steps}: rounds={t.rounds_run} "
+                      + ", ".join(f"{k}: {v:.4f}" for k, v in t.final.items()), flush=True)
+        print(f"\nBest Global Hyperparameters: hidden={best.hidden} lr={best.lr} local_steps={best.local_steps}")
+        print(f"Best Global Metrics: {best.final}")
+        print(f"\nfederated sweep wall time: {wall:.2f} s for {len(done)} trials x {rounds} rounds "
+              f"({a.trials_per_gpu} concurrent per GPU, {size} clients)", flush=True)
+        if a.json:
+            with open(a.json, "w") as f:
+                json.dump([{"hidden": t.hidden, "lr": t.lr, "local_steps": t.local_steps, "rounds": t.rounds_run,
+                            "final": t.final} for t in done] + [{"wall_s": wall}], f)
+    comm.close()
+    return best, done
 
 
 if __name__ == "__main__":

@@ -1,0 +1,67 @@
+"""Federated hyperparameter sweep with concurrent trials (BASELINE config 5)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from fedmi.data.synthetic import make_income_like
+from fedmi.fl.engine import EngineConfig, HipRoundEngine, TorchRoundEngine
+from fedmi.hpo.fed_sweep import FedTrial, FedTrialGroup, grid, run_fed_sweep
+from fedmi.models.mlp import init_flat
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_grid_is_full_product():
+    g = grid([(8,), (16, 4)], [0.01, 0.02, 0.03], [1, 2])
+    assert len(g) == 12
+    assert {(t.hidden, t.lr, t.local_steps) for t in g} == {
+        (h, lr, ls) for h in [(8,), (16, 4)] for lr in [0.01, 0.02, 0.03] for ls in [1, 2]}
+
+
+def test_cpu_group_matches_standalone_engines():
+    X, y = make_income_like(600, seed=4)
+    trials = grid([(8,), (12, 6)], [0.004, 0.02], [1, 2])
+    base = EngineConfig(max_rounds=6, early_stop=False)
+    best, done = run_fed_sweep(X, y, 2, None, trials, rounds=6, trials_per_gpu=3, base=base, backend="torch")
+    assert len(done) == 8 and all(t.rounds_run == 6 for t in done)
+    t = done[5]
+    cfg = EngineConfig(hidden=t.hidden, lr=t.lr, local_steps=t.local_steps, max_rounds=6, early_stop=False)
+    e = TorchRoundEngine(X, y, 2, cfg, None, init_flat([14, *t.hidden, 2], 0))
+    e.run(6)
+    np.testing.assert_array_equal(e.history()["global"], t.history["global"])
+    assert best.final["accuracy"] == max(x.final["accuracy"] for x in done)
+
+
+def test_federated_sweep_entrypoint_two_clients_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29633", os.path.join(REPO, "hyperparameters_tuning.py"),
+           "--federated", "--device", "cpu", "--rounds", "4", "--hidden", "[(8,)]", "--lrs", "0.004", "0.01",
+           "--local-steps", "1", "2", "--trials-per-gpu", "2", "--quiet",
+           "--data", os.path.join(REPO, "data", "balanced_income_data.csv")]
+    p = subprocess.run(cmd, cwd=REPO, env=dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1"),
+                       capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "Best Global Hyperparameters" in p.stdout
+    assert "4 trials x 4 rounds" in p.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_hip_group_matches_standalone_engines(dtype):
+    X, y = make_income_like(3000, seed=4)
+    trials = grid([(50, 200), (16,)], [0.004, 0.01], [1, 2])
+    base = EngineConfig(max_rounds=12, early_stop=True, patience=3, tolerance=5e-3, dtype=dtype, graph_rounds=0)
+    g = FedTrialGroup(X, y, 2, trials, None, base, backend="hip")
+    g.run(12)
+    for t in (trials[0], trials[5], trials[7]):
+        cfg = EngineConfig(hidden=t.hidden, lr=t.lr, local_steps=t.local_steps, max_rounds=12, early_stop=True,
+                           patience=3, tolerance=5e-3, dtype=dtype, graph_rounds=0)
+        e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *t.hidden, 2], 0))
+        e.run(12)
+        h = e.history()
+        assert h["rounds_run"] == t.history["rounds_run"] and h["stop_round"] == t.history["stop_round"]
+        np.testing.assert_array_equal(h["global"], t.history["global"])
