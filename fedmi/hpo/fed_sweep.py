@@ -33,7 +33,7 @@ from ..fl.engine import EngineConfig, HipRoundEngine, TorchRoundEngine, comm_len
 from ..fl.metrics import METRIC_NAMES
 from ..models.mlp import init_flat
 
-DEFAULT_HIDDEN: Tuple[Tuple[int, ...], ...] = ((50, 200), (100, 50), (50, 400))
+DEFAULT_HIDDEN: Tuple[Tuple[int, ...], ...] = ((50, 200), (100, 50), (50, 100))  # fit the fused engine in fp32 and bf16
 DEFAULT_LRS: Tuple[float, ...] = (0.002, 0.004, 0.01)
 DEFAULT_LOCAL_STEPS: Tuple[int, ...] = (1, 2)
 
