@@ -96,7 +96,8 @@ def main(argv=None):
     ap.add_argument("--hidden", type=int, nargs="+", default=[50, 200])
     ap.add_argument("--rows-per-block", type=int, default=32)
     ap.add_argument("--graph-rounds", type=int, default=16)
-    ap.add_argument("--backend", default="rccl", choices=["rccl", "nccl"])
+    ap.add_argument("--backend", default="xgmi", choices=["xgmi", "rccl", "nccl"],
+                    help="FedAvg data plane: one-shot xGMI peer all-reduce (falls back to RCCL) | RCCL | torch nccl")
     ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"],
                     help="MFMA operand type of the fused kernels (fp32 accumulate, fp32 master weights)")
     ap.add_argument("--no-convergence", action="store_true")
@@ -159,7 +160,7 @@ def main(argv=None):
             "data": f"synthetic income-shaped (device Philox), {a.rows_per_client} rows/client; random-init weights",
             "config": {"model": f"MLP {'-'.join(map(str, dims))} (reference [C])",
                        "global_batch": a.rows_per_client * N, "seq_len": 1,
-                       "parallelism": f"fedavg{N} (1 client/GPU, RCCL all-reduce)",
+                       "parallelism": f"fedavg{N} (1 client/GPU, {eng.aggregation} all-reduce)",
                        "rows_per_client": a.rows_per_client, "optimizer": "Adam(0.004)+StepLR(30,0.5)"},
             "samples_per_sec_per_client": value / N,
             "final_train_acc_synthetic": float(h["global"][-1][0]),

@@ -54,6 +54,10 @@ class EngineConfig:
     seed: int = 0
     debug: bool = False             # eager, synchronised phases + non-finite checks every round
     dtype: str = "fp32"             # MFMA operand type of the fused kernels: 'fp32' | 'bf16'
+    # one client: score round r's post-step model inside round r+1's train kernel (its forward
+    # pass IS that evaluation, FedAvg of one client being the identity) instead of a separate
+    # eval kernel; metrics, history and early stop are unchanged (fl_common.h FL_EVAL_FUSED)
+    fused_eval: bool = True
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -414,6 +418,8 @@ class HipRoundEngine(RoundEngineBase):
             "early_stop": bool(cfg.early_stop), "patience": int(cfg.patience), "atol": float(cfg.tolerance),
             "rtol": float(cfg.rtol), "max_rounds": mr, "metric_mode": _metric_mode_id(cfg.metric_mode),
             "dtype": _dtype_id(cfg.dtype),
+            # trial packing runs rounds through run_local + a shared all-reduce: classic rounds
+            "fused_eval": bool(cfg.fused_eval) and comm_buffers is None,
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),
@@ -444,11 +450,41 @@ class HipRoundEngine(RoundEngineBase):
         self.rounds_issued = 0
         self._stopped_seen = False
         self._native_comm = comm.native if (comm is not None and self.world > 1) else None
+        # one-shot xGMI all-reduce of [image | tails] (collective set-up; None -> RCCL)
+        self._peer = None
+        if self.world > 1 and comm_buffers is None and getattr(comm, "peer_allreduce", False):
+            from ..parallel.peer import make_peer_allreduce
+            torch.cuda.synchronize(dev)
+            self._peer = make_peer_allreduce(comm, comm_len, dev)
+            if self._peer is not None:
+                self.engine.attach_peer(self._peer)
         self._graph_ready = False
+
+    @property
+    def aggregation(self) -> str:
+        """Data plane of the FedAvg all-reduce: 'none' (one client), 'xgmi-oneshot', 'rccl' or 'host'."""
+        if self.world == 1:
+            return "none"
+        if self._peer is not None:
+            return "xgmi-oneshot"
+        return "rccl" if self._native_comm is not None else "host"
 
     # -- execution --
     def _stream(self) -> int:
         return self.stream.cuda_stream
+
+    def _engine_reduces(self) -> bool:
+        """The native engine issues the all-reduce itself (peer kernel or RCCL)."""
+        return self._peer is not None or self._native_comm is not None
+
+    def _phase_allreduce(self, r: int) -> None:
+        if self.world == 1:
+            return
+        if self._engine_reduces():
+            self.engine.phase(r, 2, self._stream(), self._native_comm)
+        else:
+            with torch.cuda.stream(self.stream):
+                self.comm.allreduce_(self.params[(r + 1) & 1])
 
     def _issue_debug(self, n: int) -> None:
         """Debug mode: every phase launched eagerly and synchronised, so a
@@ -463,12 +499,7 @@ class HipRoundEngine(RoundEngineBase):
             _check_finite(r, "local weights after the Adam step", self.local)
             self.engine.phase(r, 1, s, None)
             self.stream.synchronize()
-            if self.world > 1:
-                if self._native_comm is not None:
-                    self.engine.phase(r, 2, s, self._native_comm)
-                else:
-                    with torch.cuda.stream(self.stream):
-                        self.comm.allreduce_(out)
+            self._phase_allreduce(r)
             self.stream.synchronize()
             _check_finite(r, "aggregated weights / metric tails", out)
             self.rounds_issued += 1
@@ -488,12 +519,7 @@ class HipRoundEngine(RoundEngineBase):
             ev[1].record(self.stream)
             self.engine.phase(r, 1, s, None)
             ev[2].record(self.stream)
-            if self.world > 1:
-                if self._native_comm is not None:
-                    self.engine.phase(r, 2, s, self._native_comm)
-                else:
-                    with torch.cuda.stream(self.stream):
-                        self.comm.allreduce_(self.params[(r + 1) & 1])
+            self._phase_allreduce(r)
             ev[3].record(self.stream)
             self.stream.synchronize()
             for i, k in enumerate(names):
@@ -511,7 +537,7 @@ class HipRoundEngine(RoundEngineBase):
         s = self._stream()
         r0 = self.rounds_issued
         g = int(self.cfg.graph_rounds)
-        if self.world > 1 and self._native_comm is None:
+        if self.world > 1 and not self._engine_reduces():
             # torch-owned communicator: all-reduce from Python between rounds
             with torch.cuda.stream(self.stream):
                 for r in range(r0, r0 + n):
@@ -522,7 +548,7 @@ class HipRoundEngine(RoundEngineBase):
         r = r0
         while r < r0 + n:
             left = r0 + n - r
-            if g >= 2 and r % 2 == 0 and left >= g:
+            if g >= 2 and r % 2 == 0 and left >= g and not self.engine.needs_eager_round():
                 if not self._graph_ready:
                     self.engine.capture(g, s, self._native_comm)
                     self._graph_ready = True
@@ -535,6 +561,9 @@ class HipRoundEngine(RoundEngineBase):
 
     def _read_state(self, idx: int) -> np.ndarray:
         self.stream.synchronize()
+        if self._peer is not None:
+            from ..parallel.peer import check_peer_error
+            check_peer_error(self._peer)
         return self.state[idx].cpu().numpy().view(_STATE_DTYPE)[0]
 
     # -- step-by-step API (reference train_one_epoch / evaluate_local / federated_averaging)
@@ -547,16 +576,15 @@ class HipRoundEngine(RoundEngineBase):
         self.stream.synchronize()
         C = self.n_classes
         t0 = self.Pimg + self.rank * self.tail_stride
-        return self.params[(r + 1) & 1][t0:t0 + C * C].cpu().numpy().reshape(C, C).astype(np.int64)
+        if self._peer is not None:  # published into the peer send buffer, not yet reduced
+            cm = np.asarray(self._peer.read((r + 1) & 1, t0, C * C), dtype=np.float32)
+        else:
+            cm = self.params[(r + 1) & 1][t0:t0 + C * C].cpu().numpy()
+        return cm.reshape(C, C).astype(np.int64)
 
     def step_aggregate(self) -> None:
         r = self.rounds_issued
-        if self.world > 1:
-            if self._native_comm is not None:
-                self.engine.phase(r, 2, self._stream(), self._native_comm)
-            else:
-                with torch.cuda.stream(self.stream):
-                    self.comm.allreduce_(self.params[(r + 1) & 1])
+        self._phase_allreduce(r)
         self.rounds_issued += 1
         st = self._read_state(self.rounds_issued & 1)
         if st["stopped"]:
@@ -671,6 +699,7 @@ class HipRoundEngine(RoundEngineBase):
                 self.h_loss[:n].copy_(torch.as_tensor(self.hist.loss[:n], device=dev))
         self.stream.synchronize()
         self.engine.invalidate()
+        self.engine.reset_pending()
         self.rounds_issued = r
         self._stopped_seen = bool(st["es"]["stopped"])
 

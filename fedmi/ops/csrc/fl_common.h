@@ -21,6 +21,9 @@
 #define FL_MAX_LAYERS 4
 #define FL_MAX_CLASSES 16
 #define FL_MAX_WORLD 64
+// Dynamic LDS a fused-kernel workgroup may request: the CU's 160 KiB minus room for the
+// kernels' small static __shared__ objects (round state, counters).
+#define FL_LDS_DYNAMIC_MAX (160 * 1024 - 2048)
 
 // ldw = roundup16(K) + 4 (4 mod 8 floats): 16-byte aligned rows, and the 16 rows of a
 // 16-lane ds_read_b128 group land on 16 distinct 16-byte bank slots.
@@ -40,6 +43,7 @@ struct MLPDesc {
     int ib_off[FL_MAX_LAYERS];        // image offset of b_l
     int Pimg;                         // image floats (multiple of 4)
     int img_lds;                      // LDS float offset of the staged image
+    int cm_off;                       // LDS float offset of the C x C int confusion counters
     int lds_floats;                   // LDS floats needed per block
 };
 
@@ -58,6 +62,7 @@ struct MLPDescB {
     int act_off[FL_MAX_LAYERS + 1];   // act_l bf16 [R][lda[l]]   (l < L)
     int dlt_off[FL_MAX_LAYERS + 1];   // D_l  bf16 [R][lda[l]]    (1 <= l <= L): dLoss/dz_l
     int logit_off;                    // fp32 [R][16] classifier logits
+    int cm_off;                       // int [16][16] confusion counters (fused evaluation)
     int item_base[FL_MAX_LAYERS + 1]; // packing: prefix sums of the 8-element items of each W_l
     int param_off;                    // start of the parameter region (all W_l then all b_l):
     int param_bytes;                  // it is stored pre-packed in global memory and staged by a copy
@@ -127,15 +132,38 @@ struct FLBuffers {
     char* pk_local;     // bf16 mode: packed LDS-layout image of the local (post-Adam) weights
 };
 
+// Evaluation placement of a round (`mode` of the train kernels).
+//   FL_EVAL_CLASSIC : the train kernel folds the previous round's metrics into the state at
+//                     its start; a separate eval kernel scores the post-step model.
+//   FL_EVAL_FUSED   : one client (FedAvg is the identity, so the round's input weights ARE
+//                     the previous round's post-step local model): the train kernel's own
+//                     forward pass yields the previous round's confusion counts (argmax in
+//                     the loss epilogue) and the Adam kernel folds them and decides whether
+//                     this round is live.  No eval kernel.
+//   FL_EVAL_FUSED_SKIP : as FUSED, but the previous round's counts are already in the tail
+//                     (that round ran classic); the train kernel only trains.
+#define FL_EVAL_CLASSIC 0
+#define FL_EVAL_FUSED 1
+#define FL_EVAL_FUSED_SKIP 2
+// LDS confusion-counter region of the train kernels: C*C counters + a "score rows" flag,
+// padded to a multiple of 16 bytes.
+#define FL_CM_FLAG (FL_MAX_CLASSES * FL_MAX_CLASSES)
+#define FL_CM_INTS (FL_CM_FLAG + 4)
+
 // Launchers (fl_kernels.hip). `pg` = image the round trains from (the previous round's
 // all-reduced comm buffer), `comm` = buffer this round publishes into (Pimg + tail floats).
+// `cm_out` = this rank's confusion slots of pg's tail (FL_EVAL_FUSED only).
 hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                            const float* pg, const FLState* st_in, FLState* st_out,
-                           int local_step, hipStream_t s);
+                           int local_step, hipStream_t s, int mode = FL_EVAL_CLASSIC,
+                           float* cm_out = nullptr);
+// `st` = state the step runs under; with `fold` (FL_EVAL_FUSED rounds, first local step) it
+// is the previous round's state: every block folds pg's tail into it, block 0 writes the
+// round's state to `st_out`.
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* pin, const float* anchor, float* comm,
                           const FLState* st, int local_step, hipStream_t s,
-                          const MLPDescB* e = nullptr);
+                          const MLPDescB* e = nullptr, FLState* st_out = nullptr, int fold = 0);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
@@ -144,7 +172,8 @@ hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffe
 // bf16-operand variants (fp32 accumulate, fp32 master weights / slab / Adam state).
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                 const float* pg, const FLState* st_in, FLState* st_out, int local_step,
-                                hipStream_t s, bool stage_local = false);
+                                hipStream_t s, bool stage_local = false, int mode = FL_EVAL_CLASSIC,
+                                float* cm_out = nullptr);
 hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_set_lds_limit_bf16(size_t bytes);

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "fl_common.h"
+#include "peer_allreduce.h"
 
 namespace py = pybind11;
 
@@ -157,17 +158,19 @@ class FLEngine {
             lds += c_.R * d_.ld[l];
             lds = (lds + 3) & ~3;
         }
+        d_.cm_off = lds;  // fused evaluation's confusion counters (FL_CM_INTS ints)
+        lds += FL_CM_INTS;
         d_.img_lds = lds;
         lds += d_.Pimg;
         d_.lds_floats = lds;
         dtype_ = cfg.contains("dtype") ? cfg["dtype"].cast<int>() : 0;
         if (dtype_ == 0) {
-            if ((size_t)lds * 4 > 150 * 1024)
+            if ((size_t)lds * 4 > FL_LDS_DYNAMIC_MAX)
                 throw std::runtime_error("FLEngine: activations exceed LDS; use a smaller R or the layered path");
             HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));
         } else {
             build_bf16_layout();
-            if (e_.lds_bytes > 150 * 1024)
+            if ((size_t)e_.lds_bytes > FL_LDS_DYNAMIC_MAX)
                 throw std::runtime_error("FLEngine(bf16): model exceeds LDS; use a smaller R or the layered path");
             HIP_CHECK(fl_set_lds_limit_bf16((size_t)e_.lds_bytes));
         }
@@ -201,6 +204,10 @@ class FLEngine {
         c_.rtol = cfg["rtol"].cast<double>();
         c_.max_rounds = cfg["max_rounds"].cast<int>();
         c_.metric_mode = cfg["metric_mode"].cast<int>();
+        // Fused evaluation needs the round's input weights to BE the previous round's
+        // post-step local model: one client (FedAvg of one is the identity, agg_scale 1).
+        fused_ = cfg.contains("fused_eval") && cfg["fused_eval"].cast<bool>() && c_.world == 1 &&
+                 c_.agg_scale == 1.0f;
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
@@ -229,59 +236,123 @@ class FLEngine {
         if (pk_) hipFree(pk_);
     }
 
-    // Issue rounds [r0, r0 + n): three kernels (+1 train/adam pair per extra local step)
-    // and, when a communicator is attached and world > 1, one all-reduce per round.
+    // Issue rounds [r0, r0 + n): per round the train/Adam pair (one per local step), the
+    // evaluation (classic rounds) and, when world > 1, one all-reduce.
     void run(int r0, int n, uintptr_t stream, RcclComm* comm) {
         hipStream_t s = as_stream(stream);
-        for (int r = r0; r < r0 + n; ++r) issue_round(r, s, comm);
+        for (int r = r0; r < r0 + n; ++r) issue_round(r, s, comm, true);
     }
 
-    void run_local(int r, uintptr_t stream) { issue_round(r, as_stream(stream), nullptr); }
+    // Local part of round r (no all-reduce; the caller reduces a shared buffer).
+    void run_local(int r, uintptr_t stream) { issue_round(r, as_stream(stream), nullptr, false); }
 
     // One phase of round r: 0 = local training (all local steps), 1 = local evaluation,
     // 2 = FedAvg all-reduce.  Used by the step-by-step reference API
-    // (train_one_epoch / evaluate_local / federated_averaging).
+    // (train_one_epoch / evaluate_local / federated_averaging); always classic rounds.
     void phase(int r, int which, uintptr_t stream, RcclComm* comm) {
         hipStream_t s = as_stream(stream);
-        if (which == 0) issue_train(r, s);
-        else if (which == 1) issue_eval(r, s);
-        else if (which == 2) issue_allreduce(r, s, comm);
-        else throw std::runtime_error("phase: 0, 1 or 2");
+        if (which == 0) {
+            flush_pending_eval(r, s);
+            issue_train(r, s, false);
+        } else if (which == 1) {
+            issue_eval(r, s);
+            cm_in_tail_ = true;
+        } else if (which == 2) {
+            issue_allreduce(r, s, comm);
+        } else {
+            throw std::runtime_error("phase: 0, 1 or 2");
+        }
     }
 
+    // Fold every pending metric into the state / history (host synchronisation point); `r`
+    // = rounds issued.  A fused last round is evaluated first.
     void finalize(int r, uintptr_t stream) {
-        HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], as_stream(stream)));
+        hipStream_t s = as_stream(stream);
+        flush_pending_eval(r, s);
+        HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s));
+        cm_in_tail_ = false;
     }
 
     // Record `n` rounds (n even, starting at an even round) into one hipGraph.  Round
-    // indices live on the device, so the same graph is replayed for every chunk.
+    // indices live on the device, so the same graph is replayed for every chunk.  A graph
+    // always starts from the steady state (see needs_eager_round).
     void capture(int n, uintptr_t stream, RcclComm* comm) {
         if (n <= 0 || (n & 1)) throw std::runtime_error("capture: n must be a positive even number");
+        if (needs_eager_round()) throw std::runtime_error("capture: issue one eager round first");
         drop_graph();
         hipStream_t s = as_stream(stream);
+        const bool pend = pending_cm_, tail = cm_in_tail_;
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
-            for (int r = 0; r < n; ++r) issue_round(r, s, comm);
+            for (int r = 0; r < n; ++r) issue_round(r, s, comm, true);
         } catch (...) {
             hipGraph_t g;
             hipStreamEndCapture(s, &g);
             if (g) hipGraphDestroy(g);
+            pending_cm_ = pend;
+            cm_in_tail_ = tail;
             throw;
         }
         HIP_CHECK(hipStreamEndCapture(s, &graph_));
         HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
         graph_rounds_ = n;
+        pending_cm_ = pend;  // nothing ran yet: replay() applies the rounds' effect
+        cm_in_tail_ = tail;
     }
 
     void replay(uintptr_t stream) {
         if (!exec_) throw std::runtime_error("replay: no captured graph");
+        if (needs_eager_round()) throw std::runtime_error("replay: issue one eager round first");
         HIP_CHECK(hipGraphLaunch(exec_, as_stream(stream)));
+        pending_cm_ = fused_;
+        cm_in_tail_ = !fused_;
     }
 
     int graph_rounds() const { return graph_rounds_; }
 
+    // The captured rounds assume the steady state of their kind: a fused graph must not
+    // start behind a classic round (whose counts already sit in the tail), a classic graph
+    // not behind a fused one (whose counts were never computed).
+    bool needs_eager_round() const { return fused_ ? cm_in_tail_ : pending_cm_; }
+    bool fused() const { return fused_; }
+
     // The host wrote the global weights (set_weights / resume): the next round repacks them.
     void invalidate() { need_pack_ = true; }
+
+    // The host loaded a complete round state (resume): no metrics are pending.
+    void reset_pending() {
+        pending_cm_ = false;
+        cm_in_tail_ = false;
+    }
+
+    // Aggregate with the one-shot xGMI all-reduce (peer_allreduce.hip) instead of RCCL: every
+    // round publishes into the peer object's send buffers, and its kernel writes the reduced
+    // image into this engine's parameter buffer (plus, in bf16 mode, the packed bf16 image).
+    void attach_peer(PeerAllReduce& p) {
+        if (c_.world < 2 || p.world() != c_.world || p.rank() != c_.rank || !p.is_open())
+            throw std::runtime_error("attach_peer: communicator does not match this engine");
+        if (p.n_floats() != (long long)(d_.Pimg + c_.tail_len))
+            throw std::runtime_error("attach_peer: buffer length != parameter image + tails");
+        drop_graph();
+        peer_ = &p;
+        std::memset(&pp_, 0, sizeof(pp_));
+        if (dtype_ == 1) {
+            pp_.pk = b_.pk_global;
+            pp_.L = d_.L;
+            for (int l = 0; l < d_.L; ++l) {
+                const int K = d_.dim[l], N = d_.dim[l + 1];
+                pp_.img4_w[l] = d_.iw_off[l] / 4;
+                pp_.img4_b[l] = d_.ib_off[l] / 4;
+                pp_.img4_end[l] = (d_.ib_off[l] + ((N + 15) & ~15)) / 4;
+                pp_.ldw4[l] = fl_ldw(K) / 4;
+                pp_.k4[l] = ((K + 15) & ~15) / 4;
+                pp_.pk_w[l] = e_.w_off[l] - e_.param_off;
+                pp_.pk_lda[l] = e_.lda[l];
+                pp_.pk_b[l] = e_.bias_off[l] - e_.param_off;
+            }
+        }
+    }
+    bool has_peer() const { return peer_ != nullptr; }
 
     // Enable (ptr != 0) / disable in-kernel phase stamps: [blocks, 16] uint64 buffer.
     void set_debug(uintptr_t ptr) { b_.dbg = as_ptr<unsigned long long>(ptr); }
@@ -290,7 +361,7 @@ class FLEngine {
     void launch_one(int r, int which, uintptr_t stream) {
         hipStream_t s = as_stream(stream);
         float* pg = pbuf_[r & 1];
-        float* cb = pbuf_[(r + 1) & 1];
+        float* cb = comm_buf(r);
         FLState* so = st_[(r + 1) & 1];
         if (which == 0) launch_train(pg, so, so, 1, s);
         else if (which == 1) launch_adam(b_.local, pg, cb, so, 1, s);
@@ -303,7 +374,7 @@ class FLEngine {
     py::dict time_kernels(int r, int iters, uintptr_t stream) {
         hipStream_t s = as_stream(stream);
         float* pg = pbuf_[r & 1];
-        float* cb = pbuf_[(r + 1) & 1];
+        float* cb = comm_buf(r);
         FLState* so = st_[(r + 1) & 1];
         hipEvent_t e0, e1;
         HIP_CHECK(hipEventCreate(&e0));
@@ -376,6 +447,7 @@ class FLEngine {
         for (int l = 0; l < L; ++l) e_.act_off[l] = take(R * e_.lda[l] * 2);
         for (int l = 1; l <= L; ++l) e_.dlt_off[l] = take(R * e_.lda[l] * 2);
         e_.logit_off = take(R * 16 * 4);
+        e_.cm_off = take(FL_CM_INTS * 4);
         e_.param_off = off;
         for (int l = 0; l < L; ++l) e_.w_off[l] = take(e_.kp[l + 1] * e_.lda[l] * 2);
         for (int l = 0; l < L; ++l) e_.bias_off[l] = take(e_.kp[l + 1] * 4);
@@ -384,48 +456,81 @@ class FLEngine {
         e_.item_base[0] = 0;
         for (int l = 0; l < L; ++l) e_.item_base[l + 1] = e_.item_base[l] + e_.kp[l + 1] * (e_.kp[l] >> 3);
     }
-    void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s) {
+    void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
+                      int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr) {
         if (dtype_ == 0) {
-            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s));
+            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s, mode, cm_out));
         } else {
             // the round's input weights -> packed bf16 image.  With one client the FedAvg
             // output IS the local model (agg_scale = 1), which the Adam kernel already packed,
             // so the pack is needed only after host-side weight changes; later local steps
             // stage the Adam-packed local image too.
             const bool solo = c_.world == 1 && c_.agg_scale == 1.0f && !need_pack_;
-            if (ls == 0 && !solo) HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
+            // the peer all-reduce already wrote the packed image of its output
+            const bool packed = solo || (peer_ != nullptr && !need_pack_);
+            if (ls == 0 && !packed) HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
             need_pack_ = false;
-            HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo));
+            HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo, mode, cm_out));
         }
     }
     void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
-                     hipStream_t s) {
-        HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr));
+                     hipStream_t s, FLState* st_out = nullptr, int fold = 0) {
+        HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr, st_out,
+                                 fold));
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
         else HIP_CHECK(fl_launch_eval_bf16(d_, e_, c_, b_, params, comm, st, s));
     }
-    void issue_train(int r, hipStream_t s) {
+    // Train/Adam pairs of round r.  Fused rounds (fl_common.h FL_EVAL_FUSED): the first train
+    // kernel also scores the previous round's model from its own forward pass, and the first
+    // Adam kernel folds those counts and makes the round's live / stop decision.
+    void issue_train(int r, hipStream_t s, bool fused) {
         float* pg = pbuf_[r & 1];
-        float* cb = pbuf_[(r + 1) & 1];
+        float* cb = comm_buf(r);
         FLState* si = st_[r & 1];
         FLState* so = st_[(r + 1) & 1];
+        if (fused && need_pack_) flush_pending_eval(r, s);  // host replaced the weights: score the old model
+        const int mode = !fused ? FL_EVAL_CLASSIC : (cm_in_tail_ ? FL_EVAL_FUSED_SKIP : FL_EVAL_FUSED);
+        float* cm_out = pg + c_.tail_off + c_.rank * c_.tail_stride;
         for (int ls = 0; ls < c_.local_steps; ++ls) {
-            launch_train(pg, ls == 0 ? si : so, so, ls, s);
-            launch_adam(ls == 0 ? pg : b_.local, pg, cb, so, ls, s);
+            const bool first = ls == 0;
+            launch_train(pg, first ? si : so, so, ls, s, first ? mode : FL_EVAL_CLASSIC, cm_out);
+            if (fused && first) launch_adam(pg, pg, cb, si, ls, s, so, 1);
+            else launch_adam(first ? pg : b_.local, pg, cb, so, ls, s);
         }
+        pending_cm_ = fused;
+        cm_in_tail_ = false;
     }
     void issue_eval(int r, hipStream_t s) {
-        launch_eval(b_.local, pbuf_[(r + 1) & 1], st_[(r + 1) & 1], s);
+        launch_eval(b_.local, comm_buf(r), st_[(r + 1) & 1], s);
     }
+    // A fused round r-1 left its metrics pending (they are normally scored by round r's
+    // train kernel): score them with the eval kernel before anything that needs them.
+    void flush_pending_eval(int r, hipStream_t s) {
+        if (!pending_cm_) return;
+        issue_eval(r - 1, s);
+        pending_cm_ = false;
+        cm_in_tail_ = true;
+    }
+    // Buffer round r publishes into (FedAvg contribution + metric tails): the peer
+    // all-reduce's send buffer, or, for RCCL, the parameter buffer it reduces in place.
+    float* comm_buf(int r) const { return peer_ != nullptr ? peer_->send((r + 1) & 1) : pbuf_[(r + 1) & 1]; }
     void issue_allreduce(int r, hipStream_t s, RcclComm* comm) {
-        if (comm != nullptr && c_.world > 1)
+        if (c_.world < 2) return;
+        if (peer_ != nullptr)
+            HIP_CHECK(peer_->launch((r + 1) & 1, pbuf_[(r + 1) & 1], dtype_ == 1 ? &pp_ : nullptr, s));
+        else if (comm != nullptr)
             comm->allreduce_f32((uintptr_t)pbuf_[(r + 1) & 1], (size_t)(d_.Pimg + c_.tail_len), (uintptr_t)s);
     }
-    void issue_round(int r, hipStream_t s, RcclComm* comm) {
-        issue_train(r, s);
-        issue_eval(r, s);
+    void issue_round(int r, hipStream_t s, RcclComm* comm, bool allow_fused) {
+        const bool fused = fused_ && allow_fused;
+        if (!fused) flush_pending_eval(r, s);
+        issue_train(r, s, fused);
+        if (!fused) {
+            issue_eval(r, s);
+            cm_in_tail_ = true;
+        }
         issue_allreduce(r, s, comm);
     }
 
@@ -440,6 +545,11 @@ class FLEngine {
     int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
     char* pk_ = nullptr;
     bool need_pack_ = true;  // host changed the global weights: repack before the next round
+    PeerAllReduce* peer_ = nullptr;  // one-shot xGMI all-reduce (nullptr: RCCL)
+    PeerPack pp_;                    // its bf16 pack epilogue (bf16 mode)
+    bool fused_ = false;       // rounds evaluate the previous round inside the train kernel
+    bool pending_cm_ = false;  // the last issued round was fused: its metrics are not scored yet
+    bool cm_in_tail_ = false;  // the last round's counts sit in the tail, not yet folded
     FLConfig c_;
     FLBuffers b_;
     float* pbuf_[2];
@@ -494,6 +604,11 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("time_kernels", &FLEngine::time_kernels)
         .def("set_debug", &FLEngine::set_debug)
         .def("invalidate", &FLEngine::invalidate)
+        .def("reset_pending", &FLEngine::reset_pending)
+        .def("attach_peer", &FLEngine::attach_peer, py::keep_alive<1, 2>())
+        .def_property_readonly("has_peer", &FLEngine::has_peer)
+        .def("needs_eager_round", &FLEngine::needs_eager_round)
+        .def_property_readonly("fused", &FLEngine::fused)
         .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);
@@ -501,4 +616,5 @@ PYBIND11_MODULE(_fedmi_hip, m) {
     m.def("device_info", &device_info);
     m.attr("STATE_BYTES") = (int)sizeof(FLState);
     register_trainer(m);
+    register_peer(m);
 }

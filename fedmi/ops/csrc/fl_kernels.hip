@@ -286,23 +286,35 @@ __device__ void forward_block(const MLPDesc& d, float* acts, const float* li, un
 template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
-                const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step) {
+                const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step, int mode,
+                float* __restrict__ cm_out) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
     if (b.dbg != nullptr && threadIdx.x == 0) b.dbg[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime();
+    int* cm_s = reinterpret_cast<int*>(lds + d.cm_off);
+    const int C = d.dim[d.L];
     if (threadIdx.x < 64) {  // wave 0: round bookkeeping while the other waves stage
         FLState S0 = *st_in;
         if (local_step == 0) {
-            S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
-            if (threadIdx.x == 0) {
+            if (mode == FL_EVAL_CLASSIC) {
+                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
+                if (threadIdx.x == 0) {
+                    S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
+                    if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
+                    if (blockIdx.x == 0) *st_out = S0;
+                }
+            } else if (threadIdx.x == 0) {
+                // fused (fl_common.h): the Adam kernel folds and decides; train tentatively
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-                if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
-                if (blockIdx.x == 0) *st_out = S0;
             }
         }
-        if (threadIdx.x == 0) S_sh = S0;
+        if (threadIdx.x == 0) {
+            S_sh = S0;
+            cm_s[FL_CM_FLAG] = (local_step == 0 && mode == FL_EVAL_FUSED && S0.next_round > S0.finalized) ? 1 : 0;
+        }
     }
+    for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
     const float* params = (local_step == 0) ? pg : b.local;
     const int R = RT * 16;
     const int row0 = blockIdx.x * R;
@@ -322,18 +334,24 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
     FL_STAMP(2);
     if (b.dbg != nullptr && threadIdx.x == 0) b.dbg[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
 
-    // softmax cross-entropy (mean over the local shard): dZ = (softmax - onehot) / n
-    const int C = d.dim[L];
+    // softmax cross-entropy (mean over the local shard): dZ = (softmax - onehot) / n.
+    // Fused evaluation: the same logits score the previous round's model (argmax).
     float* z = acts + d.act_off[L];
     const int ldz = d.ld[L];
+    const bool score = cm_s[FL_CM_FLAG] != 0;
     float lossv = 0.f;
     if (threadIdx.x < R) {
         const int r = threadIdx.x, row = row0 + r;
         float* zr = z + r * ldz;
         if (row < c.n_rows) {
             const int y = ylab;
-            float mx = zr[0];
-            for (int k = 1; k < C; ++k) mx = fmaxf(mx, zr[k]);
+            float mx = zr[0], bv = zr[0];
+            int best = 0;
+            for (int k = 1; k < C; ++k) {
+                mx = fmaxf(mx, zr[k]);
+                if (zr[k] > bv) { bv = zr[k]; best = k; }  // torch.max(dim=1): first maximum
+            }
+            if (score) atomicAdd(&cm_s[y * C + best], 1);
             float se = 0.f;
             for (int k = 0; k < C; ++k) se += expf(zr[k] - mx);
             const float lse = mx + logf(se);
@@ -352,6 +370,9 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
         if (threadIdx.x == 0) slab[d.P] = lossv;  // R <= 64: wave 0 holds every row
     }
     lds_barrier();
+    if (score)
+        for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
+            if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
     FL_STAMP(3);
 
     // backward, top layer first, ONE phase per layer: wgrad_l (reads dZ_{l+1}, act_l) and
@@ -381,20 +402,38 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
 __global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
-               const FLState* __restrict__ st, int local_step, MLPDescB e, int pack) {
+               const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
+               FLState* __restrict__ st_out, int fold) {
     __shared__ float part[ADAM_WAVES][64];
+    __shared__ FLState S_sh;
     const int last_local_step = (local_step == c.local_steps - 1);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nparam_blocks = (d.P + 63) / 64;
-    const FLState S = *st;
+    // Round state.  Fused evaluation (fl_common.h): wave 0 of EVERY block folds the previous
+    // round's tail (anchor = this round's input image) into the previous state and decides
+    // whether this round is live -- the same deterministic computation everywhere, so no
+    // block waits for another; block 0 publishes it.  It overlaps the slab loads below.
+    if (wave == 0) {
+        FLState S0 = *st;
+        if (fold) {
+            S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0);
+            if (lane == 0) {
+                S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
+                if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
+                if (blockIdx.x == 0) *st_out = S0;
+            }
+        }
+        if (lane == 0) S_sh = S0;
+    }
     if (blockIdx.x >= nparam_blocks) {
-        // tail block: this rank's confusion slots are zeroed (fl_eval accumulates into
-        // them); its loss slot gets the per-workgroup CE partials, summed in a fixed order
+        // tail block: this rank's confusion slots are zeroed (the eval pass accumulates
+        // into them); its loss slot gets the per-workgroup CE partials, summed in a fixed order
         if (!last_local_step) return;
         float lp = 0.f;
         for (int s = threadIdx.x; s < c.n_slabs; s += blockDim.x) lp += b.slab[(size_t)s * c.slab_stride + d.P];
         part[wave][lane] = lp;
         lds_barrier();
+        const FLState S = S_sh;
         if (wave == 0) {
             float t = 0.f;
 #pragma unroll
@@ -435,9 +474,10 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             is_bias = true;
         }
     }
-    if (!S.live) {
-        // past the stop: rank 0 contributes the (identical) global weights, others 0, so the
-        // all-reduce returns them bit-exactly
+    // past the stop: rank 0 contributes the (identical) global weights, others 0, so the
+    // all-reduce returns them bit-exactly.  Classic rounds know the state on entry and skip
+    // the reduction; fused rounds learn it at the barrier below.
+    if (!fold && !st->live) {
         if (wave == 0 && valid && last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
         return;
     }
@@ -459,6 +499,11 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     part[wave][lane] = g;
     lds_barrier();
     if (wave != 0 || !valid) return;
+    const FLState S = S_sh;
+    if (!S.live) {
+        if (last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
+        return;
+    }
     g = 0.f;
 #pragma unroll
     for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
@@ -607,29 +652,32 @@ static inline size_t lds_bytes(const MLPDesc& d) { return (size_t)d.lds_floats *
 
 template <int RT>
 static hipError_t launch_train_rt(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
-                                  const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s) {
+                                  const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
+                                  int mode, float* cm_out) {
     hipLaunchKernelGGL(fl_train_kernel<RT>, dim3(c.n_slabs), dim3(FL_THREADS), lds_bytes(d), s, d, c, b, pg, si,
-                       so, ls);
+                       so, ls, mode, cm_out);
     return hipGetLastError();
 }
 
 hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pg,
-                           const FLState* si, FLState* so, int ls, hipStream_t s) {
+                           const FLState* si, FLState* so, int ls, hipStream_t s, int mode, float* cm_out) {
+    if (mode == FL_EVAL_FUSED && cm_out == nullptr) return hipErrorInvalidValue;
     switch (c.R) {
-        case 16: return launch_train_rt<1>(d, c, b, pg, si, so, ls, s);
-        case 32: return launch_train_rt<2>(d, c, b, pg, si, so, ls, s);
+        case 16: return launch_train_rt<1>(d, c, b, pg, si, so, ls, s, mode, cm_out);
+        case 32: return launch_train_rt<2>(d, c, b, pg, si, so, ls, s, mode, cm_out);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
                           const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s,
-                          const MLPDescB* e) {
+                          const MLPDescB* e, FLState* st_out, int fold) {
+    if (fold && st_out == nullptr) return hipErrorInvalidValue;
     const int blocks = (d.P + 63) / 64 + 1;
     MLPDescB ee = {};
     if (e != nullptr) ee = *e;
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
-                       local_step, ee, e != nullptr ? 1 : 0);
+                       local_step, ee, e != nullptr ? 1 : 0, st_out, fold);
     return hipGetLastError();
 }
 

@@ -268,22 +268,35 @@ template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                      const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
-                     int stage_local) {
+                     int stage_local, int mode, float* __restrict__ cm_out) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
+    int* cm_s = reinterpret_cast<int*>(lds + e.cm_off);
+    const int C = d.dim[d.L];
     if (threadIdx.x < 64) {  // wave 0: round bookkeeping while the other waves stage
         FLState S0 = *st_in;
         if (local_step == 0) {
-            S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
-            if (threadIdx.x == 0) {
+            if (mode == FL_EVAL_CLASSIC) {
+                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
+                if (threadIdx.x == 0) {
+                    S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
+                    if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
+                    if (blockIdx.x == 0) *st_out = S0;
+                }
+            } else if (threadIdx.x == 0) {
+                // fused: the Adam kernel folds the previous round and decides; train on the
+                // tentative decision (a stop only turns this round into a no-op later)
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-                if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
-                if (blockIdx.x == 0) *st_out = S0;
             }
         }
-        if (threadIdx.x == 0) S_sh = S0;
+        if (threadIdx.x == 0) {
+            S_sh = S0;
+            // score the rows for the previous round iff its metrics are still pending
+            cm_s[FL_CM_FLAG] = (local_step == 0 && mode == FL_EVAL_FUSED && S0.next_round > S0.finalized) ? 1 : 0;
+        }
     }
+    for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
     const float* params = (local_step == 0) ? pg : b.local;
     const int R = RT * 16;
     const int row0 = blockIdx.x * R;
@@ -293,7 +306,7 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     FL_STAMP(8);
     stage_rows_bf16<RT>(b.X, c.n_rows, d.dim[0], row0, lds + e.act_off[0], e.kp[0], e.lda[0]);
     {   // padding columns [C, kp[L]) of D_L never change: zero them here, off the CE's path
-        const int C = d.dim[L], padc = e.kp[L] - d.dim[L];
+        const int padc = e.kp[L] - C;
         uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
         for (int i = threadIdx.x; i < R * padc; i += FL_THREADS) {
             const int r = i / padc;
@@ -308,11 +321,12 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     forward_block_bf16<RT>(d, e, lds, b.dbg);
     FL_STAMP(2);
 
-    // softmax cross-entropy (mean over the shard): D_L = (softmax - onehot) / n, bf16
-    const int C = d.dim[L];
+    // softmax cross-entropy (mean over the shard): D_L = (softmax - onehot) / n, bf16.
+    // Fused evaluation: the same logits score the previous round's model (argmax).
     const float* z = reinterpret_cast<const float*>(lds + e.logit_off);
     uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
     const int ldL = e.lda[L];
+    const bool score = cm_s[FL_CM_FLAG] != 0;
     float lossv = 0.f;
     if (threadIdx.x < R) {
         const int r = threadIdx.x, row = row0 + r;
@@ -320,8 +334,13 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
         uint16_t* dr = DL + r * ldL;
         if (row < c.n_rows) {
             const int y = ylab;
-            float mx = zr[0];
-            for (int k = 1; k < C; ++k) mx = fmaxf(mx, zr[k]);
+            float mx = zr[0], bv = zr[0];
+            int best = 0;
+            for (int k = 1; k < C; ++k) {
+                mx = fmaxf(mx, zr[k]);
+                if (zr[k] > bv) { bv = zr[k]; best = k; }  // torch.max(dim=1): first maximum
+            }
+            if (score) atomicAdd(&cm_s[y * C + best], 1);
             float se = 0.f;
             for (int k = 0; k < C; ++k) se += expf(zr[k] - mx);
             const float lse = mx + logf(se);
@@ -339,6 +358,9 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
         if (threadIdx.x == 0) slab[d.P] = lossv;
     }
     lds_barrier();
+    if (score)
+        for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
+            if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
     FL_STAMP(3);
 
     // backward, top layer first, one phase per layer (wgrad_l and dgrad_l are independent)
@@ -394,15 +416,16 @@ fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float*
 // ---------------------------------------------------------------------------------------
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                 const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
-                                bool stage_local) {
+                                bool stage_local, int mode, float* cm_out) {
+    if (mode == FL_EVAL_FUSED && cm_out == nullptr) return hipErrorInvalidValue;
     switch (c.R) {
         case 16:
             hipLaunchKernelGGL(fl_train_bf16_kernel<1>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
-                               pg, si, so, ls, stage_local ? 1 : 0);
+                               pg, si, so, ls, stage_local ? 1 : 0, mode, cm_out);
             break;
         case 32:
             hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
-                               pg, si, so, ls, stage_local ? 1 : 0);
+                               pg, si, so, ls, stage_local ? 1 : 0, mode, cm_out);
             break;
         default: return hipErrorInvalidValue;
     }

@@ -11,6 +11,10 @@ working, but the data plane is different:
 * **data plane** (every round, device buffers): one in-place SUM all-reduce on a flat
   device buffer.  Backends:
 
+  - ``xgmi``  -- (default on GPUs) the fused round engine aggregates with the one-shot
+    peer all-reduce over xGMI (``fedmi.parallel.peer``: IPC-mapped send buffers, one kernel
+    per round, self-tested at start-up); everything else uses the RCCL communicator below,
+    which is also the automatic fallback.
   - ``rccl``  -- the engine-owned RCCL communicator in the native extension
     (``RcclComm``: ``ncclCommInitRank`` over xGMI, unique id exchanged over the gloo
     store).  The engine issues ``ncclAllReduce`` itself, inside captured HIP graphs.
@@ -37,7 +41,12 @@ def _env_int(name: str, default: int) -> int:
 
 
 class Comm:
-    def __init__(self, backend: str = "auto", device: Optional[str] = None, timeout_s: float = 600.0):
+    """``rccl=False`` (with ``backend='xgmi'``) skips the RCCL communicator: device
+    all-reduces outside the round engine then go through the host.  That is the setting for
+    several ranks sharing one GPU (tests), which RCCL does not support."""
+
+    def __init__(self, backend: str = "auto", device: Optional[str] = None, timeout_s: float = 600.0,
+                 rccl: bool = True):
         self.rank = _env_int("RANK", 0)
         self.size = _env_int("WORLD_SIZE", 1)
         self.local_rank = _env_int("LOCAL_RANK", self.rank)
@@ -50,10 +59,13 @@ class Comm:
         else:
             self.device = torch.device("cpu")
         if backend == "auto":
-            backend = "rccl" if self.device.type == "cuda" else "gloo"
+            backend = "xgmi" if self.device.type == "cuda" else "gloo"
+        if backend not in ("xgmi", "rccl", "nccl", "gloo"):
+            raise ValueError(f"unknown backend {backend!r}")
         if self.device.type == "cpu" and backend != "gloo":
             raise ValueError(f"backend {backend!r} needs a GPU device")
         self.backend = backend
+        self.peer_allreduce = backend == "xgmi"   # round engines use the one-shot xGMI all-reduce
         self.native = None       # RcclComm
         self._nccl_group = None
         self._initialized_here = False
@@ -65,7 +77,7 @@ class Comm:
                 dist.init_process_group("gloo", rank=self.rank, world_size=self.size,
                                         timeout=timedelta(seconds=timeout_s))
                 self._initialized_here = True
-            if backend == "rccl":
+            if backend == "rccl" or (backend == "xgmi" and rccl):
                 from ..ops import native
                 m = native()
                 uid = [m.RcclComm.unique_id() if self.rank == 0 else None]
@@ -131,8 +143,12 @@ class Comm:
                     self.native.allreduce_f64(t.data_ptr(), t.numel(), stream)
                 else:
                     raise TypeError(f"allreduce_: unsupported dtype {t.dtype}")
-            else:
+            elif self._nccl_group is not None:
                 dist.all_reduce(t, group=self._nccl_group)
+            else:  # no device communicator: through the host (gloo)
+                h = t.cpu()
+                dist.all_reduce(h)
+                t.copy_(h)
         else:
             dist.all_reduce(t)
         return t
@@ -149,11 +165,11 @@ class Comm:
 _WORLD: Optional[Comm] = None
 
 
-def get_world(backend: str = "auto", device: Optional[str] = None) -> Comm:
+def get_world(backend: str = "auto", device: Optional[str] = None, rccl: bool = True) -> Comm:
     """Process-wide communicator (the analogue of ``MPI.COMM_WORLD``)."""
     global _WORLD
     if _WORLD is None:
-        _WORLD = Comm(backend=backend, device=device)
+        _WORLD = Comm(backend=backend, device=device, rccl=rccl)
     return _WORLD
 
 

@@ -1,0 +1,101 @@
+"""Set-up of the one-shot xGMI all-reduce (``fedmi/ops/csrc/peer_allreduce.hip``).
+
+The fused round engine's FedAvg message is ~50 KB (the reference MLP's parameter image plus
+metric tails), so its all-reduce is latency-bound.  On an MI355X node every GPU has a direct
+xGMI link to each of its 7 peers: the native ``PeerAllReduce`` maps every rank's send buffers
+through HIP IPC and reduces them in ONE kernel (publish flag -> wait -> pull all peers over
+the 7 links at once -> sum in rank order), instead of a ring's 2 x 7 dependent steps.  RCCL
+stays the path for bandwidth-bound messages (the wide-MLP buckets) and the fallback here.
+
+:func:`make_peer_allreduce` is collective: every rank either gets a working, self-tested
+communicator or ``None`` -- never a mix, so ranks cannot disagree about the data plane.
+"""
+from __future__ import annotations
+
+import sys
+from typing import Optional
+
+import numpy as np
+import torch
+
+PEER_MAX_WORLD = 8
+
+
+def _all_ok(comm, ok: bool) -> bool:
+    """Logical AND over ranks (host control plane)."""
+    return all(comm.allgather(bool(ok)))
+
+
+def fill_values(n: int, rank: int, salt: int) -> np.ndarray:
+    """Host copy of the self-test payload written by ``fill_test`` (peer_fill_kernel)."""
+    i = np.arange(n, dtype=np.uint64)
+    h = (i * np.uint64(2654435761) + np.uint64(rank * 40503) + np.uint64(salt * 97)) & np.uint64(0xFFFFFFFF)
+    return (h % np.uint64(2048)).astype(np.float64) * 0.25 - 256.0
+
+
+def selftest(h, comm, device, calls: int = 4, timeout_s: float = 10.0) -> bool:
+    """Run ``calls`` all-reduces of a known payload (both parities) and check every float on
+    every rank.  All ranks run every call even after a mismatch, so nobody is left waiting."""
+    n = int(h.n_floats)
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    s = torch.cuda.current_stream(device)
+    h.set_timeout(timeout_s)
+    ok = True
+    for k in range(calls):
+        salt = 1000 + k
+        h.fill_test(k & 1, salt, s.cuda_stream)
+        h.allreduce(k & 1, out.data_ptr(), s.cuda_stream)
+        got = out.cpu().numpy()
+        expect = sum(fill_values(n, r, salt) for r in range(comm.size)).astype(np.float32)
+        ok = ok and bool(np.array_equal(got, expect))
+    ok = ok and h.error() == 0
+    return ok
+
+
+def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, check: bool = True):
+    """Collective.  Returns a native ``PeerAllReduce`` of ``n_floats`` floats, open and
+    self-tested on every rank, or ``None`` on every rank (then the caller uses RCCL)."""
+    from ..ops import native
+    if comm is None or comm.size < 2 or comm.size > PEER_MAX_WORLD:
+        return None
+    m = native()
+    h, why = None, ""
+    try:
+        h = m.PeerAllReduce(comm.size, comm.rank, torch.device(device).index or 0, int(n_floats), float(timeout_s))
+        handle = bytes(h.handle())
+    except Exception as e:  # noqa: BLE001 -- reported, and every rank falls back together
+        handle, why = None, f"rank {comm.rank}: {e}"
+    handles = comm.allgather(handle)
+    ok = all(x is not None for x in handles)
+    if ok:
+        try:
+            h.open(handles)
+        except Exception as e:  # noqa: BLE001
+            ok, why = False, f"rank {comm.rank}: {e}"
+    ok = _all_ok(comm, ok)
+    if ok and check:
+        ok = _all_ok(comm, selftest(h, comm, device))
+        why = why or "self-test mismatch or timeout"
+    if h is not None:
+        h.set_timeout(timeout_s)
+    if not ok:
+        if comm.rank == 0:
+            print(f"[fedmi] one-shot xGMI all-reduce unavailable ({why or 'peer set-up failed'}); using RCCL",
+                  file=sys.stderr, flush=True)
+        comm.Barrier()  # nobody still reads a buffer we are about to free
+        if h is not None:
+            h.close()
+        return None
+    # The self-test left its payload in the send buffers; the engine never writes the image
+    # padding, which must read as 0.  Every rank finished its self-test reads before the
+    # allgather above, so the buffers can be zeroed now; the barrier orders the zeroing
+    # before any rank's first real call.
+    h.clear()
+    comm.Barrier()
+    return h
+
+
+def check_peer_error(h) -> None:
+    if h is not None and h.error():
+        raise RuntimeError("one-shot xGMI all-reduce: a peer did not arrive within the timeout "
+                           "(a client died or stalled); results since then are invalid")

@@ -333,6 +333,52 @@ def test_bf16_engine_tracks_fp32_oracle(R, hidden):
     assert abs(hb.history()["loss"][-1] - ref.history()["loss"][-1]) < 0.02
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_eval_equals_classic_rounds(dtype):
+    """One client: scoring round r inside round r+1's train kernel (fused evaluation) gives
+    bit-identical weights, metric history and early-stop round to the separate eval kernel."""
+    X, y = make_income_like(3000, seed=11)
+    flat = init_flat(DIMS, 6)
+    out = []
+    for fused in (False, True):
+        cfg = EngineConfig(max_rounds=200, patience=4, tolerance=2e-3, dtype=dtype, fused_eval=fused,
+                           graph_rounds=8)
+        e = HipRoundEngine(X, y, 2, cfg, None, flat)
+        assert e.engine.fused == fused
+        e.run(200)
+        out.append((e.global_flat(), e.history()))
+    (wc, hc), (wf, hf) = out
+    assert hc["stop_round"] > 0 and hf["stop_round"] == hc["stop_round"]
+    assert hf["rounds_run"] == hc["rounds_run"]
+    np.testing.assert_array_equal(wf, wc)
+    np.testing.assert_array_equal(hf["global"], hc["global"])
+    np.testing.assert_array_equal(hf["loss"], hc["loss"])
+
+
+def test_fused_eval_mixed_with_step_api():
+    """Fused rounds, then reference step-by-step rounds (classic), then fused again: the
+    pending/evaluated hand-over keeps every round's metrics exact."""
+    X, y = make_income_like(2000, seed=12)
+    flat = init_flat(DIMS, 7)
+    hist = []
+    for fused in (False, True):
+        e = HipRoundEngine(X, y, 2, EngineConfig(max_rounds=40, early_stop=False, fused_eval=fused,
+                                                 graph_rounds=4), None, flat)
+        e.run(5)
+        cms = []
+        for _ in range(2):
+            e.step_train()
+            cms.append(e.step_eval())
+            e.step_aggregate()
+        e.run(7)
+        e.sync_history()
+        hist.append((e.history(), cms, e.global_flat()))
+    assert hist[0][0]["rounds_run"] == hist[1][0]["rounds_run"] == 14
+    np.testing.assert_array_equal(hist[0][0]["global"], hist[1][0]["global"])
+    np.testing.assert_array_equal(hist[0][1], hist[1][1])
+    np.testing.assert_array_equal(hist[0][2], hist[1][2])
+
+
 def test_bf16_engine_layout_fits_two_blocks_per_cu():
     X, y = make_income_like(500, seed=1)
     e = HipRoundEngine(X, y, 2, EngineConfig(rows_per_block=16, dtype="bf16"), None, init_flat([14, 50, 200, 2], 0))
