@@ -68,12 +68,38 @@ def parse_args(argv=None):
     ap.add_argument("--profile", type=int, default=0, metavar="N",
                     help="time the first N rounds per phase with hipEvents (HIP engine)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--wide", action="store_true",
+                    help="BASELINE config 3: layer-by-layer wide-MLP client (e.g. --hidden 4096 4096 4096) on "
+                         "device-generated synthetic shards of --synthetic-rows rows per client")
+    ap.add_argument("--synthetic-rows", type=int, default=131072, help="rows per client for --wide")
+    ap.add_argument("--micro-batch", type=int, default=16384, help="rows per micro-batch for --wide")
+    ap.add_argument("--eval-every", type=int, default=0, help="--wide: local accuracy every N rounds")
     return ap.parse_args(argv)
+
+
+def main_wide(a, comm):
+    """--wide: federated wide-MLP rounds (fedmi.fl.wide.run_wide_fedavg)."""
+    from fedmi.fl.wide import run_wide_fedavg
+    dims = [14, *a.hidden, 2]
+    res = run_wide_fedavg(comm, dims, a.synthetic_rows, a.rounds, micro_batch=a.micro_batch, dtype=a.dtype,
+                          lr=a.lr, eval_every=a.eval_every, seed=a.seed + 7, verbose=not a.quiet)
+    if comm.rank == 0:
+        print(f"wide MLP {'-'.join(map(str, dims))}, {comm.size} client(s) x {a.synthetic_rows} rows: "
+              f"{res['median_round_s'] * 1e3:.1f} ms/round, {res['tflops_per_client']:.1f} TFLOP/s per client, "
+              f"{res['samples_per_s_per_client'] / 1e6:.2f} M samples/s/client", flush=True)
+        if a.jsonl:
+            w = JsonlWriter(a.jsonl)
+            w.write(script="C-wide", dims=dims, clients=comm.size, **res)
+            w.close()
+    comm.close()
+    return res
 
 
 def main(argv=None):
     a = parse_args(argv)
     comm = get_world(backend=a.backend, device=a.device)
+    if a.wide:
+        return main_wide(a, comm)
     rank, size = comm.Get_rank(), comm.Get_size()
 
     # every rank derives the same split locally: no broadcast of the table (C:243-246)

@@ -49,21 +49,8 @@ def ref_per_client(n: int) -> float:
 
 def synth_shard(n_rows: int, rank: int, device, seed: int = 7):
     """Income-shaped rows generated on the device by the Philox kernel."""
-    from fedmi.data.synthetic import teacher_weights, make_income_like
-    from fedmi.ops import native
-    m = native()
-    w1, w2 = teacher_weights()
-    # balance threshold estimated on a host sample from the same distribution
-    Xs, _ = make_income_like(4096, seed=123)
-    th = float(np.median(np.maximum(Xs @ w1.T, 0.0) @ w2))
-    X = torch.empty((n_rows, 14), dtype=torch.float32, device=device)
-    y = torch.empty(n_rows, dtype=torch.int32, device=device)
-    tw1 = torch.as_tensor(w1, device=device)
-    tw2 = torch.as_tensor(np.append(w2, th).astype(np.float32), device=device)
-    m.synth(X.data_ptr(), y.data_ptr(), n_rows, 14, seed, rank * n_rows, tw1.data_ptr(), tw2.data_ptr(),
-            int(w1.shape[0]), torch.cuda.current_stream(device).cuda_stream)
-    torch.cuda.synchronize(device)
-    return X, y
+    from fedmi.data.synthetic import device_shard
+    return device_shard(n_rows, rank, device, seed)
 
 
 def rounds_to_target(comm, targets=(0.80, 0.83), max_rounds=300, dtype="fp32"):

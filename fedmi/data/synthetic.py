@@ -44,3 +44,25 @@ def make_income_like(n: int, seed: int = 0, teacher_seed: int = 1234, dtype=np.f
     score = np.maximum(X.astype(np.float32) @ w1.T, 0.0) @ w2
     y = (score > np.median(score)).astype(np.int64)
     return X, y
+
+
+def device_shard(n_rows: int, rank: int, device, seed: int = 7):
+    """Income-shaped rows generated ON the device by the Philox kernel (no host copy; the
+    1e8-row shards of BASELINE config 3): client ``rank`` gets rows
+    ``[rank * n_rows, (rank + 1) * n_rows)`` of one global counter-based stream, labels from
+    the same teacher as :func:`make_income_like`, balanced by a threshold estimated on a host
+    sample of the same distribution."""
+    import torch
+    from ..ops import native
+    m = native()
+    w1, w2 = teacher_weights()
+    Xs, _ = make_income_like(4096, seed=123)
+    th = float(np.median(np.maximum(Xs @ w1.T, 0.0) @ w2))
+    X = torch.empty((n_rows, N_FEATURES), dtype=torch.float32, device=device)
+    y = torch.empty(n_rows, dtype=torch.int32, device=device)
+    tw1 = torch.as_tensor(w1, device=device)
+    tw2 = torch.as_tensor(np.append(w2, th).astype(np.float32), device=device)
+    m.synth(X.data_ptr(), y.data_ptr(), n_rows, N_FEATURES, seed, rank * n_rows, tw1.data_ptr(), tw2.data_ptr(),
+            int(w1.shape[0]), torch.cuda.current_stream(device).cuda_stream)
+    torch.cuda.synchronize(device)
+    return X, y

@@ -58,6 +58,10 @@ class EngineConfig:
     # pass IS that evaluation, FedAvg of one client being the identity) instead of a separate
     # eval kernel; metrics, history and early stop are unchanged (fl_common.h FL_EVAL_FUSED)
     fused_eval: bool = True
+    # world > 1 with the one-shot xGMI all-reduce: evaluate the post-step local model and
+    # all-reduce in ONE kernel, the weights' all-reduce overlapping the evaluation
+    # (fedmi/ops/csrc/peer_device.h); False = separate eval and all-reduce kernels
+    eval_fedavg: bool = True
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -420,6 +424,7 @@ class HipRoundEngine(RoundEngineBase):
             "dtype": _dtype_id(cfg.dtype),
             # trial packing runs rounds through run_local + a shared all-reduce: classic rounds
             "fused_eval": bool(cfg.fused_eval) and comm_buffers is None,
+            "eval_fedavg": bool(cfg.eval_fedavg),
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),

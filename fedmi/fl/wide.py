@@ -9,10 +9,12 @@ layer by layer on the grid-level MFMA GEMMs of ``fedmi/ops/csrc/gemm_mfma.hip``:
 * bf16 operands, fp32 accumulation, fp32 master weights / Adam state / gradients;
 * the shard is processed in micro-batches with gradient accumulation (beta = 1 in the
   wgrad epilogue), which is exactly the full-batch gradient (SURVEY §5.7: row-wise scale-up);
-* FedAvg = one RCCL all-reduce per layer bucket of the pre-scaled (n_i / N) fp32 weights;
-  buckets are issued in backward order on a side stream as soon as that layer's Adam
-  update is done, so the all-reduce of the top layers overlaps the update / re-quantisation
-  of the lower ones.
+* FedAvg = one RCCL all-reduce per layer bucket of the pre-scaled (n_i / N) fp32 weights,
+  issued in FORWARD order on a side stream, each followed (same stream) by the bf16
+  re-quantisation of its layer and an event.  FedAvg's data dependency is per layer: the
+  next round's forward of layer l waits only on bucket l's event, so the all-reduce of the
+  deeper (larger) buckets overlaps the first micro-batch's forward of the layers before
+  them (SURVEY §5.8 "bucket per layer in forward order").
 """
 from __future__ import annotations
 
@@ -80,22 +82,35 @@ class WideClient:
         self.nt_calls = 0
         # transposed (k = rows) operands need 16-byte aligned rows of the micro-batch buffers
         self._t_ok = bool(self.dtype) and mb % 128 == 0
+        self._bucket_ev: List[Optional[torch.cuda.Event]] = [None] * self.L  # pending FedAvg buckets
         self._quantize()
 
     # ------------------------------------------------------------------
     def _s(self) -> int:
         return self.stream.cuda_stream
 
+    def _quantize_layer(self, l: int, stream: torch.cuda.Stream):
+        """GEMM operand copies of layer l (bf16 W and W^T, or fp32 W) on `stream`."""
+        w, q = self.W[l], self.Wq[l]
+        with torch.cuda.stream(stream):
+            if self.dtype:
+                self.m.to_bf16(w.data_ptr(), q.data_ptr(), w.numel(), stream.cuda_stream)
+                if self.WqT[l] is not None:
+                    N, K = w.shape
+                    self.m.transpose_bf16(w.data_ptr(), N, K, K, self.WqT[l].data_ptr(), N, stream.cuda_stream)
+            else:
+                q.copy_(w)
+
     def _quantize(self):
-        with torch.cuda.stream(self.stream):
-            for l, (w, q) in enumerate(zip(self.W, self.Wq)):
-                if self.dtype:
-                    self.m.to_bf16(w.data_ptr(), q.data_ptr(), w.numel(), self._s())
-                    if self.WqT[l] is not None:
-                        N, K = w.shape
-                        self.m.transpose_bf16(w.data_ptr(), N, K, K, self.WqT[l].data_ptr(), N, self._s())
-                else:
-                    q.copy_(w)
+        for l in range(self.L):
+            self._quantize_layer(l, self.stream)
+
+    def _wait_bucket(self, l: int):
+        """The compute stream's first use of layer l after FedAvg waits for its bucket only."""
+        ev = self._bucket_ev[l]
+        if ev is not None:
+            self.stream.wait_event(ev)
+            self._bucket_ev[l] = None
 
     @staticmethod
     def _nt_ok(M: int, N: int, K: int) -> bool:
@@ -113,6 +128,7 @@ class WideClient:
             inp = x
         for l in range(self.L):
             K, N = self.dims[l], self.dims[l + 1]
+            self._wait_bucket(l)
             if l + 1 == self.L:  # logits head: fp32 output for the loss
                 m.gemm(rows, N, K, inp.data_ptr(), K, 1, self.Wq[l].data_ptr(), K, 1, self.logits.data_ptr(), N, 1,
                        self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
@@ -214,17 +230,27 @@ class WideClient:
                              self.params.numel(), lr, self.betas[0], self.betas[1], self.eps, t, s)
 
     def aggregate(self):
-        """Sample-size-weighted FedAvg: scale by n_i/N, all-reduce per layer bucket (top
-        layer first) on the comm stream, then refresh the bf16 operand copies."""
-        if self.world > 1:
-            self.comm_stream.wait_stream(self.stream)
+        """Sample-size-weighted FedAvg: per layer bucket [W_l | b_l], in forward order on the
+        comm stream: scale by n_i/N, all-reduce, re-quantise, record the bucket's event.  The
+        compute stream does not wait here: its next use of layer l waits on event l."""
+        if self.world == 1:
+            self._quantize()
+            return
+        self.comm_stream.wait_stream(self.stream)  # the Adam step (and evaluation) are done
+        for l, ((name, shape, off), (bn, bs, boff)) in enumerate(zip(self.layout[0::2], self.layout[1::2])):
             with torch.cuda.stream(self.comm_stream):
-                for (name, shape, off), (bn, bs, boff) in reversed(list(zip(self.layout[0::2], self.layout[1::2]))):
-                    seg = self.params[off:boff + int(np.prod(bs))]
-                    seg.mul_(self.agg)
-                    self.comm.allreduce_(seg)
-            self.stream.wait_stream(self.comm_stream)
-        self._quantize()
+                seg = self.params[off:boff + int(np.prod(bs))]
+                seg.mul_(self.agg)
+                self.comm.allreduce_(seg)
+            self._quantize_layer(l, self.comm_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.comm_stream)
+            self._bucket_ev[l] = ev
+
+    def sync(self):
+        """Join every pending FedAvg bucket into the compute stream."""
+        for l in range(self.L):
+            self._wait_bucket(l)
 
     def evaluate(self) -> float:
         rows = min(self.eval_rows or self.mb, self.n, self.mb)
@@ -243,6 +269,7 @@ class WideClient:
         return acc
 
     def loss(self) -> float:
+        self.sync()
         self.stream.synchronize()
         return float(self.loss_acc.item()) / self.n
 
@@ -250,3 +277,40 @@ class WideClient:
     def flops_per_round(self) -> float:
         macs = sum(a * b for a, b in zip(self.dims[:-1], self.dims[1:]))
         return 6.0 * self.n * macs
+
+
+def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int, micro_batch: int = 16384,
+                    dtype: str = "bf16", lr: float = 0.004, eval_every: int = 0, seed: int = 7,
+                    verbose: bool = True) -> dict:
+    """BASELINE config 3 driver: every rank is one client holding ``rows_per_client``
+    synthetic income-shaped rows generated on its GPU, trains the wide MLP ``dims`` with
+    full-batch (micro-batched) Adam steps and averages per layer bucket every round.
+    Returns the per-round loss history, evaluation accuracies and timings."""
+    import time
+
+    from ..data.synthetic import device_shard
+    dev = comm.device if comm is not None else torch.device("cuda", torch.cuda.current_device())
+    rank = comm.rank if comm is not None else 0
+    world = comm.size if comm is not None else 1
+    X, y = device_shard(rows_per_client, rank, dev, seed=seed)
+    c = WideClient(X, y, dims, comm=comm if world > 1 else None, n_total=rows_per_client * world,
+                   micro_batch=micro_batch, lr=lr, dtype=dtype, seed=0)
+    losses, accs, times = [], [], []
+    for r in range(rounds):
+        t0 = time.perf_counter()
+        acc = c.run_round(evaluate=bool(eval_every) and (r + 1) % eval_every == 0)
+        loss = c.loss()          # joins the round (and its FedAvg buckets)
+        times.append(time.perf_counter() - t0)
+        losses.append(loss)
+        if acc is not None:
+            accs.append((r + 1, acc))
+        if verbose and rank == 0:
+            msg = f"Round {r + 1}: loss {loss:.5f}, {times[-1] * 1e3:.1f} ms"
+            if acc is not None:
+                msg += f", local accuracy {acc:.4f}"
+            print(msg, flush=True)
+    steady = times[1:] or times
+    dt = float(np.median(steady))
+    return {"loss": losses, "accuracy": accs, "round_s": times, "median_round_s": dt,
+            "tflops_per_client": c.flops_per_round / dt / 1e12,
+            "samples_per_s_per_client": rows_per_client / dt}

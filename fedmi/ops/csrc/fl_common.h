@@ -178,6 +178,17 @@ hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConf
                                const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_set_lds_limit_bf16(size_t bytes);
 // fp32 parameter image -> packed bf16 LDS-layout parameter region (MLPDescB)
+// Local evaluation + FedAvg in one kernel (world > 1 with the one-shot xGMI all-reduce,
+// peer_device.h): the all-reduce of the call described by `a` runs in extra blocks beside
+// the evaluation of `params` into this rank's tail slot of `comm` (the call's send buffer).
+struct PeerArgs;
+struct PeerPack;
+hipError_t fl_launch_eval_fedavg(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* params,
+                                 float* comm, const FLState* st, const PeerArgs& a, const PeerPack& pk,
+                                 hipStream_t s);
+hipError_t fl_launch_eval_fedavg_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                                      const float* params, float* comm, const FLState* st, const PeerArgs& a,
+                                      const PeerPack& pk, hipStream_t s);
 hipError_t fl_launch_pack_bf16(const MLPDesc& d, const MLPDescB& e, const float* params, char* out, hipStream_t s);
 // Stand-alone forward + confusion on an arbitrary row set (held-out evaluation).
 hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const int* y, int n_rows,

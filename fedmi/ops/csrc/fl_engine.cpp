@@ -208,6 +208,7 @@ class FLEngine {
         // post-step local model: one client (FedAvg of one is the identity, agg_scale 1).
         fused_ = cfg.contains("fused_eval") && cfg["fused_eval"].cast<bool>() && c_.world == 1 &&
                  c_.agg_scale == 1.0f;
+        eval_fedavg_ = !cfg.contains("eval_fedavg") || cfg["eval_fedavg"].cast<bool>();
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
@@ -329,12 +330,15 @@ class FLEngine {
     // round publishes into the peer object's send buffers, and its kernel writes the reduced
     // image into this engine's parameter buffer (plus, in bf16 mode, the packed bf16 image).
     void attach_peer(PeerAllReduce& p) {
-        if (c_.world < 2 || p.world() != c_.world || p.rank() != c_.rank || !p.is_open())
+        // (world 1 is accepted: a one-rank "all-reduce" emulates the multi-client round on
+        // one GPU for measurements, tools/round_emulate.py)
+        if (fused_ || p.world() != c_.world || p.rank() != c_.rank || !p.is_open())
             throw std::runtime_error("attach_peer: communicator does not match this engine");
         if (p.n_floats() != (long long)(d_.Pimg + c_.tail_len))
             throw std::runtime_error("attach_peer: buffer length != parameter image + tails");
         drop_graph();
         peer_ = &p;
+        p.prepare_eval((c_.n_rows + c_.R - 1) / c_.R);
         std::memset(&pp_, 0, sizeof(pp_));
         if (dtype_ == 1) {
             pp_.pk = b_.pk_global;
@@ -422,6 +426,8 @@ class FLEngine {
         o["ld"] = ld;
         o["dims"] = dims;
         o["lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : e_.lds_bytes;
+        o["eval_lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : ev_.lds_bytes;
+        o["eval_fedavg"] = peer_ != nullptr && !fused_ && eval_fedavg_fits();
         o["dtype"] = dtype_;
         o["slab_stride"] = c_.slab_stride;
         o["n_slabs"] = c_.n_slabs;
@@ -455,6 +461,22 @@ class FLEngine {
         e_.lds_bytes = off;
         e_.item_base[0] = 0;
         for (int l = 0; l < L; ++l) e_.item_base[l + 1] = e_.item_base[l] + e_.kp[l + 1] * (e_.kp[l] >> 3);
+        // Evaluation kernels run the forward pass only: their layout drops the delta buffers,
+        // which brings a 14-50-200-2 workgroup at R = 32 under half the CU's LDS (two blocks
+        // per CU), so the fused evaluation + FedAvg grid (evaluation blocks + all-reduce
+        // blocks > 256) stays resident in one wave.
+        ev_ = e_;
+        off = 0;
+        for (int l = 0; l < L; ++l) ev_.act_off[l] = take(R * e_.lda[l] * 2);
+        for (int l = 1; l <= L; ++l) ev_.dlt_off[l] = -1;
+        ev_.logit_off = take(R * 16 * 4);
+        ev_.cm_off = take(FL_CM_INTS * 4);
+        ev_.param_off = off;
+        for (int l = 0; l < L; ++l) {
+            ev_.w_off[l] = e_.w_off[l] - e_.param_off + ev_.param_off;
+            ev_.bias_off[l] = e_.bias_off[l] - e_.param_off + ev_.param_off;
+        }
+        ev_.lds_bytes = ev_.param_off + e_.param_bytes;
     }
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
                       int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr) {
@@ -480,7 +502,7 @@ class FLEngine {
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
-        else HIP_CHECK(fl_launch_eval_bf16(d_, e_, c_, b_, params, comm, st, s));
+        else HIP_CHECK(fl_launch_eval_bf16(d_, ev_, c_, b_, params, comm, st, s));
     }
     // Train/Adam pairs of round r.  Fused rounds (fl_common.h FL_EVAL_FUSED): the first train
     // kernel also scores the previous round's model from its own forward pass, and the first
@@ -517,7 +539,7 @@ class FLEngine {
     // all-reduce's send buffer, or, for RCCL, the parameter buffer it reduces in place.
     float* comm_buf(int r) const { return peer_ != nullptr ? peer_->send((r + 1) & 1) : pbuf_[(r + 1) & 1]; }
     void issue_allreduce(int r, hipStream_t s, RcclComm* comm) {
-        if (c_.world < 2) return;
+        if (c_.world < 2 && peer_ == nullptr) return;
         if (peer_ != nullptr)
             HIP_CHECK(peer_->launch((r + 1) & 1, pbuf_[(r + 1) & 1], dtype_ == 1 ? &pp_ : nullptr, s));
         else if (comm != nullptr)
@@ -527,11 +549,36 @@ class FLEngine {
         const bool fused = fused_ && allow_fused;
         if (!fused) flush_pending_eval(r, s);
         issue_train(r, s, fused);
+        if (!fused && peer_ != nullptr && eval_fedavg_fits()) {
+            // evaluation and the one-shot all-reduce in one kernel (peer_device.h)
+            issue_eval_fedavg(r, s);
+            cm_in_tail_ = true;
+            return;
+        }
         if (!fused) {
             issue_eval(r, s);
             cm_in_tail_ = true;
         }
         issue_allreduce(r, s, comm);
+    }
+    // The fused evaluation + FedAvg grid (evaluation blocks + all-reduce blocks) must be
+    // resident in one wave, which needs two evaluation workgroups per CU (measured: with one
+    // per CU the extra blocks spill into a second wave and the fused kernel loses to the
+    // separate kernels, tools/round_emulate.py).
+    bool eval_fedavg_fits() const {
+        const size_t lds = dtype_ == 0 ? (size_t)d_.lds_floats * 4 : (size_t)ev_.lds_bytes;
+        return eval_fedavg_ && 2 * lds <= (size_t)160 * 1024;
+    }
+    void issue_eval_fedavg(int r, hipStream_t s) {
+        const int p = (r + 1) & 1;
+        const PeerArgs a = peer_->args(p, pbuf_[p], d_.Pimg);
+        PeerPack pk;
+        std::memset(&pk, 0, sizeof(pk));
+        if (dtype_ == 1) pk = pp_;
+        if (dtype_ == 0)
+            HIP_CHECK(fl_launch_eval_fedavg(d_, c_, b_, b_.local, comm_buf(r), st_[(r + 1) & 1], a, pk, s));
+        else
+            HIP_CHECK(fl_launch_eval_fedavg_bf16(d_, ev_, c_, b_, b_.local, comm_buf(r), st_[(r + 1) & 1], a, pk, s));
     }
 
     void drop_graph() {
@@ -542,11 +589,13 @@ class FLEngine {
 
     MLPDesc d_;
     MLPDescB e_;
+    MLPDescB ev_;  // evaluation-only layout of e_ (no delta buffers)
     int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
     char* pk_ = nullptr;
     bool need_pack_ = true;  // host changed the global weights: repack before the next round
     PeerAllReduce* peer_ = nullptr;  // one-shot xGMI all-reduce (nullptr: RCCL)
     PeerPack pp_;                    // its bf16 pack epilogue (bf16 mode)
+    bool eval_fedavg_ = true;  // world > 1 with peer: evaluation + all-reduce in one kernel
     bool fused_ = false;       // rounds evaluate the previous round inside the train kernel
     bool pending_cm_ = false;  // the last issued round was fused: its metrics are not scored yet
     bool cm_in_tail_ = false;  // the last round's counts sit in the tail, not yet folded

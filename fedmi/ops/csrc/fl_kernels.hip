@@ -23,6 +23,7 @@
 // VALU with a fixed-order split-K shuffle reduction.
 #include "fl_common.h"
 #include "fl_device.h"
+#include "peer_device.h"
 #include <math.h>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -539,14 +540,11 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,
 // argmax, confusion counts into this rank's tail (exact: integer-valued fp32 < 2^24).
 template <int RT>
-__global__ void __launch_bounds__(FL_THREADS)
-fl_eval_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ params,
-               float* __restrict__ cm_out, const FLState* __restrict__ st) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
+__device__ void eval_rows(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* __restrict__ params,
+                          float* __restrict__ cm_out, int blk, float* lds) {
     __shared__ int cm_s[FL_MAX_CLASSES * FL_MAX_CLASSES];
-    if (st != nullptr && !st->live) return;
     const int R = RT * 16;
-    const int row0 = blockIdx.x * R;
+    const int row0 = blk * R;
     const int C = d.dim[d.L];
     float* acts = lds;
     float* li = lds + d.img_lds;
@@ -575,6 +573,32 @@ fl_eval_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ par
     for (int e = threadIdx.x; e < C * C; e += FL_THREADS)
         if (cm_s[e]) atomicAdd(&cm_out[e], (float)cm_s[e]);
     FL_STAMP(15);
+}
+
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_eval_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ params,
+               float* __restrict__ cm_out, const FLState* __restrict__ st) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (st != nullptr && !st->live) return;
+    eval_rows<RT>(d, c, b, params, cm_out, blockIdx.x, lds);
+}
+
+// Local evaluation + FedAvg in one kernel (world > 1, one-shot xGMI all-reduce); see
+// fl_eval_fedavg_bf16_kernel.
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_eval_fedavg_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ params,
+                      float* __restrict__ cm_out, const FLState* __restrict__ st, PeerArgs a, PeerPack pk, int n_ar) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const unsigned target = peer_target(a);
+    if ((int)blockIdx.x < n_ar) {
+        peer_fused_reduce(a, pk, target, blockIdx.x, n_ar);
+        peer_finish(a, target, n_ar);
+    } else {
+        if (st->live) eval_rows<RT>(d, c, b, params, cm_out, blockIdx.x - n_ar, lds);
+        peer_eval_done(a, target, blockIdx.x - n_ar);
+    }
 }
 
 __global__ void fl_finalize_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
@@ -699,6 +723,27 @@ hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
     }
 }
 
+hipError_t fl_launch_eval_fedavg(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* params,
+                                 float* comm, const FLState* st, const PeerArgs& a, const PeerPack& pk,
+                                 hipStream_t s) {
+    float* cm = comm + c.tail_off + c.rank * c.tail_stride;
+    const int blocks = nblocks(c.n_rows, c.R);
+    const int n_ar = fl_fedavg_blocks(a.n_w);
+    if (a.eflags == nullptr || a.n_eval != blocks) return hipErrorInvalidValue;
+    switch (c.R) {
+        case 16:
+            hipLaunchKernelGGL(fl_eval_fedavg_kernel<1>, dim3(n_ar + blocks), dim3(FL_THREADS), lds_bytes(d), s, d, c,
+                               b, params, cm, st, a, pk, n_ar);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_eval_fedavg_kernel<2>, dim3(n_ar + blocks), dim3(FL_THREADS), lds_bytes(d), s, d, c,
+                               b, params, cm, st, a, pk, n_ar);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pg,
                               const FLState* si, FLState* so, hipStream_t s) {
     hipLaunchKernelGGL(fl_finalize_kernel, dim3(1), dim3(64), 0, s, d, c, b, pg, si, so);
@@ -740,6 +785,7 @@ hipError_t fl_set_lds_limit(size_t bytes) {
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, b)
     FL_SET(fl_train_kernel<1>); FL_SET(fl_train_kernel<2>);
     FL_SET(fl_eval_kernel<1>); FL_SET(fl_eval_kernel<2>);
+    FL_SET(fl_eval_fedavg_kernel<1>); FL_SET(fl_eval_fedavg_kernel<2>);
 #undef FL_SET
     return e;
 }

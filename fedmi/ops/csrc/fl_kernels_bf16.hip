@@ -19,6 +19,7 @@
 // (FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:12-25, 63-73), evaluation C:75-91.
 #include "fl_common.h"
 #include "fl_device.h"
+#include "peer_device.h"
 #include <math.h>
 #include <stdint.h>
 
@@ -373,15 +374,14 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     FL_STAMP(15);
 }
 
+// Local evaluation of one row block (rows [blk*R, blk*R + R)) of the post-step model:
+// forward, argmax, confusion counts added to cm_out (exact: integer-valued fp32 < 2^24).
 template <int RT>
-__global__ void __launch_bounds__(FL_THREADS)
-fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ params,
-                    float* __restrict__ cm_out, const FLState* __restrict__ st) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ void eval_rows_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                               const float* __restrict__ params, float* __restrict__ cm_out, int blk, char* lds) {
     __shared__ int cm_s[FL_MAX_CLASSES * FL_MAX_CLASSES];
-    if (st != nullptr && !st->live) return;
     const int R = RT * 16;
-    const int row0 = blockIdx.x * R;
+    const int row0 = blk * R;
     const int C = d.dim[d.L];
     FL_STAMP(0);
     for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
@@ -409,6 +409,38 @@ fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float*
     for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
         if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
     FL_STAMP(15);
+}
+
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ params,
+                    float* __restrict__ cm_out, const FLState* __restrict__ st) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    if (st != nullptr && !st->live) return;
+    eval_rows_bf16<RT>(d, e, c, b, params, cm_out, blockIdx.x, lds);
+}
+
+// Local evaluation + FedAvg in one kernel (world > 1, one-shot xGMI all-reduce;
+// peer_device.h).  Blocks [0, n_ar) all-reduce: they pull and sum the peers' weights as soon
+// as every rank published them -- the weights were complete when the Adam kernel ended --
+// and, once every rank's evaluation is done, the metric tails.  Blocks [n_ar, grid) evaluate
+// the post-step local model on the shard into this rank's tail slot; the last of them
+// publishes the tails.  The all-reduce's waiting and xGMI latency hide behind the
+// evaluation instead of following it.
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_eval_fedavg_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ params,
+                           float* __restrict__ cm_out, const FLState* __restrict__ st, PeerArgs a, PeerPack pk,
+                           int n_ar) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const unsigned target = peer_target(a);
+    if ((int)blockIdx.x < n_ar) {
+        peer_fused_reduce(a, pk, target, blockIdx.x, n_ar);
+        peer_finish(a, target, n_ar);
+    } else {
+        if (st->live) eval_rows_bf16<RT>(d, e, c, b, params, cm_out, blockIdx.x - n_ar, lds);
+        peer_eval_done(a, target, blockIdx.x - n_ar);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -450,6 +482,27 @@ hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConf
     return hipGetLastError();
 }
 
+hipError_t fl_launch_eval_fedavg_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                                      const float* params, float* comm, const FLState* st, const PeerArgs& a,
+                                      const PeerPack& pk, hipStream_t s) {
+    float* cm = comm + c.tail_off + c.rank * c.tail_stride;
+    const int blocks = (c.n_rows + c.R - 1) / c.R;
+    const int n_ar = fl_fedavg_blocks(a.n_w);
+    if (a.eflags == nullptr || a.n_eval != blocks) return hipErrorInvalidValue;
+    switch (c.R) {
+        case 16:
+            hipLaunchKernelGGL(fl_eval_fedavg_bf16_kernel<1>, dim3(n_ar + blocks), dim3(FL_THREADS), e.lds_bytes, s, d,
+                               e, c, b, params, cm, st, a, pk, n_ar);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_eval_fedavg_bf16_kernel<2>, dim3(n_ar + blocks), dim3(FL_THREADS), e.lds_bytes, s, d,
+                               e, c, b, params, cm, st, a, pk, n_ar);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t fl_launch_pack_bf16(const MLPDesc& d, const MLPDescB& e, const float* params, char* out, hipStream_t s) {
     int bias_items = 0;
     for (int l = 0; l < d.L; ++l) bias_items += e.kp[l + 1];
@@ -466,6 +519,7 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
     r = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, v)
     FLB_SET(fl_train_bf16_kernel<1>); FLB_SET(fl_train_bf16_kernel<2>);
     FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>);
+    FLB_SET(fl_eval_fedavg_bf16_kernel<1>); FLB_SET(fl_eval_fedavg_bf16_kernel<2>);
 #undef FLB_SET
     return r;
 }

@@ -7,27 +7,8 @@
 #include <vector>
 
 #include "fl_common.h"
+#include "peer_device.h"
 
-#define PEER_MAX_WORLD 8  // one node: every GPU has a direct xGMI link to each of its 7 peers
-
-// Optional epilogue of the reduction: also write the reduced fp32 parameter image as the
-// packed bf16 LDS image the bf16 train kernel stages (fl_kernels_bf16.hip, MLPDescB), so the
-// separate pack kernel after FedAvg disappears.  Offsets are in float4 units of the fp32
-// image (fl_common.h layout) and bytes of the packed region.
-struct PeerPack {
-    char* pk;                       // packed region (nullptr: no packing)
-    int L;
-    int img4_w[FL_MAX_LAYERS];      // first float4 of W_l in the image
-    int img4_b[FL_MAX_LAYERS];      // first float4 of b_l
-    int img4_end[FL_MAX_LAYERS];    // one past the last float4 of b_l
-    int ldw4[FL_MAX_LAYERS];        // float4s per image row of W_l
-    int k4[FL_MAX_LAYERS];          // packed float4 columns per row: roundup16(K_l) / 4
-    int pk_w[FL_MAX_LAYERS];        // byte offset of W_l in the packed region
-    int pk_lda[FL_MAX_LAYERS];      // packed row stride (bf16 elements)
-    int pk_b[FL_MAX_LAYERS];        // byte offset of b_l in the packed region
-};
-
-struct PeerCtl;
 
 class PeerAllReduce {
   public:
@@ -41,6 +22,12 @@ class PeerAllReduce {
     float* send(int parity) const;                      // this rank's send buffer of a parity
     // out[0:n] = sum over ranks (rank order) of send(parity); optional bf16 pack epilogue
     hipError_t launch(int parity, float* out, const PeerPack* pack, hipStream_t s) const;
+    // Kernel arguments of a call on `parity` writing `out` (peer_device.h), for kernels that
+    // fuse the all-reduce with other work; `n_w` = floats of the weights part (default: all
+    // whole float4s).
+    PeerArgs args(int parity, float* out, long long n_w = -1) const;
+    // Per-block completion flags for fused calls with `n_eval` evaluation blocks.
+    void prepare_eval(int n_eval);
     // Zero both send buffers (image padding is never written by the engine's kernels and
     // must read as 0).  Call only while no peer is reading: after a host barrier.
     void clear();
@@ -61,6 +48,8 @@ class PeerAllReduce {
     char* peer_base_[PEER_MAX_WORLD] = {};
     long long timeout_ticks_ = 0;      // s_memrealtime ticks (100 MHz)
     bool open_ = false;
+    unsigned* eflags_ = nullptr;       // fused calls: one completion flag per evaluation block
+    int n_eval_ = 0;
 };
 
 void register_peer(pybind11::module_& m);

@@ -37,121 +37,23 @@ namespace py = pybind11;
 #define PEER_THREADS 256
 #define PEER_MAX_BLOCKS 64
 
-struct PeerCtl {
-    unsigned flags[PEER_MAX_WORLD];  // flags[j]: last call rank j has published to this rank
-    unsigned seq;                    // calls this rank has completed
-    unsigned done;                   // blocks of the running call that have finished
-    unsigned err;                    // sticky: a wait timed out
-    unsigned pad[64 - PEER_MAX_WORLD - 3];
-};
-static_assert(sizeof(PeerCtl) == 256, "PeerCtl is one 256-byte block");
-
-struct PeerArgs {
-    const float* src[PEER_MAX_WORLD];  // every rank's send buffer of this parity (mapped)
-    unsigned* flag_dst[PEER_MAX_WORLD];  // &ctl_j->flags[rank]
-    PeerCtl* ctl;                      // this rank's control block
-    float* out;
-    long long n;                       // floats
-    long long timeout;                 // s_memrealtime ticks
-};
-
 static void phip(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e) + " at " + what);
 }
 #define PHIP(expr) phip((expr), #expr)
 
-__device__ __forceinline__ uint32_t bf16_rne(float x) {
-    const uint32_t u = __float_as_uint(x);
-    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-}
-
-// System-coherent (sc0 sc1: aux 17) buffer loads: they bypass this GPU's L1 and L2, so a
-// peer's buffer is read from its memory as published, with no stale local copy.
-__device__ __forceinline__ float4 load_sys16(const float* base, int bytes, int off) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes,
-                                                                         0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17);
-    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
-}
-__device__ __forceinline__ float load_sys4(const float* base, int bytes, int off) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes,
-                                                                         0x00020000);
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 17));
-}
-
-// Image float4 i (fp32 parameter image) -> packed bf16 LDS image (PeerPack).
-__device__ __forceinline__ void pack_store(const PeerPack& p, int i, float4 s) {
-#pragma unroll
-    for (int l = 0; l < FL_MAX_LAYERS; ++l) {
-        if (l >= p.L || i < p.img4_w[l] || i >= p.img4_end[l]) continue;
-        if (i < p.img4_b[l]) {
-            const int q = i - p.img4_w[l];
-            const int n = q / p.ldw4[l], c4 = q - n * p.ldw4[l];
-            if (c4 < p.k4[l])  // columns [roundup16(K), ldw) are the image's zero pad
-                *reinterpret_cast<uint2*>(p.pk + p.pk_w[l] + (n * p.pk_lda[l] + 4 * c4) * 2) =
-                    make_uint2(bf16_rne(s.x) | (bf16_rne(s.y) << 16), bf16_rne(s.z) | (bf16_rne(s.w) << 16));
-        } else {
-            *reinterpret_cast<float4*>(p.pk + p.pk_b[l] + (i - p.img4_b[l]) * 16) = s;
-        }
-    }
-}
-
-template <int W>
+// Standalone call: both parts were written by earlier kernels on this stream, so both flags
+// are published at once; then every block pulls its share of all send buffers.
 __global__ void __launch_bounds__(PEER_THREADS) peer_allreduce_kernel(PeerArgs a, PeerPack pk) {
-    __shared__ unsigned target_s;
-    const int tid = threadIdx.x;
-    if (tid == 0) target_s = __hip_atomic_load(&a.ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    __syncthreads();
-    const unsigned target = target_s;
-    // publish this rank's send buffer for call `target` to every rank (itself included)
-    if (blockIdx.x == 0 && tid < W)
-        __hip_atomic_store(a.flag_dst[tid], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // wait until every rank has published call `target`: one polling lane per rank, bounded
-    if (tid < W) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while ((int)(__hip_atomic_load(&a.ctl->flags[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
-            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
-                __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
+    const unsigned target = peer_target(a);
+    if (blockIdx.x == 0) {
+        peer_publish(a.flag_dst, a.world, target);
+        peer_publish(a.tflag_dst, a.world, target);
     }
-    __syncthreads();
-    // pull + reduce in rank order: every rank computes the same bits
-    const int bytes = (int)(a.n * 4);
-    const long long n4 = a.n >> 2;
-    for (long long i = (long long)blockIdx.x * PEER_THREADS + tid; i < n4; i += (long long)gridDim.x * PEER_THREADS) {
-        float4 v[W];
-#pragma unroll
-        for (int j = 0; j < W; ++j) v[j] = load_sys16(a.src[j], bytes, (int)(i * 16));
-        float4 s = v[0];
-#pragma unroll
-        for (int j = 1; j < W; ++j) {
-            s.x += v[j].x;
-            s.y += v[j].y;
-            s.z += v[j].z;
-            s.w += v[j].w;
-        }
-        reinterpret_cast<float4*>(a.out)[i] = s;
-        if (pk.pk != nullptr) pack_store(pk, (int)i, s);
-    }
-    if (blockIdx.x == 0)
-        for (long long e = n4 * 4 + tid; e < a.n; e += PEER_THREADS) {
-            float s = load_sys4(a.src[0], bytes, (int)(e * 4));
-#pragma unroll
-            for (int j = 1; j < W; ++j) s += load_sys4(a.src[j], bytes, (int)(e * 4));
-            a.out[e] = s;
-        }
-    // the last block to finish advances the call counter (every block has read it by then)
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(&a.ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == gridDim.x - 1) {
-            __hip_atomic_store(&a.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl->seq, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    peer_wait(a, a.ctl->flags, target);
+    peer_reduce4(a, pk, 0, a.n >> 2, blockIdx.x, gridDim.x);
+    if (blockIdx.x == 0) peer_reduce1(a, a.n & ~3ll, a.n);
+    peer_finish(a, target, gridDim.x);
 }
 
 // Self-test payload: exact in fp32 for any summation order (multiples of 1/4 in [-256, 256)).
@@ -164,7 +66,7 @@ __global__ void peer_fill_kernel(float* dst, long long n, int rank, unsigned sal
 
 PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, double timeout_s)
     : world_(world), rank_(rank), device_(device), n_(n) {
-    if (world < 2 || world > PEER_MAX_WORLD) throw std::runtime_error("PeerAllReduce: world must be 2..8");
+    if (world < 1 || world > PEER_MAX_WORLD) throw std::runtime_error("PeerAllReduce: world must be 1..8");
     if (rank < 0 || rank >= world) throw std::runtime_error("PeerAllReduce: bad rank");
     if (n <= 0 || n * 4 > (1ll << 30)) throw std::runtime_error("PeerAllReduce: 1..2^28 floats");
     PHIP(hipSetDevice(device));
@@ -192,11 +94,16 @@ PeerAllReduce::~PeerAllReduce() {
 }
 
 void PeerAllReduce::close() {
-    for (char* p : mapped_) hipIpcCloseMemHandle(p);
+    for (char* p : mapped_) (void)hipIpcCloseMemHandle(p);
     mapped_.clear();
     open_ = false;
+    if (eflags_) {
+        (void)hipFree(eflags_);
+        eflags_ = nullptr;
+        n_eval_ = 0;
+    }
     if (base_) {
-        hipFree(base_);
+        (void)hipFree(base_);
         base_ = nullptr;
     }
 }
@@ -230,6 +137,24 @@ void PeerAllReduce::open(const std::vector<py::bytes>& handles) {
 
 float* PeerAllReduce::send(int parity) const { return reinterpret_cast<float*>(base_ + (parity & 1) * buf_bytes_); }
 
+void PeerAllReduce::prepare_eval(int n_eval) {
+    if (n_eval == n_eval_) return;
+    PHIP(hipSetDevice(device_));
+    if (eflags_ != nullptr) (void)hipFree(eflags_);
+    eflags_ = nullptr;
+    n_eval_ = 0;
+    const size_t bytes = (size_t)std::max(n_eval, 1) * sizeof(unsigned);
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&eflags_), bytes, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        eflags_ = nullptr;
+        PHIP(hipMalloc(reinterpret_cast<void**>(&eflags_), bytes));
+    }
+    // call indices are monotonic and start at 1: 0 = "no call finished yet"
+    PHIP(hipMemset(eflags_, 0, bytes));
+    PHIP(hipDeviceSynchronize());
+    n_eval_ = n_eval;
+}
+
 void PeerAllReduce::clear() {
     PHIP(hipSetDevice(device_));
     PHIP(hipMemset(base_, 0, 2 * buf_bytes_));
@@ -244,32 +169,35 @@ int PeerAllReduce::error() const {
     return (int)e;
 }
 
-hipError_t PeerAllReduce::launch(int parity, float* out, const PeerPack* pack, hipStream_t s) const {
-    if (!open_) return hipErrorNotInitialized;
+PeerArgs PeerAllReduce::args(int parity, float* out, long long n_w) const {
     PeerArgs a;
     std::memset(&a, 0, sizeof(a));
     for (int j = 0; j < world_; ++j) {
         a.src[j] = reinterpret_cast<const float*>(peer_base_[j] + (parity & 1) * buf_bytes_);
-        a.flag_dst[j] = &reinterpret_cast<PeerCtl*>(peer_base_[j] + 2 * buf_bytes_)->flags[rank_];
+        PeerCtl* cj = reinterpret_cast<PeerCtl*>(peer_base_[j] + 2 * buf_bytes_);
+        a.flag_dst[j] = &cj->flags[rank_];
+        a.tflag_dst[j] = &cj->tflags[rank_];
     }
     a.ctl = reinterpret_cast<PeerCtl*>(base_ + 2 * buf_bytes_);
     a.out = out;
     a.n = n_;
+    a.n_w = n_w < 0 ? (n_ & ~3ll) : n_w;
     a.timeout = timeout_ticks_;
+    a.eflags = eflags_;
+    a.n_eval = n_eval_;
+    a.world = world_;
+    return a;
+}
+
+hipError_t PeerAllReduce::launch(int parity, float* out, const PeerPack* pack, hipStream_t s) const {
+    if (!open_) return hipErrorNotInitialized;
+    const PeerArgs a = args(parity, out);
     PeerPack p;
     std::memset(&p, 0, sizeof(p));
     if (pack != nullptr) p = *pack;
     const long long n4 = n_ / 4;
     const int blocks = (int)std::min<long long>(PEER_MAX_BLOCKS, std::max<long long>(1, (n4 + PEER_THREADS - 1) / PEER_THREADS));
-    switch (world_) {
-#define PEER_CASE(W)                                                                                  \
-    case W:                                                                                           \
-        hipLaunchKernelGGL(peer_allreduce_kernel<W>, dim3(blocks), dim3(PEER_THREADS), 0, s, a, p);  \
-        break;
-        PEER_CASE(2) PEER_CASE(3) PEER_CASE(4) PEER_CASE(5) PEER_CASE(6) PEER_CASE(7) PEER_CASE(8)
-#undef PEER_CASE
-        default: return hipErrorInvalidValue;
-    }
+    hipLaunchKernelGGL(peer_allreduce_kernel, dim3(blocks), dim3(PEER_THREADS), 0, s, a, p);
     return hipGetLastError();
 }
 

@@ -1,0 +1,239 @@
+// Device side of the one-shot xGMI peer all-reduce (peer_allreduce.hip): control block,
+// kernel arguments and the publish / wait / pull-reduce building blocks.  Shared by the
+// standalone all-reduce kernel and the fused "local evaluation + FedAvg" kernels of the round
+// engine (fl_kernels.hip, fl_kernels_bf16.hip), which overlap the weight all-reduce with the
+// evaluation of the post-step local model.
+//
+// A call reduces [0, n) = [weights | metric tails].  Every rank publishes the two parts with
+// separate monotonic flags, so the weights can be pulled while the tails are still being
+// computed:
+//   * flags[j]  = last call whose WEIGHTS rank j has published to this rank;
+//   * tflags[j] = last call whose TAILS rank j has published (the standalone kernel publishes
+//     both at once; the fused kernel publishes tflags when its last evaluation block is done).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fl_common.h"
+
+#define PEER_MAX_WORLD 8  // one node: every GPU has a direct xGMI link to each of its 7 peers
+
+// Optional epilogue of the reduction: also write the reduced fp32 parameter image as the
+// packed bf16 LDS image the bf16 train kernel stages (fl_kernels_bf16.hip, MLPDescB), so the
+// separate pack kernel after FedAvg disappears.  Offsets are in float4 units of the fp32
+// image (fl_common.h layout) and bytes of the packed region.
+struct PeerPack {
+    char* pk;                       // packed region (nullptr: no packing)
+    int L;
+    int img4_w[FL_MAX_LAYERS];      // first float4 of W_l in the image
+    int img4_b[FL_MAX_LAYERS];      // first float4 of b_l
+    int img4_end[FL_MAX_LAYERS];    // one past the last float4 of b_l
+    int ldw4[FL_MAX_LAYERS];        // float4s per image row of W_l
+    int k4[FL_MAX_LAYERS];          // packed float4 columns per row: roundup16(K_l) / 4
+    int pk_w[FL_MAX_LAYERS];        // byte offset of W_l in the packed region
+    int pk_lda[FL_MAX_LAYERS];      // packed row stride (bf16 elements)
+    int pk_b[FL_MAX_LAYERS];        // byte offset of b_l in the packed region
+};
+
+
+struct PeerCtl {
+    unsigned flags[PEER_MAX_WORLD];   // weights published, per source rank
+    unsigned tflags[PEER_MAX_WORLD];  // tails published, per source rank
+    unsigned seq;                     // calls this rank has completed
+    unsigned done;                    // blocks of the running call that have finished
+    unsigned err;                     // sticky: a wait timed out
+    unsigned pad[64 - 2 * PEER_MAX_WORLD - 3];
+};
+static_assert(sizeof(PeerCtl) == 256, "PeerCtl is one 256-byte block");
+
+struct PeerArgs {
+    const float* src[PEER_MAX_WORLD];    // every rank's send buffer of this parity (mapped)
+    unsigned* flag_dst[PEER_MAX_WORLD];  // &ctl_j->flags[rank]
+    unsigned* tflag_dst[PEER_MAX_WORLD]; // &ctl_j->tflags[rank]
+    PeerCtl* ctl;                        // this rank's control block
+    float* out;
+    long long n;                         // floats in the call
+    long long n_w;                       // floats of the weights part (multiple of 4); tails = [n_w, n)
+    long long timeout;                   // s_memrealtime ticks
+    unsigned* eflags;                    // fused calls: per evaluation block, last call it finished
+    int n_eval;                          // evaluation blocks of a fused call
+    int world;
+};
+
+// All-reduce blocks of a fused evaluation + FedAvg kernel (FL_THREADS = 512 threads each):
+// one float4 of the weights per thread, at most 32 blocks.
+static inline int fl_fedavg_blocks(long long n_w) {
+    const long long n4 = n_w >> 2;
+    const long long nb = (n4 + 511) / 512;
+    return (int)(nb < 1 ? 1 : (nb > 32 ? 32 : nb));
+}
+
+__device__ __forceinline__ uint32_t peer_bf16_rne(float x) {
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// System-coherent (sc0 sc1: aux 17) buffer loads: they bypass this GPU's L1 and L2, so a
+// peer's buffer is read from its memory as published, with no stale local copy.
+__device__ __forceinline__ float4 peer_load16(const float* base, int bytes, int off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes,
+                                                                         0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+__device__ __forceinline__ float peer_load4(const float* base, int bytes, int off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes,
+                                                                         0x00020000);
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 17));
+}
+
+// Image float4 i (fp32 parameter image) -> packed bf16 LDS image (PeerPack).
+__device__ __forceinline__ void peer_pack_store(const PeerPack& p, int i, float4 s) {
+#pragma unroll
+    for (int l = 0; l < FL_MAX_LAYERS; ++l) {
+        if (l >= p.L || i < p.img4_w[l] || i >= p.img4_end[l]) continue;
+        if (i < p.img4_b[l]) {
+            const int q = i - p.img4_w[l];
+            const int n = q / p.ldw4[l], c4 = q - n * p.ldw4[l];
+            if (c4 < p.k4[l])  // columns [roundup16(K), ldw) are the image's zero pad
+                *reinterpret_cast<uint2*>(p.pk + p.pk_w[l] + (n * p.pk_lda[l] + 4 * c4) * 2) =
+                    make_uint2(peer_bf16_rne(s.x) | (peer_bf16_rne(s.y) << 16),
+                               peer_bf16_rne(s.z) | (peer_bf16_rne(s.w) << 16));
+        } else {
+            *reinterpret_cast<float4*>(p.pk + p.pk_b[l] + (i - p.img4_b[l]) * 16) = s;
+        }
+    }
+}
+
+// The call this kernel performs: one more than the calls completed (written by the last
+// block of the previous call, which finished before this kernel started).
+__device__ __forceinline__ unsigned peer_target(const PeerArgs& a) {
+    __shared__ unsigned target_s;
+    if (threadIdx.x == 0) target_s = __hip_atomic_load(&a.ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __syncthreads();
+    return target_s;
+}
+
+// Lanes 0..world-1: store `target` into every rank's flag slot for this rank.
+__device__ __forceinline__ void peer_publish(unsigned* const* dst, int world, unsigned target) {
+    if (threadIdx.x < (unsigned)world)
+        __hip_atomic_store(dst[threadIdx.x], target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wait until every rank has published `target` in `flags` (one polling lane per rank,
+// bounded by the timeout: on expiry the sticky error word is set and the wait ends).
+__device__ __forceinline__ void peer_wait(const PeerArgs& a, unsigned* flags, unsigned target) {
+    if (threadIdx.x < (unsigned)a.world) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        // relaxed: everything read after the wait uses cache-bypassing loads
+        while ((int)(__hip_atomic_load(&flags[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
+                __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+// out[4*i0 .. 4*i1) = sum over ranks, rank order (bit-identical on every rank); block `bid`
+// of `nb` blocks takes a grid-stride share.  Optional bf16 pack of the weights.
+__device__ __forceinline__ void peer_reduce4(const PeerArgs& a, const PeerPack& pk, long long i0, long long i1,
+                                             int bid, int nb) {
+    const int bytes = (int)(a.n * 4);
+    for (long long i = i0 + (long long)bid * blockDim.x + threadIdx.x; i < i1; i += (long long)nb * blockDim.x) {
+        float4 v[PEER_MAX_WORLD];
+#pragma unroll
+        for (int j = 0; j < PEER_MAX_WORLD; ++j)
+            if (j < a.world) v[j] = peer_load16(a.src[j], bytes, (int)(i * 16));
+        float4 s = v[0];
+#pragma unroll
+        for (int j = 1; j < PEER_MAX_WORLD; ++j)
+            if (j < a.world) {
+                s.x += v[j].x;
+                s.y += v[j].y;
+                s.z += v[j].z;
+                s.w += v[j].w;
+            }
+        reinterpret_cast<float4*>(a.out)[i] = s;
+        if (pk.pk != nullptr) peer_pack_store(pk, (int)i, s);
+    }
+}
+
+// Scalar reduce of floats [e0, e1) by one block.
+__device__ __forceinline__ void peer_reduce1(const PeerArgs& a, long long e0, long long e1) {
+    const int bytes = (int)(a.n * 4);
+    for (long long e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        float s = peer_load4(a.src[0], bytes, (int)(e * 4));
+#pragma unroll
+        for (int j = 1; j < PEER_MAX_WORLD; ++j)
+            if (j < a.world) s += peer_load4(a.src[j], bytes, (int)(e * 4));
+        a.out[e] = s;
+    }
+}
+
+// The `n_count` blocks that read the call's data call this last: the last of them to finish
+// advances the call counter.  (Blocks that only read `seq` at their start need not count if
+// some counting block waits for them, as the fused kernel's tail block does.)
+__device__ __forceinline__ void peer_finish(const PeerArgs& a, unsigned target, unsigned n_count) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // relaxed: seq is read only by the next call, after the kernel boundary
+        const unsigned prev = __hip_atomic_fetch_add(&a.ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == n_count - 1) {
+            __hip_atomic_store(&a.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->seq, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Wait (bounded) until every evaluation block of this call has stored `target` in its flag:
+// plain per-block stores into uncached memory, so no block serialises on a shared counter.
+__device__ __forceinline__ void peer_wait_eval(const PeerArgs& a, unsigned target) {
+    __shared__ int pending_s;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        int pend = 0;
+        for (int i = threadIdx.x; i < a.n_eval; i += blockDim.x)
+            pend |= (int)(__hip_atomic_load(&a.eflags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0;
+        if (threadIdx.x == 0) pending_s = 0;
+        __syncthreads();
+        if (pend) pending_s = 1;
+        __syncthreads();
+        const int any = pending_s;
+        __syncthreads();
+        if (!any) break;
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
+            if (threadIdx.x == 0) __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// Fused evaluation + FedAvg call, role of the all-reduce blocks (bid < nb): pull and reduce
+// the weights as soon as every rank published them, then the tails once every rank's
+// evaluation is done.  The tails are a few dozen floats: block 0 alone publishes and
+// reduces them.
+__device__ __forceinline__ void peer_fused_reduce(const PeerArgs& a, const PeerPack& pk, unsigned target, int bid,
+                                                  int nb) {
+    if (bid == 0) peer_publish(a.flag_dst, a.world, target);
+    peer_wait(a, a.ctl->flags, target);
+    peer_reduce4(a, pk, 0, a.n_w >> 2, bid, nb);
+    if (bid == 0) {
+        peer_wait_eval(a, target);
+        peer_publish(a.tflag_dst, a.world, target);
+        peer_wait(a, a.ctl->tflags, target);
+        peer_reduce1(a, a.n_w, a.n);
+    }
+}
+
+// Fused call, evaluation block `blk`: once its confusion counts are in the send buffer
+// (device-scope atomics into uncached memory, complete when acknowledged: vmcnt 0), it
+// stores the call index in its flag.
+__device__ __forceinline__ void peer_eval_done(const PeerArgs& a, unsigned target, int blk) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&a.eflags[blk], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

@@ -30,10 +30,10 @@ def _free_port():
     return p
 
 
-def _run_engine(comm, peer: bool, dtype: str, X, y, flat):
+def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = True):
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
     comm.peer_allreduce = peer
-    cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4)
+    cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4, eval_fedavg=eval_fedavg)
     e = HipRoundEngine(X, y, 2, cfg, comm, flat)
     assert e.aggregation == ("xgmi-oneshot" if peer else "host"), e.aggregation
     e.run(3)                       # eager rounds
@@ -45,6 +45,15 @@ def _run_engine(comm, peer: bool, dtype: str, X, y, flat):
     e.run(9)                       # graph-captured chunks
     e.sync_history()
     return e.global_flat(), e.history(), np.stack(cms)
+
+
+def _run_early_stop(comm, peer: bool, X, y, flat):
+    from fedmi.fl.engine import EngineConfig, HipRoundEngine
+    comm.peer_allreduce = peer
+    cfg = EngineConfig(max_rounds=200, patience=4, tolerance=2e-3, dtype="bf16", graph_rounds=8)
+    e = HipRoundEngine(X, y, 2, cfg, comm, flat)
+    e.run(200)
+    return e.global_flat(), e.history()
 
 
 def _worker(rank, port, q):
@@ -70,9 +79,12 @@ def _worker(rank, port, q):
         X, y = make_income_like(2400, seed=20 + rank)
         flat = init_flat([14, 50, 200, 2], 3)
         for dtype in ("fp32", "bf16"):
-            a = _run_engine(comm, True, dtype, X, y, flat)
-            b = _run_engine(comm, False, dtype, X, y, flat)
-            res[dtype] = (a, b)
+            a = _run_engine(comm, True, dtype, X, y, flat)            # fused eval + all-reduce kernel
+            b = _run_engine(comm, False, dtype, X, y, flat)           # host (gloo) aggregation
+            c = _run_engine(comm, True, dtype, X, y, flat, False)     # separate eval / peer kernels
+            res[dtype] = (a, b, c)
+        # early stop: rounds past the stop (non-live) must reproduce the stop round's model
+        res["es"] = (_run_early_stop(comm, True, X, y, flat), _run_early_stop(comm, False, X, y, flat))
         torch.cuda.synchronize()
         comm.Barrier()
         q.put((rank, res, None))
@@ -97,13 +109,20 @@ def test_peer_allreduce_two_ranks_one_gpu():
         for n in (4099, 50003):
             assert res[f"open{n}"] and res[f"self{n}"], (rank, n, res)
         for dtype in ("fp32", "bf16"):
-            (wa, ha, ca), (wb, hb, cb) = res[dtype]
+            (wa, ha, ca), (wb, hb, cb), (wc, hc, cc) = res[dtype]
+            np.testing.assert_array_equal(wc, wb, err_msg=f"{dtype} weights (separate kernels)")
+            np.testing.assert_array_equal(hc["global"], hb["global"])
             np.testing.assert_array_equal(wa, wb, err_msg=f"{dtype} weights")
             np.testing.assert_array_equal(ha["global"], hb["global"])
             np.testing.assert_array_equal(ha["per_rank"], hb["per_rank"])
             np.testing.assert_array_equal(ha["loss"], hb["loss"])
             np.testing.assert_array_equal(ca, cb)
             assert ha["rounds_run"] == 14
+        (we, he), (wf, hf) = res["es"]
+        assert he["stop_round"] > 0 and he["stop_round"] == hf["stop_round"], (he["stop_round"], hf["stop_round"])
+        assert he["rounds_run"] == hf["rounds_run"]
+        np.testing.assert_array_equal(we, wf)
+        np.testing.assert_array_equal(he["global"], hf["global"])
     # both ranks hold the same global model
     for dtype in ("fp32", "bf16"):
         np.testing.assert_array_equal(out[0][1][dtype][0][0], out[1][1][dtype][0][0])

@@ -1,0 +1,90 @@
+"""Wide-MLP federated rounds (BASELINE config 3 path, fedmi/fl/wide.py) with two clients sharing
+one GPU: the per-layer FedAvg buckets run on the comm stream and the next round's forward of
+layer l waits only on bucket l's event.  The result must equal a single-process simulation
+that averages the two clients' weights (n_i / N weighted) after every local step."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+DIMS = [14, 256, 128, 2]
+ROWS = (1536, 1024)
+ROUNDS = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(rank, dev):
+    import torch
+    from fedmi.data.synthetic import make_income_like
+    X, y = make_income_like(ROWS[rank], seed=40 + rank)
+    return torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
+
+
+def _worker(rank, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        import torch
+        from fedmi.fl.wide import WideClient
+        from fedmi.parallel.comm import Comm
+        comm = Comm(backend="xgmi", device="cuda:0", rccl=False)
+        X, y = _data(rank, comm.device)
+        c = WideClient(X, y, DIMS, comm=comm, n_total=sum(ROWS), micro_batch=512, dtype="bf16")
+        losses = []
+        for _ in range(ROUNDS):
+            c.run_round()
+            losses.append(c.loss())
+        c.sync()
+        torch.cuda.synchronize()
+        q.put((rank, c.params.cpu().numpy(), losses, None))
+        comm.Barrier()
+        comm.close()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+def test_wide_fedavg_buckets_match_simulation():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=110) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+    for rank, _, _, err in out:
+        assert err is None, f"rank {rank}:\n{err}"
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+    # single-process simulation of the same two clients
+    import torch
+    from fedmi.fl.wide import WideClient
+    dev = torch.device("cuda", 0)
+    cl = [WideClient(*_data(r, dev), DIMS, micro_batch=512, dtype="bf16") for r in range(2)]
+    n = sum(ROWS)
+    for _ in range(ROUNDS):
+        for c in cl:
+            c.local_step()
+            c.stream.synchronize()
+        avg = cl[0].params * (ROWS[0] / n) + cl[1].params * (ROWS[1] / n)
+        for c in cl:
+            c.params.copy_(avg)
+            c._quantize()
+            c.stream.synchronize()
+            c.round += 1
+    ref = cl[0].params.cpu().numpy()
+    err = np.max(np.abs(out[0][1] - ref)) / np.max(np.abs(ref))
+    assert err < 1e-6, err
