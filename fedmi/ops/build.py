@@ -50,12 +50,14 @@ def _digest(paths) -> str:
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(ARCH.encode())
+    h.update(os.environ.get("FEDMI_HIPCC_FLAGS", "").encode())
     return h.hexdigest()[:16]
 
 
 def _compile(src: str) -> str:
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    cmd = ["hipcc", "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}",
+    extra = os.environ.get("FEDMI_HIPCC_FLAGS", "").split()  # experiments, e.g. -DFL_THREADS=1024
+    cmd = ["hipcc", "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}", *extra,
            "-I" + CSRC, *_pybind_includes(), src, "-o", obj]
     if src.endswith(".cpp"):
         cmd[1:1] = ["-x", "hip"]

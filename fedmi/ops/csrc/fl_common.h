@@ -130,6 +130,11 @@ struct FLBuffers {
     unsigned long long* dbg;  // optional [blocks, 16] s_memrealtime phase stamps (profiling)
     char* pk_global;    // bf16 mode: packed LDS-layout image of the round's input weights
     char* pk_local;     // bf16 mode: packed LDS-layout image of the local (post-Adam) weights
+    // Adam + StepLR scalars per optimizer step t = 1 .. max_rounds * local_steps, computed on
+    // the host in double exactly as torch does (python float pow): [t-1] = {step_size,
+    // sqrt(bias_correction2)} rounded to fp32.  A table lookup instead of three double pow()
+    // on the Adam kernel's critical path.
+    const float* sched;
 };
 
 // Evaluation placement of a round (`mode` of the train kernels).

@@ -17,6 +17,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <cmath>
 #include <vector>
 
 #include "fl_common.h"
@@ -223,6 +224,20 @@ class FLEngine {
         pbuf_[1] = as_ptr<float>(bufs["params1"].cast<uintptr_t>());
         st_[0] = as_ptr<FLState>(bufs["state0"].cast<uintptr_t>());
         st_[1] = as_ptr<FLState>(bufs["state1"].cast<uintptr_t>());
+        {
+            // Adam/StepLR schedule (fl_common.h FLBuffers::sched): torch's host arithmetic
+            const int T = std::max(1, c_.max_rounds) * std::max(1, c_.local_steps);
+            std::vector<float> sch(2 * (size_t)T);
+            for (int t = 1; t <= T; ++t) {
+                const int round = (t - 1) / std::max(1, c_.local_steps);
+                const double lr = c_.lr0 * std::pow(c_.gamma, (double)(round / c_.step_size));
+                sch[2 * (t - 1)] = (float)(lr / (1.0 - std::pow(c_.beta1, (double)t)));
+                sch[2 * (t - 1) + 1] = (float)std::sqrt(1.0 - std::pow(c_.beta2, (double)t));
+            }
+            HIP_CHECK(hipMalloc(&sched_, sch.size() * sizeof(float)));
+            HIP_CHECK(hipMemcpy(sched_, sch.data(), sch.size() * sizeof(float), hipMemcpyHostToDevice));
+            b_.sched = sched_;
+        }
         if (dtype_ == 1) {
             // packed bf16 parameter regions; padding stays zero forever
             HIP_CHECK(hipMalloc(&pk_, 2 * (size_t)e_.param_bytes));
@@ -234,7 +249,8 @@ class FLEngine {
 
     ~FLEngine() {
         drop_graph();
-        if (pk_) hipFree(pk_);
+        if (pk_) (void)hipFree(pk_);
+        if (sched_) (void)hipFree(sched_);
     }
 
     // Issue rounds [r0, r0 + n): per round the train/Adam pair (one per local step), the
@@ -592,6 +608,7 @@ class FLEngine {
     MLPDescB ev_;  // evaluation-only layout of e_ (no delta buffers)
     int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
     char* pk_ = nullptr;
+    float* sched_ = nullptr;  // Adam/StepLR scalars per optimizer step
     bool need_pack_ = true;  // host changed the global weights: repack before the next round
     PeerAllReduce* peer_ = nullptr;  // one-shot xGMI all-reduce (nullptr: RCCL)
     PeerPack pp_;                    // its bf16 pack epilogue (bf16 mode)

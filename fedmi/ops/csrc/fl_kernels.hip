@@ -230,8 +230,8 @@ __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int o0 = ot0 * 16 + lg * 4 + j, o1 = ot1 * 16 + lg * 4 + j;
-            if (i0 < K && o0 < N) gW[o0 * K + i0] = acc0[j];
-            if (has1 && i1 < K && o1 < N) gW[o1 * K + i1] = acc1[j];
+            if (i0 < K && o0 < N) slab_store(&gW[o0 * K + i0], acc0[j]);
+            if (has1 && i1 < K && o1 < N) slab_store(&gW[o1 * K + i1], acc1[j]);
         }
     }
     for (int o = threadIdx.x; o < N; o += FL_THREADS) {
@@ -241,7 +241,7 @@ __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float
             s0 += dz[r * ld_z + o];
             s1 += dz[(r + 1) * ld_z + o];
         }
-        gb[o] = s0 + s1;
+        slab_store(&gb[o], s0 + s1);
     }
 }
 
@@ -490,7 +490,8 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
 #pragma unroll
             for (int u = 0; u < ADAM_DEPTH; ++u) {
                 const int s = s0 + u * ADAM_WAVES;
-                const float v = sp[(size_t)(s < c.n_slabs ? s : 0) * c.slab_stride];  // unpredicated
+                // unpredicated; non-temporal: the slab is read once
+                const float v = __builtin_nontemporal_load(&sp[(size_t)(s < c.n_slabs ? s : 0) * c.slab_stride]);
                 x[u] = s < c.n_slabs ? v : 0.f;
             }
 #pragma unroll
@@ -515,9 +516,8 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
     // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
     const int t = S.cur_round * c.local_steps + local_step + 1;
-    const double lr = c.lr0 * pow(c.gamma, (double)(S.cur_round / c.step_size));
-    const float step_size = (float)(lr / (1.0 - pow(c.beta1, (double)t)));
-    const float bc2_sqrt = (float)sqrt(1.0 - pow(c.beta2, (double)t));
+    const float step_size = b.sched[2 * (t - 1)];
+    const float bc2_sqrt = b.sched[2 * (t - 1) + 1];
     float m = b.m[j], v = b.v[j];
     m = m + c.omb1 * (g - m);
     v = v * c.beta2f + c.omb2 * g * g;

@@ -93,19 +93,60 @@ __global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restri
     }
 }
 
-// Stage the packed parameter region: a straight 16-byte copy (the padding is already zero).
-__device__ __forceinline__ void stage_params_bf16(const MLPDescB& e, const char* __restrict__ packed, char* lds) {
+// Stage the packed parameter region AND this block's input rows with every global load in
+// flight before the first LDS store: the two ~1 us L2 latencies overlap instead of adding.
+// Loads beyond STAGE_UNROLL per thread (large models) fall back to a loop.
+#define STAGE_P_UNROLL 4
+#define STAGE_X_UNROLL 2
+template <int RT>
+__device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const char* __restrict__ packed,
+                                                       const float* __restrict__ X, int n_rows, int F, int row0,
+                                                       char* lds) {
     const uint4* src = reinterpret_cast<const uint4*>(packed);
     uint4* dst = reinterpret_cast<uint4*>(lds + e.param_off);
     const int n16 = e.param_bytes >> 4;
-    for (int i = threadIdx.x; i < n16; i += FL_THREADS) dst[i] = src[i];
-}
-
-template <int RT>
-__device__ void stage_rows_bf16(const float* __restrict__ X, int n_rows, int F, int row0, char* act, int kp,
-                                int lda) {
-    uint16_t* a = reinterpret_cast<uint16_t*>(act);
-    for (int idx = threadIdx.x; idx < RT * 16 * kp; idx += FL_THREADS) {
+    const int kp = e.kp[0], lda = e.lda[0];
+    const int nx = RT * 16 * kp;
+    uint4 pv[STAGE_P_UNROLL];
+    float xv[STAGE_X_UNROLL];
+    // unpredicated loads (clamped indices): a conditionally written register array is
+    // demoted to scratch by the compiler
+#pragma unroll
+    for (int u = 0; u < STAGE_P_UNROLL; ++u) {
+        const int i = threadIdx.x + u * FL_THREADS;
+        pv[u] = src[i < n16 ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < STAGE_X_UNROLL; ++u) {
+        const int idx = threadIdx.x + u * FL_THREADS;
+        const int r = idx / kp, k = idx - r * kp;
+        const int row = row0 + r;
+        const bool ok = idx < nx && row < n_rows && k < F;
+        const float v = X[ok ? (size_t)row * F + k : 0];
+        xv[u] = ok ? v : 0.f;
+    }
+    // pin every load here (an empty asm consuming the registers): otherwise the compiler
+    // sinks each load into its conditional store below and the latencies serialise again
+#pragma unroll
+    for (int u = 0; u < STAGE_P_UNROLL; ++u) asm volatile("" ::"v"(pv[u].x), "v"(pv[u].y), "v"(pv[u].z), "v"(pv[u].w));
+#pragma unroll
+    for (int u = 0; u < STAGE_X_UNROLL; ++u) asm volatile("" ::"v"(xv[u]));
+    for (int i = threadIdx.x + STAGE_P_UNROLL * FL_THREADS; i < n16; i += FL_THREADS) dst[i] = src[i];
+#pragma unroll
+    for (int u = 0; u < STAGE_P_UNROLL; ++u) {
+        const int i = threadIdx.x + u * FL_THREADS;
+        if (i < n16) dst[i] = pv[u];
+    }
+    uint16_t* a = reinterpret_cast<uint16_t*>(lds + e.act_off[0]);
+#pragma unroll
+    for (int u = 0; u < STAGE_X_UNROLL; ++u) {
+        const int idx = threadIdx.x + u * FL_THREADS;
+        if (idx < nx) {
+            const int r = idx / kp, k = idx - r * kp;
+            a[r * lda + k] = (uint16_t)bf16_bits(xv[u]);
+        }
+    }
+    for (int idx = threadIdx.x + STAGE_X_UNROLL * FL_THREADS; idx < nx; idx += FL_THREADS) {
         const int r = idx / kp, k = idx - r * kp;
         const int row = row0 + r;
         const bool ok = row < n_rows && k < F;
@@ -198,7 +239,7 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int o = ot * 16 + 4 * lg + j;
-            if (i < K && o < N) gW[o * K + i] = acc[j];
+            if (i < K && o < N) slab_store(&gW[o * K + i], acc[j]);
         }
     }
     const uint16_t* Dh = reinterpret_cast<const uint16_t*>(D);
@@ -209,7 +250,7 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
             s0 += bf16_to_f32(Dh[r * ldd + o]);
             s1 += bf16_to_f32(Dh[(r + 1) * ldd + o]);
         }
-        gb[o] = s0 + s1;
+        slab_store(&gb[o], s0 + s1);
     }
 }
 
@@ -303,9 +344,9 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     const int row0 = blockIdx.x * R;
     const int L = d.L;
     const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
-    stage_params_bf16(e, (local_step == 0 && !stage_local) ? b.pk_global : b.pk_local, lds);
+    stage_params_rows_bf16<RT>(e, (local_step == 0 && !stage_local) ? b.pk_global : b.pk_local, b.X, c.n_rows,
+                               d.dim[0], row0, lds);
     FL_STAMP(8);
-    stage_rows_bf16<RT>(b.X, c.n_rows, d.dim[0], row0, lds + e.act_off[0], e.kp[0], e.lda[0]);
     {   // padding columns [C, kp[L]) of D_L never change: zero them here, off the CE's path
         const int padc = e.kp[L] - C;
         uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
@@ -342,12 +383,16 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
                 if (zr[k] > bv) { bv = zr[k]; best = k; }  // torch.max(dim=1): first maximum
             }
             if (score) atomicAdd(&cm_s[y * C + best], 1);
+            // hardware exp2/log2 (v_exp_f32 / v_log_f32): the deltas are rounded to bf16
+            // right after, far coarser than the fast intrinsics' error; the libm versions
+            // were a ~1 us dependent chain per round (in-kernel stamps)
             float se = 0.f;
-            for (int k = 0; k < C; ++k) se += expf(zr[k] - mx);
-            const float lse = mx + logf(se);
+            for (int k = 0; k < C; ++k) se += __expf(zr[k] - mx);
+            const float inv_se = 1.f / se;
+            const float lse = mx + __logf(se);
             lossv = (lse - zr[y]) * c.inv_n;
             for (int k = 0; k < C; ++k) {
-                const float p = expf(zr[k] - mx) / se;
+                const float p = __expf(zr[k] - mx) * inv_se;
                 dr[k] = (uint16_t)bf16_bits((p - (k == y ? 1.f : 0.f)) * c.inv_n);
             }
         } else {
@@ -386,9 +431,9 @@ __device__ void eval_rows_bf16(const MLPDesc& d, const MLPDescB& e, const FLConf
     FL_STAMP(0);
     for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
     const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
-    stage_params_bf16(e, params == b.local ? b.pk_local : b.pk_global, lds);
+    stage_params_rows_bf16<RT>(e, params == b.local ? b.pk_local : b.pk_global, b.X, c.n_rows, d.dim[0], row0,
+                               lds);
     FL_STAMP(8);
-    stage_rows_bf16<RT>(b.X, c.n_rows, d.dim[0], row0, lds + e.act_off[0], e.kp[0], e.lda[0]);
     FL_STAMP(9);
     lds_barrier();
     FL_STAMP(1);
