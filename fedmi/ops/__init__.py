@@ -22,6 +22,14 @@ def native(build_if_missing: bool = True):
     if _NATIVE is not None:
         return _NATIVE
     import torch  # noqa: F401  -- must load torch's libamdhip64/librccl before the extension
+    alt = os.environ.get("FEDMI_NATIVE_SO")  # A/B measurements of alternative builds
+    if alt:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("fedmi.ops._fedmi_hip", alt)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _NATIVE = mod
+        return _NATIVE
     try:
         _NATIVE = importlib.import_module("fedmi.ops._fedmi_hip")
         return _NATIVE
