@@ -24,9 +24,9 @@ def native(build_if_missing: bool = True):
     import torch  # noqa: F401  -- must load torch's libamdhip64/librccl before the extension
     alt = os.environ.get("FEDMI_NATIVE_SO")  # A/B measurements of alternative builds
     if alt:
-        import importlib.util
-        spec = importlib.util.spec_from_file_location("fedmi.ops._fedmi_hip", alt)
-        mod = importlib.util.module_from_spec(spec)
+        from importlib import util as _ilu
+        spec = _ilu.spec_from_file_location("fedmi.ops._fedmi_hip", alt)
+        mod = _ilu.module_from_spec(spec)
         spec.loader.exec_module(mod)
         _NATIVE = mod
         return _NATIVE

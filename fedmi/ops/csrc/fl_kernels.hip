@@ -413,11 +413,14 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     // Round state.  Fused evaluation (fl_common.h): wave 0 of EVERY block folds the previous
     // round's tail (anchor = this round's input image) into the previous state and decides
     // whether this round is live -- the same deterministic computation everywhere, so no
-    // block waits for another; block 0 publishes it.  It overlaps the slab loads below.
-    if (wave == 0) {
+    // block waits for another; block 0 publishes it.  Without early stopping the fold cannot
+    // change the decision and only block 0 (history) runs it.  Called after the wave issued
+    // its first slab loads, so the fold's double-precision metrics overlap them.
+    auto round_state = [&]() {
+        if (wave != 0) return;
         FLState S0 = *st;
         if (fold) {
-            S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0);
+            if (c.es_enabled || blockIdx.x == 0) S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0);
             if (lane == 0) {
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
                 if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
@@ -425,13 +428,17 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             }
         }
         if (lane == 0) S_sh = S0;
-    }
+    };
     if (blockIdx.x >= nparam_blocks) {
         // tail block: this rank's confusion slots are zeroed (the eval pass accumulates
         // into them); its loss slot gets the per-workgroup CE partials, summed in a fixed order
-        if (!last_local_step) return;
+        if (!last_local_step) {
+            round_state();
+            return;
+        }
         float lp = 0.f;
         for (int s = threadIdx.x; s < c.n_slabs; s += blockDim.x) lp += b.slab[(size_t)s * c.slab_stride + d.P];
+        round_state();
         part[wave][lane] = lp;
         lds_barrier();
         const FLState S = S_sh;
@@ -483,6 +490,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         return;
     }
     float g = 0.f;
+    bool have_state = false;
     {
         const float* sp = b.slab + (valid ? di : 0);
         for (int s0 = wave; s0 < c.n_slabs; s0 += ADAM_WAVES * ADAM_DEPTH) {
@@ -494,10 +502,15 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
                 const float v = __builtin_nontemporal_load(&sp[(size_t)(s < c.n_slabs ? s : 0) * c.slab_stride]);
                 x[u] = s < c.n_slabs ? v : 0.f;
             }
+            if (!have_state) {
+                have_state = true;
+                round_state();
+            }
 #pragma unroll
             for (int u = 0; u < ADAM_DEPTH; ++u) g += x[u];
         }
     }
+    if (!have_state) round_state();
     part[wave][lane] = g;
     lds_barrier();
     if (wave != 0 || !valid) return;
