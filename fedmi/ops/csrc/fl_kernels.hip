@@ -600,7 +600,7 @@ fl_eval_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ par
 // Local evaluation + FedAvg in one kernel (world > 1, one-shot xGMI all-reduce); see
 // fl_eval_fedavg_bf16_kernel.
 template <int RT>
-__global__ void __launch_bounds__(FL_THREADS)
+__global__ void __launch_bounds__(FL_THREADS, 8)  // 8 waves/SIMD = two workgroups per CU: one resident wave of blocks
 fl_eval_fedavg_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ params,
                       float* __restrict__ cm_out, const FLState* __restrict__ st, PeerArgs a, PeerPack pk, int n_ar) {
     extern __shared__ __attribute__((aligned(16))) float lds[];

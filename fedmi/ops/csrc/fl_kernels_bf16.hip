@@ -473,7 +473,7 @@ fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float*
 // publishes the tails.  The all-reduce's waiting and xGMI latency hide behind the
 // evaluation instead of following it.
 template <int RT>
-__global__ void __launch_bounds__(FL_THREADS)
+__global__ void __launch_bounds__(FL_THREADS, 8)  // 8 waves/SIMD = two workgroups per CU: one resident wave of blocks
 fl_eval_fedavg_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ params,
                            float* __restrict__ cm_out, const FLState* __restrict__ st, PeerArgs a, PeerPack pk,
                            int n_ar) {

@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(PEER_THREADS) peer_allreduce_kernel(PeerArgs a
         peer_publish(a.tflag_dst, a.world, target);
     }
     peer_wait(a, a.ctl->flags, target);
-    peer_reduce4(a, pk, 0, a.n >> 2, blockIdx.x, gridDim.x);
+    peer_reduce4<PEER_MAX_WORLD>(a, pk, 0, a.n >> 2, blockIdx.x, gridDim.x);
     if (blockIdx.x == 0) peer_reduce1(a, a.n & ~3ll, a.n);
     peer_finish(a, target, gridDim.x);
 }

@@ -18,6 +18,7 @@
 
 #define PEER_MAX_WORLD 8  // one node: every GPU has a direct xGMI link to each of its 7 peers
 
+
 // Optional epilogue of the reduction: also write the reduced fp32 parameter image as the
 // packed bf16 LDS image the bf16 train kernel stages (fl_kernels_bf16.hip, MLPDescB), so the
 // separate pack kernel after FedAvg disappears.  Offsets are in float4 units of the fp32
@@ -139,23 +140,35 @@ __device__ __forceinline__ void peer_wait(const PeerArgs& a, unsigned* flags, un
 
 // out[4*i0 .. 4*i1) = sum over ranks, rank order (bit-identical on every rank); block `bid`
 // of `nb` blocks takes a grid-stride share.  Optional bf16 pack of the weights.
+// BATCH = ranks whose float4 is in flight at once per thread: all 8 in the standalone kernel;
+// 2 in the fused evaluation kernel, which must stay within 64 VGPRs (two 1024-thread
+// workgroups per CU) -- there the extra round trips hide behind the evaluation.
+template <int BATCH>
 __device__ __forceinline__ void peer_reduce4(const PeerArgs& a, const PeerPack& pk, long long i0, long long i1,
                                              int bid, int nb) {
     const int bytes = (int)(a.n * 4);
     for (long long i = i0 + (long long)bid * blockDim.x + threadIdx.x; i < i1; i += (long long)nb * blockDim.x) {
-        float4 v[PEER_MAX_WORLD];
+        // the sum is the same left fold in rank order for any BATCH
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int j = 0; j < PEER_MAX_WORLD; ++j)
-            if (j < a.world) v[j] = peer_load16(a.src[j], bytes, (int)(i * 16));
-        float4 s = v[0];
+        for (int j0 = 0; j0 < PEER_MAX_WORLD; j0 += BATCH) {
+            float4 v[BATCH];
 #pragma unroll
-        for (int j = 1; j < PEER_MAX_WORLD; ++j)
-            if (j < a.world) {
-                s.x += v[j].x;
-                s.y += v[j].y;
-                s.z += v[j].z;
-                s.w += v[j].w;
-            }
+            for (int j = 0; j < BATCH; ++j)
+                if (j0 + j < a.world) v[j] = peer_load16(a.src[j0 + j], bytes, (int)(i * 16));
+#pragma unroll
+            for (int j = 0; j < BATCH; ++j)
+                if (j0 + j < a.world) {
+                    if (j0 + j == 0) {
+                        s = v[j];
+                    } else {
+                        s.x += v[j].x;
+                        s.y += v[j].y;
+                        s.z += v[j].z;
+                        s.w += v[j].w;
+                    }
+                }
+        }
         reinterpret_cast<float4*>(a.out)[i] = s;
         if (pk.pk != nullptr) peer_pack_store(pk, (int)i, s);
     }
@@ -220,7 +233,7 @@ __device__ __forceinline__ void peer_fused_reduce(const PeerArgs& a, const PeerP
                                                   int nb) {
     if (bid == 0) peer_publish(a.flag_dst, a.world, target);
     peer_wait(a, a.ctl->flags, target);
-    peer_reduce4(a, pk, 0, a.n_w >> 2, bid, nb);
+    peer_reduce4<2>(a, pk, 0, a.n_w >> 2, bid, nb);
     if (bid == 0) {
         peer_wait_eval(a, target);
         peer_publish(a.tflag_dst, a.world, target);
