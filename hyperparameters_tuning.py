@@ -29,9 +29,57 @@ import time
 import numpy as np
 
 from fedmi.data.sharding import split_data
-from fedmi.data.tabular import DEFAULT_DATASET, DEFAULT_LABEL, load_tabular
+from fedmi.data.tabular import DEFAULT_DATASET, DEFAULT_LABEL, encode_categorical_features  # noqa: F401
+from fedmi.data.tabular import load_tabular
+from fedmi.fl.metrics import confusion_matrix, metrics_from_confusion
+from fedmi.fl.sklearn_fed import average_estimator_weights
 from fedmi.hpo.sweep import HIDDEN_GRID, LR_GRID, run_sweep
 from fedmi.parallel.comm import get_world
+
+
+class FederatedMLPLearning:
+    """Reference [H] client API (hyperparameters_tuning.py:10-132) over fedmi components:
+    ``_split_data`` (contiguous shard, H:17-22), ``federated_averaging`` (uniform mean of
+    ``coefs_ + intercepts_``, H:24-46), ``_set_weights`` (H:48-54), ``_compute_metrics``
+    (H:56-66) and ``train_and_evaluate`` -- the 10 x 9 grid of H:68-132, whose 9 learning
+    rates per hidden config train as ONE packed job on the GPU (``fedmi.hpo.sweep``).
+    ``train_and_evaluate`` returns ``(best_params, best_metrics, best_weights)`` like the
+    reference's root rank prints them (H:126-132)."""
+
+    def __init__(self, X, y, rank, size, comm=None, backend="auto", packed=True):
+        self.rank = rank
+        self.size = size
+        self.comm = comm
+        self.X_local, self.y_local = self._split_data(X, y, rank, size)
+        self.local_model = None
+        self.backend, self.packed = backend, packed
+
+    def _split_data(self, X, y, rank, size):
+        return split_data(X, y, rank, size, mode="contiguous")
+
+    def federated_averaging(self, comm):
+        global_weights = average_estimator_weights(self.local_model, comm, weighting="uniform")
+        self._set_weights(global_weights)
+        return global_weights
+
+    def _set_weights(self, global_weights):
+        k = len(self.local_model.coefs_)
+        self.local_model.coefs_ = [np.array(w, dtype=np.float64) for w in global_weights[:k]]
+        self.local_model.intercepts_ = [np.array(w, dtype=np.float64) for w in global_weights[k:]]
+
+    def _compute_metrics(self, y_true, y_pred):
+        return metrics_from_confusion(confusion_matrix(y_true, y_pred, 2))
+
+    def train_and_evaluate(self, comm, rounds=1, hidden_grid=HIDDEN_GRID, lr_grid=LR_GRID, max_iter=400,
+                           on_trial=None):
+        best, results = None, []
+        for _ in range(rounds):
+            best, results = run_sweep(self.X_local, self.y_local, comm, hidden_grid, lr_grid, max_iter=max_iter,
+                                      backend=self.backend, packed=self.packed, on_trial=on_trial)
+        self.results = results
+        if best is None:
+            return None, None, None
+        return ({"hidden_layer_sizes": best.hidden, "learning_rate": best.lr}, best.global_, best.weights)
 
 
 def main(argv=None):

@@ -65,3 +65,21 @@ def test_hip_group_matches_standalone_engines(dtype):
         h = e.history()
         assert h["rounds_run"] == t.history["rounds_run"] and h["stop_round"] == t.history["stop_round"]
         np.testing.assert_array_equal(h["global"], t.history["global"])
+
+
+def test_reference_h_client_api_runs_grid_and_returns_best():
+    """[H] client class (hyperparameters_tuning.py): reference method names, packed grid."""
+    sys.path.insert(0, REPO)
+    import hyperparameters_tuning as H
+    X, y = make_income_like(400, seed=9)
+    c = H.FederatedMLPLearning(X, y, 0, 1, backend="numpy")
+    assert len(c.X_local) == 400
+    params, metrics, weights = c.train_and_evaluate(None, hidden_grid=[(6,), (8, 4)], lr_grid=[0.01, 0.05],
+                                                    max_iter=15)
+    assert len(c.results) == 4
+    best = max(c.results, key=lambda r: r.global_["accuracy"])
+    assert params == {"hidden_layer_sizes": best.hidden, "learning_rate": best.lr}
+    assert metrics == best.global_ and 0.0 <= metrics["accuracy"] <= 1.0
+    assert [w.shape for w in weights] == [w.shape for w in best.weights]
+    # single client: the uniform FedAvg is the identity and the confusion matrix is local
+    assert c._compute_metrics(y[:10], y[:10])["accuracy"] == 1.0
