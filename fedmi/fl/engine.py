@@ -62,6 +62,11 @@ class EngineConfig:
     # all-reduce in ONE kernel, the weights' all-reduce overlapping the evaluation
     # (fedmi/ops/csrc/peer_device.h); False = separate eval and all-reduce kernels
     eval_fedavg: bool = True
+    # world > 1, early stopping off, bf16: score round r's post-step local model inside round
+    # r+1's train kernel and publish the counts with round r+1's all-reduce -- no evaluation
+    # kernel in the round; the last round of every run() evaluates itself (fl_common.h
+    # FL_EVAL_LAGGED).  Metrics, history and weights are identical to classic rounds.
+    lagged_eval: bool = True
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -365,7 +370,7 @@ class HipRoundEngine(RoundEngineBase):
     tensors already on the device (e.g. from the synthetic generator)."""
 
     def __init__(self, X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None, device=None,
-                 comm_buffers=None):
+                 comm_buffers=None, emulate_clients: bool = False):
         """``comm_buffers``: optional pair of float32 device views of length
         :meth:`comm_len` to use as the double-buffered FedAvg buffers (trial packing shares one
         all-reduce between engines by handing each a slice of one allocation)."""
@@ -390,7 +395,11 @@ class HipRoundEngine(RoundEngineBase):
         slab_stride = ((self.P + 1) + 3) & ~3
         # device parameter buffers use the padded image layout (fl_common.h)
         self.Pimg = image_layout(self.dims)[2]
-        comm_len = self.Pimg + self.world * self.tail_stride
+        # lagged evaluation carries a second metric region after the tails (fl_common.h)
+        # (emulate_clients: one process measures the multi-client round shape, tools/round_emulate.py)
+        self._lag = ((self.world > 1 or emulate_clients) and not cfg.early_stop and cfg.dtype == "bf16"
+                     and comm_buffers is None and bool(cfg.lagged_eval))
+        comm_len = self.Pimg + self.world * self.tail_stride * (2 if self._lag else 1)
         if comm_buffers is None:
             self.params = [torch.zeros(comm_len, **f32), torch.zeros(comm_len, **f32)]
         else:
@@ -425,6 +434,8 @@ class HipRoundEngine(RoundEngineBase):
             # trial packing runs rounds through run_local + a shared all-reduce: classic rounds
             "fused_eval": bool(cfg.fused_eval) and comm_buffers is None,
             "eval_fedavg": bool(cfg.eval_fedavg),
+            "lagged_eval": self._lag,
+            "emulate_clients": bool(emulate_clients),
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),
@@ -550,17 +561,21 @@ class HipRoundEngine(RoundEngineBase):
                     self.comm.allreduce_(self.params[(r + 1) & 1])
             self.rounds_issued += n
             return
+        # lagged engines: graphs hold lagged rounds only, the last round of the call is eager and
+        # evaluates itself (then every metric is in the buffers for the host)
+        lag = bool(self.engine.lagged)
         r = r0
         while r < r0 + n:
             left = r0 + n - r
-            if g >= 2 and r % 2 == 0 and left >= g and not self.engine.needs_eager_round():
+            if (g >= 2 and r % 2 == 0 and (left > g if lag else left >= g)
+                    and not self.engine.needs_eager_round()):
                 if not self._graph_ready:
                     self.engine.capture(g, s, self._native_comm)
                     self._graph_ready = True
                 self.engine.replay(s)
                 r += g
             else:
-                self.engine.run(r, 1, s, self._native_comm)
+                self.engine.run(r, 1, s, self._native_comm, close=(r == r0 + n - 1))
                 r += 1
         self.rounds_issued = r
 

@@ -81,6 +81,7 @@ struct FLConfig {
     int tail_off;       // == Pimg: start of the per-rank metric tail in the comm buffer
     int tail_stride;    // C*C confusion counts + 1 loss slot
     int tail_len;       // world * tail_stride
+    int lag_off;        // > 0: start of the lag region A (tail_len floats, FL_EVAL_LAGGED)
     int local_steps;    // optimizer steps per round (reference: 1 full-batch step, C:63-73)
     // optimizer (torch.optim.Adam + StepLR, C:44-46); scalars kept in double like torch
     double lr0;
@@ -135,6 +136,8 @@ struct FLBuffers {
     // sqrt(bias_correction2)} rounded to fp32.  A table lookup instead of three double pow()
     // on the Adam kernel's critical path.
     const float* sched;
+    float* cnt;         // FL_EVAL_LAGGED: confusion counts of the previous round's local model
+    float* lbuf;        // FL_EVAL_LAGGED: the previous round's loss, published one round later
 };
 
 // Evaluation placement of a round (`mode` of the train kernels).
@@ -150,6 +153,17 @@ struct FLBuffers {
 #define FL_EVAL_CLASSIC 0
 #define FL_EVAL_FUSED 1
 #define FL_EVAL_FUSED_SKIP 2
+//   FL_EVAL_LAGGED  : several clients, early stopping off: the train kernel of round r also
+//                     scores round r-1's post-step LOCAL model (a second forward pass on the
+//                     staged local image) into the local count buffer; the Adam kernel
+//                     publishes those counts (+ round r-1's loss) in region A of round r's
+//                     all-reduce, so no round needs a separate evaluation.  The metrics of
+//                     round r-1 are folded at round r+1 -- one round later, which only
+//                     matters to a stop decision, hence early stopping off.
+#define FL_EVAL_LAGGED 3
+// Metric regions of an all-reduced comm buffer that a fold consumes (fl_device.h).
+#define FL_FOLD_A 1  // lag region: round next_round - 2
+#define FL_FOLD_B 2  // tail region: round next_round - 1
 // LDS confusion-counter region of the train kernels: C*C counters + a "score rows" flag,
 // padded to a multiple of 16 bytes.
 #define FL_CM_FLAG (FL_MAX_CLASSES * FL_MAX_CLASSES)
@@ -161,24 +175,27 @@ struct FLBuffers {
 hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                            const float* pg, const FLState* st_in, FLState* st_out,
                            int local_step, hipStream_t s, int mode = FL_EVAL_CLASSIC,
-                           float* cm_out = nullptr);
+                           float* cm_out = nullptr, int fold_mask = FL_FOLD_B);
 // `st` = state the step runs under; with `fold` (FL_EVAL_FUSED rounds, first local step) it
 // is the previous round's state: every block folds pg's tail into it, block 0 writes the
 // round's state to `st_out`.
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* pin, const float* anchor, float* comm,
                           const FLState* st, int local_step, hipStream_t s,
-                          const MLPDescB* e = nullptr, FLState* st_out = nullptr, int fold = 0);
+                          const MLPDescB* e = nullptr, FLState* st_out = nullptr, int fold = 0,
+                          int tail_a = 0, int fold_mask = FL_FOLD_B);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                               const float* pg, const FLState* st_in, FLState* st_out,
-                              hipStream_t s);
+                              hipStream_t s, int mask = FL_FOLD_B);
 // bf16-operand variants (fp32 accumulate, fp32 master weights / slab / Adam state).
+// `el` (FL_EVAL_LAGGED): layout whose parameter region is the second image (after e's), and
+// whose lds_bytes covers both.
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                 const float* pg, const FLState* st_in, FLState* st_out, int local_step,
                                 hipStream_t s, bool stage_local = false, int mode = FL_EVAL_CLASSIC,
-                                float* cm_out = nullptr);
+                                float* cm_out = nullptr, int fold_mask = FL_FOLD_B, const MLPDescB* el = nullptr);
 hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_set_lds_limit_bf16(size_t bytes);

@@ -72,16 +72,16 @@ __device__ void metrics_from_cm(CM cmv, int C, double out[4]) {
     out[0] = tp_sum / total; out[1] = prec; out[2] = rec; out[3] = f1;
 }
 
-// Fold the previous round's all-reduced tails into the state.  Executed by one full wave:
-// lane k computes client k's metrics, lane 0 combines them in rank order (the reference's
-// np.mean order) and applies the early-stop rule.  Returns the new state in lane 0.
-static __device__ FLState finalize_state(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
-                                  const float* pg, FLState S, bool write_hist) {
+// Fold round k's all-reduced tails (`tails` = per-rank slots of C*C counts + loss) into the
+// state, if k is the next round to finalize.  Executed by one full wave: lane j computes
+// client j's metrics, lane 0 combines them in rank order (the reference's np.mean order)
+// and applies the early-stop rule.  Returns the new state in lane 0.
+static __device__ FLState fold_round(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
+                                     const float* tails, int r, FLState S, bool write_hist) {
     const int lane = threadIdx.x & 63;
-    if (!S.stopped && S.next_round > S.finalized) {
-        const int r = S.next_round - 1;
+    if (S.stopped || r < 0 || r < S.finalized) return S;
+    {
         const int C = d.dim[d.L];
-        const float* tails = pg + c.tail_off;
         double mk[4] = {0, 0, 0, 0};
         double lk = 0;
         if (lane < c.world) {
@@ -120,15 +120,31 @@ static __device__ FLState finalize_state(const MLPDesc& d, const FLConfig& c, co
                     close = close && (fabs(mean[q] - S.prev[q]) <= c.atol + c.rtol * fabs(S.prev[q]));
             if (close) {
                 S.count -= 1;
-                if (S.count == 0) { S.stopped = 1; S.stop_round = S.next_round; }
+                if (S.count == 0) { S.stopped = 1; S.stop_round = r + 1; }
             } else {
                 for (int q = 0; q < 4; ++q) S.prev[q] = mean[q];
                 S.has_prev = 1;
                 S.count = c.patience;
             }
         }
-        S.finalized = S.next_round;
+        S.finalized = r + 1;
     }
+    return S;
+}
+
+// Regions of the all-reduced comm buffer `pg` that hold metrics (fl_common.h FL_FOLD_*):
+//   B (tail_off): the previous round's (next_round - 1) own evaluation;
+//   A (lag_off) : lagged rounds -- the round before it (next_round - 2), scored inside the
+//                 previous round's train kernel.  Folded first: rounds finalize in order.
+static __device__ FLState finalize_state(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
+                                         const float* pg, FLState S, bool write_hist, int mask = FL_FOLD_B) {
+    if ((mask & FL_FOLD_A) && c.lag_off > 0) {
+        S = fold_round(d, c, b, pg + c.lag_off, S.next_round - 2, S, write_hist);
+        // only lane 0 holds the folded state: every lane must take the same branch below
+        S.finalized = __shfl(S.finalized, 0, 64);
+        S.stopped = __shfl(S.stopped, 0, 64);
+    }
+    if (mask & FL_FOLD_B) S = fold_round(d, c, b, pg + c.tail_off, S.next_round - 1, S, write_hist);
     return S;
 }
 

@@ -210,6 +210,16 @@ class FLEngine {
         fused_ = cfg.contains("fused_eval") && cfg["fused_eval"].cast<bool>() && c_.world == 1 &&
                  c_.agg_scale == 1.0f;
         eval_fedavg_ = !cfg.contains("eval_fedavg") || cfg["eval_fedavg"].cast<bool>();
+        // Lagged evaluation (fl_common.h FL_EVAL_LAGGED): several clients, early stopping off,
+        // bf16 kernels, and room in LDS for the second parameter image.  The comm buffer then
+        // carries the lag region A after the tails (the caller sized it: comm_len).
+        const bool lag_req = cfg.contains("lagged_eval") && cfg["lagged_eval"].cast<bool>();
+        if (lag_req) c_.lag_off = d_.Pimg + c_.tail_len;
+        comm_len_ = d_.Pimg + c_.tail_len * (lag_req ? 2 : 1);
+        const bool emulate = cfg.contains("emulate_clients") && cfg["emulate_clients"].cast<bool>();
+        lagged_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !c_.es_enabled && !fused_ &&
+                  (size_t)el_.lds_bytes <= FL_LDS_DYNAMIC_MAX;
+        if (lagged_) HIP_CHECK(fl_set_lds_limit_bf16((size_t)el_.lds_bytes));
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
@@ -237,6 +247,12 @@ class FLEngine {
             HIP_CHECK(hipMalloc(&sched_, sch.size() * sizeof(float)));
             HIP_CHECK(hipMemcpy(sched_, sch.data(), sch.size() * sizeof(float), hipMemcpyHostToDevice));
             b_.sched = sched_;
+            // FL_EVAL_LAGGED: previous round's counts + loss (zero)
+            const size_t nlag = FL_MAX_CLASSES * FL_MAX_CLASSES + 4;
+            HIP_CHECK(hipMalloc(&lagbuf_, nlag * sizeof(float)));
+            HIP_CHECK(hipMemset(lagbuf_, 0, nlag * sizeof(float)));
+            b_.cnt = lagbuf_;
+            b_.lbuf = lagbuf_ + FL_MAX_CLASSES * FL_MAX_CLASSES;
         }
         if (dtype_ == 1) {
             // packed bf16 parameter regions; padding stays zero forever
@@ -251,13 +267,16 @@ class FLEngine {
         drop_graph();
         if (pk_) (void)hipFree(pk_);
         if (sched_) (void)hipFree(sched_);
+        if (lagbuf_) (void)hipFree(lagbuf_);
     }
 
     // Issue rounds [r0, r0 + n): per round the train/Adam pair (one per local step), the
     // evaluation (classic rounds) and, when world > 1, one all-reduce.
-    void run(int r0, int n, uintptr_t stream, RcclComm* comm) {
+    // Lagged engines (several clients, no early stop) issue every round lagged except, with
+    // `close`, the last, which evaluates itself: after it every metric is in the buffers.
+    void run(int r0, int n, uintptr_t stream, RcclComm* comm, bool close = true) {
         hipStream_t s = as_stream(stream);
-        for (int r = r0; r < r0 + n; ++r) issue_round(r, s, comm, true);
+        for (int r = r0; r < r0 + n; ++r) issue_round(r, s, comm, true, lagged_ && !(close && r == r0 + n - 1));
     }
 
     // Local part of round r (no all-reduce; the caller reduces a shared buffer).
@@ -271,6 +290,7 @@ class FLEngine {
         if (which == 0) {
             flush_pending_eval(r, s);
             issue_train(r, s, false);
+            prev_lagged_ = false;
         } else if (which == 1) {
             issue_eval(r, s);
             cm_in_tail_ = true;
@@ -286,7 +306,10 @@ class FLEngine {
     void finalize(int r, uintptr_t stream) {
         hipStream_t s = as_stream(stream);
         flush_pending_eval(r, s);
-        HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s));
+        if (prev_lagged_)
+            throw std::runtime_error("finalize: the last round is lagged (its metrics need one more round)");
+        const int mask = (prev_scored_ ? FL_FOLD_A : 0) | FL_FOLD_B;
+        HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s, mask));
         cm_in_tail_ = false;
     }
 
@@ -298,16 +321,18 @@ class FLEngine {
         if (needs_eager_round()) throw std::runtime_error("capture: issue one eager round first");
         drop_graph();
         hipStream_t s = as_stream(stream);
-        const bool pend = pending_cm_, tail = cm_in_tail_;
+        const bool pend = pending_cm_, tail = cm_in_tail_, plag = prev_lagged_, pscore = prev_scored_;
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
-            for (int r = 0; r < n; ++r) issue_round(r, s, comm, true);
+            for (int r = 0; r < n; ++r) issue_round(r, s, comm, true, lagged_);
         } catch (...) {
             hipGraph_t g;
             hipStreamEndCapture(s, &g);
             if (g) hipGraphDestroy(g);
             pending_cm_ = pend;
             cm_in_tail_ = tail;
+            prev_lagged_ = plag;
+            prev_scored_ = pscore;
             throw;
         }
         HIP_CHECK(hipStreamEndCapture(s, &graph_));
@@ -315,6 +340,8 @@ class FLEngine {
         graph_rounds_ = n;
         pending_cm_ = pend;  // nothing ran yet: replay() applies the rounds' effect
         cm_in_tail_ = tail;
+        prev_lagged_ = plag;
+        prev_scored_ = pscore;
     }
 
     void replay(uintptr_t stream) {
@@ -323,6 +350,8 @@ class FLEngine {
         HIP_CHECK(hipGraphLaunch(exec_, as_stream(stream)));
         pending_cm_ = fused_;
         cm_in_tail_ = !fused_;
+        prev_lagged_ = lagged_;
+        prev_scored_ = lagged_;
     }
 
     int graph_rounds() const { return graph_rounds_; }
@@ -330,7 +359,12 @@ class FLEngine {
     // The captured rounds assume the steady state of their kind: a fused graph must not
     // start behind a classic round (whose counts already sit in the tail), a classic graph
     // not behind a fused one (whose counts were never computed).
-    bool needs_eager_round() const { return fused_ ? cm_in_tail_ : pending_cm_; }
+    // A lagged graph must start behind a lagged round (its rounds score their predecessor).
+    bool needs_eager_round() const {
+        if (lagged_) return !prev_lagged_;
+        return fused_ ? cm_in_tail_ : pending_cm_;
+    }
+    bool lagged() const { return lagged_; }
     bool fused() const { return fused_; }
 
     // The host wrote the global weights (set_weights / resume): the next round repacks them.
@@ -340,6 +374,8 @@ class FLEngine {
     void reset_pending() {
         pending_cm_ = false;
         cm_in_tail_ = false;
+        prev_lagged_ = false;
+        prev_scored_ = false;
     }
 
     // Aggregate with the one-shot xGMI all-reduce (peer_allreduce.hip) instead of RCCL: every
@@ -350,7 +386,7 @@ class FLEngine {
         // one GPU for measurements, tools/round_emulate.py)
         if (fused_ || p.world() != c_.world || p.rank() != c_.rank || !p.is_open())
             throw std::runtime_error("attach_peer: communicator does not match this engine");
-        if (p.n_floats() != (long long)(d_.Pimg + c_.tail_len))
+        if (p.n_floats() != comm_len_)
             throw std::runtime_error("attach_peer: buffer length != parameter image + tails");
         drop_graph();
         peer_ = &p;
@@ -385,6 +421,7 @@ class FLEngine {
         FLState* so = st_[(r + 1) & 1];
         if (which == 0) launch_train(pg, so, so, 1, s);
         else if (which == 1) launch_adam(b_.local, pg, cb, so, 1, s);
+        else if (which == 3 && dtype_ == 1) launch_train(pg, so, so, 0, s, FL_EVAL_LAGGED, b_.cnt, 0);  // advances so
         else launch_eval(b_.local, cb, so, s);
     }
 
@@ -450,7 +487,8 @@ class FLEngine {
         o["tail_off"] = c_.tail_off;
         o["tail_stride"] = c_.tail_stride;
         o["tail_len"] = c_.tail_len;
-        o["comm_len"] = d_.Pimg + c_.tail_len;
+        o["comm_len"] = comm_len_;
+        o["lagged_eval"] = lagged_;
         o["state_bytes"] = (int)sizeof(FLState);
         return o;
     }
@@ -493,11 +531,20 @@ class FLEngine {
             ev_.bias_off[l] = e_.bias_off[l] - e_.param_off + ev_.param_off;
         }
         ev_.lds_bytes = ev_.param_off + e_.param_bytes;
+        // FL_EVAL_LAGGED: the train layout plus a second parameter region (the previous
+        // round's local model) after it; el_ addresses that region
+        el_ = e_;
+        el_.param_off = e_.lds_bytes;
+        for (int l = 0; l < L; ++l) {
+            el_.w_off[l] = e_.w_off[l] - e_.param_off + el_.param_off;
+            el_.bias_off[l] = e_.bias_off[l] - e_.param_off + el_.param_off;
+        }
+        el_.lds_bytes = el_.param_off + e_.param_bytes;
     }
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
-                      int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr) {
+                      int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr, int fold_mask = FL_FOLD_B) {
         if (dtype_ == 0) {
-            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s, mode, cm_out));
+            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s, mode, cm_out, fold_mask));
         } else {
             // the round's input weights -> packed bf16 image.  With one client the FedAvg
             // output IS the local model (agg_scale = 1), which the Adam kernel already packed,
@@ -508,13 +555,15 @@ class FLEngine {
             const bool packed = solo || (peer_ != nullptr && !need_pack_);
             if (ls == 0 && !packed) HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
             need_pack_ = false;
-            HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo, mode, cm_out));
+            HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo, mode, cm_out, fold_mask,
+                                           mode == FL_EVAL_LAGGED ? &el_ : nullptr));
         }
     }
     void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
-                     hipStream_t s, FLState* st_out = nullptr, int fold = 0) {
+                     hipStream_t s, FLState* st_out = nullptr, int fold = 0, int tail_a = 0,
+                     int fold_mask = FL_FOLD_B) {
         HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr, st_out,
-                                 fold));
+                                 fold, tail_a, fold_mask));
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
@@ -523,22 +572,32 @@ class FLEngine {
     // Train/Adam pairs of round r.  Fused rounds (fl_common.h FL_EVAL_FUSED): the first train
     // kernel also scores the previous round's model from its own forward pass, and the first
     // Adam kernel folds those counts and makes the round's live / stop decision.
+    // Lagged rounds (FL_EVAL_LAGGED): the train kernel scores the previous round's local model
+    // iff that round had no evaluation of its own; its fold consumes region A when the previous
+    // round scored ITS predecessor and region B when the previous round was evaluated.
     void issue_train(int r, hipStream_t s, bool fused) {
         float* pg = pbuf_[r & 1];
         float* cb = comm_buf(r);
         FLState* si = st_[r & 1];
         FLState* so = st_[(r + 1) & 1];
         if (fused && need_pack_) flush_pending_eval(r, s);  // host replaced the weights: score the old model
-        const int mode = !fused ? FL_EVAL_CLASSIC : (cm_in_tail_ ? FL_EVAL_FUSED_SKIP : FL_EVAL_FUSED);
-        float* cm_out = pg + c_.tail_off + c_.rank * c_.tail_stride;
+        // Every round's metric fold runs in its first Adam kernel (overlapped with the slab
+        // loads; measured: folding at the start of the train kernel cost ~3 us per round), the
+        // train kernel trains on the tentative live decision.
+        const bool score = !fused && prev_lagged_;
+        int mode = (fused && !cm_in_tail_) ? FL_EVAL_FUSED : FL_EVAL_FUSED_SKIP;
+        if (score) mode = FL_EVAL_LAGGED;
+        const int mask = fused ? FL_FOLD_B : ((prev_scored_ ? FL_FOLD_A : 0) | (prev_lagged_ ? 0 : FL_FOLD_B));
+        float* cm_out = score ? b_.cnt : pg + c_.tail_off + c_.rank * c_.tail_stride;
         for (int ls = 0; ls < c_.local_steps; ++ls) {
             const bool first = ls == 0;
-            launch_train(pg, first ? si : so, so, ls, s, first ? mode : FL_EVAL_CLASSIC, cm_out);
-            if (fused && first) launch_adam(pg, pg, cb, si, ls, s, so, 1);
-            else launch_adam(first ? pg : b_.local, pg, cb, so, ls, s);
+            launch_train(pg, first ? si : so, so, ls, s, first ? mode : FL_EVAL_CLASSIC, cm_out, mask);
+            if (first) launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask);
+            else launch_adam(b_.local, pg, cb, so, ls, s);
         }
         pending_cm_ = fused;
         cm_in_tail_ = false;
+        prev_scored_ = score;
     }
     void issue_eval(int r, hipStream_t s) {
         launch_eval(b_.local, comm_buf(r), st_[(r + 1) & 1], s);
@@ -559,12 +618,19 @@ class FLEngine {
         if (peer_ != nullptr)
             HIP_CHECK(peer_->launch((r + 1) & 1, pbuf_[(r + 1) & 1], dtype_ == 1 ? &pp_ : nullptr, s));
         else if (comm != nullptr)
-            comm->allreduce_f32((uintptr_t)pbuf_[(r + 1) & 1], (size_t)(d_.Pimg + c_.tail_len), (uintptr_t)s);
+            comm->allreduce_f32((uintptr_t)pbuf_[(r + 1) & 1], (size_t)comm_len_, (uintptr_t)s);
     }
-    void issue_round(int r, hipStream_t s, RcclComm* comm, bool allow_fused) {
+    // `lag`: a lagged round -- no evaluation; the next round's train kernel scores it.
+    void issue_round(int r, hipStream_t s, RcclComm* comm, bool allow_fused, bool lag = false) {
         const bool fused = fused_ && allow_fused;
+        lag = lag && lagged_ && !fused;
         if (!fused) flush_pending_eval(r, s);
         issue_train(r, s, fused);
+        prev_lagged_ = lag;
+        if (lag) {
+            issue_allreduce(r, s, comm);
+            return;
+        }
         if (!fused && peer_ != nullptr && eval_fedavg_fits()) {
             // evaluation and the one-shot all-reduce in one kernel (peer_device.h)
             issue_eval_fedavg(r, s);
@@ -606,9 +672,15 @@ class FLEngine {
     MLPDesc d_;
     MLPDescB e_;
     MLPDescB ev_;  // evaluation-only layout of e_ (no delta buffers)
+    MLPDescB el_;  // e_ plus a second parameter region (FL_EVAL_LAGGED scoring)
     int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
     char* pk_ = nullptr;
     float* sched_ = nullptr;  // Adam/StepLR scalars per optimizer step
+    float* lagbuf_ = nullptr;  // FL_EVAL_LAGGED count + loss carry-over
+    long long comm_len_ = 0;   // floats of a comm buffer: image + tails (+ lag region)
+    bool lagged_ = false;      // several clients: evaluation scored one round later (no eval kernel)
+    bool prev_lagged_ = false; // the last issued round had no evaluation of its own
+    bool prev_scored_ = false; // the last issued round's train kernel scored its predecessor
     bool need_pack_ = true;  // host changed the global weights: repack before the next round
     PeerAllReduce* peer_ = nullptr;  // one-shot xGMI all-reduce (nullptr: RCCL)
     PeerPack pp_;                    // its bf16 pack epilogue (bf16 mode)
@@ -660,7 +732,8 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def_property_readonly("size", &RcclComm::size);
     py::class_<FLEngine>(m, "FLEngine")
         .def(py::init<std::vector<int>, py::dict, py::dict>())
-        .def("run", &FLEngine::run, py::arg("r0"), py::arg("n"), py::arg("stream"), py::arg("comm") = nullptr)
+        .def("run", &FLEngine::run, py::arg("r0"), py::arg("n"), py::arg("stream"), py::arg("comm") = nullptr,
+             py::arg("close") = true)
         .def("run_local", &FLEngine::run_local)
         .def("phase", &FLEngine::phase, py::arg("r"), py::arg("which"), py::arg("stream"), py::arg("comm") = nullptr)
         .def("finalize", &FLEngine::finalize)
@@ -675,6 +748,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def_property_readonly("has_peer", &FLEngine::has_peer)
         .def("needs_eager_round", &FLEngine::needs_eager_round)
         .def_property_readonly("fused", &FLEngine::fused)
+        .def_property_readonly("lagged", &FLEngine::lagged)
         .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);

@@ -288,7 +288,7 @@ template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                 const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step, int mode,
-                float* __restrict__ cm_out) {
+                float* __restrict__ cm_out, int fold_mask) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
@@ -299,7 +299,7 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
         FLState S0 = *st_in;
         if (local_step == 0) {
             if (mode == FL_EVAL_CLASSIC) {
-                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
+                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0, fold_mask);
                 if (threadIdx.x == 0) {
                     S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
                     if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
                const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
-               FLState* __restrict__ st_out, int fold) {
+               FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask) {
     __shared__ float part[ADAM_WAVES][64];
     __shared__ FLState S_sh;
     const int last_local_step = (local_step == c.local_steps - 1);
@@ -420,7 +420,8 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         if (wave != 0) return;
         FLState S0 = *st;
         if (fold) {
-            if (c.es_enabled || blockIdx.x == 0) S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0);
+            if (c.es_enabled || blockIdx.x == 0)
+                S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0, fold_mask);
             if (lane == 0) {
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
                 if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
@@ -459,6 +460,26 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             }
             const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
             comm[i] = (k == c.rank && e == c.tail_stride - 1) ? loss : 0.f;
+        }
+        if (c.lag_off > 0) {
+            // lag region A (FL_EVAL_LAGGED): the previous round's counts (scored by this round's
+            // train kernel) and loss, when `tail_a`; then this round's loss is kept for the next
+            // round and the count buffer cleared for the next train kernel
+            const int CC = c.tail_stride - 1;
+            for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
+                const int i = c.lag_off + jj;
+                if (!S.live) {
+                    comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
+                    continue;
+                }
+                const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
+                comm[i] = (tail_a && k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
+            }
+            __syncthreads();  // every read of cnt / lbuf is done
+            if (S.live) {
+                for (int e = threadIdx.x; e < CC; e += blockDim.x) b.cnt[e] = 0.f;
+                if (threadIdx.x == 0) b.lbuf[0] = loss;
+            }
         }
         return;
     }
@@ -615,9 +636,9 @@ fl_eval_fedavg_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restric
 }
 
 __global__ void fl_finalize_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
-                                   const FLState* __restrict__ st_in, FLState* __restrict__ st_out) {
+                                   const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int mask) {
     if (blockIdx.x != 0) return;
-    FLState S = finalize_state(d, c, b, pg, *st_in, true);
+    FLState S = finalize_state(d, c, b, pg, *st_in, true, mask);
     if (threadIdx.x != 0) return;
     S.live = 0;
     *st_out = S;
@@ -690,31 +711,33 @@ static inline size_t lds_bytes(const MLPDesc& d) { return (size_t)d.lds_floats *
 template <int RT>
 static hipError_t launch_train_rt(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                                   const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
-                                  int mode, float* cm_out) {
+                                  int mode, float* cm_out, int fold_mask) {
     hipLaunchKernelGGL(fl_train_kernel<RT>, dim3(c.n_slabs), dim3(FL_THREADS), lds_bytes(d), s, d, c, b, pg, si,
-                       so, ls, mode, cm_out);
+                       so, ls, mode, cm_out, fold_mask);
     return hipGetLastError();
 }
 
 hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pg,
-                           const FLState* si, FLState* so, int ls, hipStream_t s, int mode, float* cm_out) {
+                           const FLState* si, FLState* so, int ls, hipStream_t s, int mode, float* cm_out,
+                           int fold_mask) {
     if (mode == FL_EVAL_FUSED && cm_out == nullptr) return hipErrorInvalidValue;
+    if (mode == FL_EVAL_LAGGED) return hipErrorInvalidValue;  // bf16 kernels only
     switch (c.R) {
-        case 16: return launch_train_rt<1>(d, c, b, pg, si, so, ls, s, mode, cm_out);
-        case 32: return launch_train_rt<2>(d, c, b, pg, si, so, ls, s, mode, cm_out);
+        case 16: return launch_train_rt<1>(d, c, b, pg, si, so, ls, s, mode, cm_out, fold_mask);
+        case 32: return launch_train_rt<2>(d, c, b, pg, si, so, ls, s, mode, cm_out, fold_mask);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
                           const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s,
-                          const MLPDescB* e, FLState* st_out, int fold) {
+                          const MLPDescB* e, FLState* st_out, int fold, int tail_a, int fold_mask) {
     if (fold && st_out == nullptr) return hipErrorInvalidValue;
     const int blocks = (d.P + 63) / 64 + 1;
     MLPDescB ee = {};
     if (e != nullptr) ee = *e;
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
-                       local_step, ee, e != nullptr ? 1 : 0, st_out, fold);
+                       local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask);
     return hipGetLastError();
 }
 
@@ -758,8 +781,8 @@ hipError_t fl_launch_eval_fedavg(const MLPDesc& d, const FLConfig& c, const FLBu
 }
 
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pg,
-                              const FLState* si, FLState* so, hipStream_t s) {
-    hipLaunchKernelGGL(fl_finalize_kernel, dim3(1), dim3(64), 0, s, d, c, b, pg, si, so);
+                              const FLState* si, FLState* so, hipStream_t s, int mask) {
+    hipLaunchKernelGGL(fl_finalize_kernel, dim3(1), dim3(64), 0, s, d, c, b, pg, si, so, mask);
     return hipGetLastError();
 }
 

@@ -98,10 +98,13 @@ __global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restri
 // Loads beyond STAGE_UNROLL per thread (large models) fall back to a loop.
 #define STAGE_P_UNROLL 4
 #define STAGE_X_UNROLL 2
+// `packed2` (optional): a second packed image staged at `param2_off` in the same load batch
+// (FL_EVAL_LAGGED: the previous round's local model beside this round's input weights).
 template <int RT>
 __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const char* __restrict__ packed,
                                                        const float* __restrict__ X, int n_rows, int F, int row0,
-                                                       char* lds) {
+                                                       char* lds, const char* __restrict__ packed2 = nullptr,
+                                                       int param2_off = 0) {
     const uint4* src = reinterpret_cast<const uint4*>(packed);
     uint4* dst = reinterpret_cast<uint4*>(lds + e.param_off);
     const int n16 = e.param_bytes >> 4;
@@ -109,12 +112,21 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
     const int nx = RT * 16 * kp;
     uint4 pv[STAGE_P_UNROLL];
     float xv[STAGE_X_UNROLL];
+    uint4 pv2[STAGE_P_UNROLL];
+    const uint4* src2 = reinterpret_cast<const uint4*>(packed2 != nullptr ? packed2 : packed);
     // unpredicated loads (clamped indices): a conditionally written register array is
     // demoted to scratch by the compiler
 #pragma unroll
     for (int u = 0; u < STAGE_P_UNROLL; ++u) {
         const int i = threadIdx.x + u * FL_THREADS;
         pv[u] = src[i < n16 ? i : 0];
+    }
+    if (packed2 != nullptr) {
+#pragma unroll
+        for (int u = 0; u < STAGE_P_UNROLL; ++u) {
+            const int i = threadIdx.x + u * FL_THREADS;
+            pv2[u] = src2[i < n16 ? i : 0];
+        }
     }
 #pragma unroll
     for (int u = 0; u < STAGE_X_UNROLL; ++u) {
@@ -136,6 +148,17 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
     for (int u = 0; u < STAGE_P_UNROLL; ++u) {
         const int i = threadIdx.x + u * FL_THREADS;
         if (i < n16) dst[i] = pv[u];
+    }
+    if (packed2 != nullptr) {
+        uint4* dst2 = reinterpret_cast<uint4*>(lds + param2_off);
+#pragma unroll
+        for (int u = 0; u < STAGE_P_UNROLL; ++u) asm volatile("" ::"v"(pv2[u].x), "v"(pv2[u].y), "v"(pv2[u].z), "v"(pv2[u].w));
+        for (int i = threadIdx.x + STAGE_P_UNROLL * FL_THREADS; i < n16; i += FL_THREADS) dst2[i] = src2[i];
+#pragma unroll
+        for (int u = 0; u < STAGE_P_UNROLL; ++u) {
+            const int i = threadIdx.x + u * FL_THREADS;
+            if (i < n16) dst2[i] = pv2[u];
+        }
     }
     uint16_t* a = reinterpret_cast<uint16_t*>(lds + e.act_off[0]);
 #pragma unroll
@@ -310,7 +333,7 @@ template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                      const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
-                     int stage_local, int mode, float* __restrict__ cm_out) {
+                     int stage_local, int mode, float* __restrict__ cm_out, int fold_mask, MLPDescB el) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
@@ -320,15 +343,16 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
         FLState S0 = *st_in;
         if (local_step == 0) {
             if (mode == FL_EVAL_CLASSIC) {
-                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0);
+                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0, fold_mask);
                 if (threadIdx.x == 0) {
                     S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
                     if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
                     if (blockIdx.x == 0) *st_out = S0;
                 }
             } else if (threadIdx.x == 0) {
-                // fused: the Adam kernel folds the previous round and decides; train on the
-                // tentative decision (a stop only turns this round into a no-op later)
+                // FUSED / FUSED_SKIP / LAGGED: the Adam kernel folds the previous round and
+                // decides; train on the tentative decision (a stop only turns this round into a
+                // no-op later)
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
             }
         }
@@ -344,8 +368,11 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     const int row0 = blockIdx.x * R;
     const int L = d.L;
     const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
+    // FL_EVAL_LAGGED (first local step): the previous round's local model, still intact in
+    // pk_local (this round's Adam has not run), is staged beside the input weights
+    const bool lagged = mode == FL_EVAL_LAGGED && local_step == 0;
     stage_params_rows_bf16<RT>(e, (local_step == 0 && !stage_local) ? b.pk_global : b.pk_local, b.X, c.n_rows,
-                               d.dim[0], row0, lds);
+                               d.dim[0], row0, lds, lagged ? b.pk_local : nullptr, el.param_off);
     FL_STAMP(8);
     {   // padding columns [C, kp[L]) of D_L never change: zero them here, off the CE's path
         const int padc = e.kp[L] - C;
@@ -360,6 +387,23 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     FL_STAMP(1);
     if (!S_sh.live) return;
     float* slab = b.slab + (size_t)blockIdx.x * c.slab_stride;
+    if (lagged) {
+        // score the previous round's local model on these rows (C:148 evaluation, published
+        // one round later): forward on the second image, argmax, counts -> b.cnt
+        forward_block_bf16<RT>(d, el, lds, nullptr);
+        const float* zl = reinterpret_cast<const float*>(lds + e.logit_off);
+        if (threadIdx.x < R && row0 + (int)threadIdx.x < c.n_rows) {
+            const float* zr = zl + threadIdx.x * 16;
+            int best = 0;
+            float bv = zr[0];
+            for (int k = 1; k < C; ++k)
+                if (zr[k] > bv) { bv = zr[k]; best = k; }
+            atomicAdd(&cm_s[ylab * C + best], 1);
+        }
+        lds_barrier();
+        for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
+            if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
+    }
     forward_block_bf16<RT>(d, e, lds, b.dbg);
     FL_STAMP(2);
 
@@ -493,16 +537,20 @@ fl_eval_fedavg_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const
 // ---------------------------------------------------------------------------------------
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                 const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
-                                bool stage_local, int mode, float* cm_out) {
-    if (mode == FL_EVAL_FUSED && cm_out == nullptr) return hipErrorInvalidValue;
+                                bool stage_local, int mode, float* cm_out, int fold_mask, const MLPDescB* el) {
+    if ((mode == FL_EVAL_FUSED || mode == FL_EVAL_LAGGED) && cm_out == nullptr) return hipErrorInvalidValue;
+    if (mode == FL_EVAL_LAGGED && el == nullptr) return hipErrorInvalidValue;
+    const MLPDescB eloc = el != nullptr ? *el : e;
+    // the lagged layout extends the LDS by the second parameter image
+    const size_t lds = el != nullptr ? (size_t)el->lds_bytes : (size_t)e.lds_bytes;
     switch (c.R) {
         case 16:
-            hipLaunchKernelGGL(fl_train_bf16_kernel<1>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
-                               pg, si, so, ls, stage_local ? 1 : 0, mode, cm_out);
+            hipLaunchKernelGGL(fl_train_bf16_kernel<1>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
+                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask, eloc);
             break;
         case 32:
-            hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
-                               pg, si, so, ls, stage_local ? 1 : 0, mode, cm_out);
+            hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
+                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask, eloc);
             break;
         default: return hipErrorInvalidValue;
     }

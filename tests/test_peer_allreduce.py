@@ -30,12 +30,14 @@ def _free_port():
     return p
 
 
-def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = True):
+def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = True, lagged: bool = True):
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
     comm.peer_allreduce = peer
-    cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4, eval_fedavg=eval_fedavg)
+    cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4, eval_fedavg=eval_fedavg,
+                       lagged_eval=lagged)
     e = HipRoundEngine(X, y, 2, cfg, comm, flat)
     assert e.aggregation == ("xgmi-oneshot" if peer else "host"), e.aggregation
+    assert bool(e.engine.lagged) == (lagged and dtype == "bf16"), (e.engine.lagged, lagged, dtype)
     e.run(3)                       # eager rounds
     cms = []
     for _ in range(2):             # reference step-by-step API
@@ -79,10 +81,13 @@ def _worker(rank, port, q):
         X, y = make_income_like(2400, seed=20 + rank)
         flat = init_flat([14, 50, 200, 2], 3)
         for dtype in ("fp32", "bf16"):
-            a = _run_engine(comm, True, dtype, X, y, flat)            # fused eval + all-reduce kernel
-            b = _run_engine(comm, False, dtype, X, y, flat)           # host (gloo) aggregation
-            c = _run_engine(comm, True, dtype, X, y, flat, False)     # separate eval / peer kernels
-            res[dtype] = (a, b, c)
+            # bf16 default: lagged evaluation (scored in the next train kernel); fp32: fused
+            # evaluation + all-reduce kernel
+            a = _run_engine(comm, True, dtype, X, y, flat)
+            b = _run_engine(comm, False, dtype, X, y, flat, lagged=False)     # host (gloo) aggregation
+            c = _run_engine(comm, True, dtype, X, y, flat, False, False)      # separate eval / peer kernels
+            d = _run_engine(comm, True, dtype, X, y, flat, True, False)       # fused eval + all-reduce kernel
+            res[dtype] = (a, b, c, d)
         # early stop: rounds past the stop (non-live) must reproduce the stop round's model
         res["es"] = (_run_early_stop(comm, True, X, y, flat), _run_early_stop(comm, False, X, y, flat))
         torch.cuda.synchronize()
@@ -109,9 +114,11 @@ def test_peer_allreduce_two_ranks_one_gpu():
         for n in (4099, 50003):
             assert res[f"open{n}"] and res[f"self{n}"], (rank, n, res)
         for dtype in ("fp32", "bf16"):
-            (wa, ha, ca), (wb, hb, cb), (wc, hc, cc) = res[dtype]
-            np.testing.assert_array_equal(wc, wb, err_msg=f"{dtype} weights (separate kernels)")
-            np.testing.assert_array_equal(hc["global"], hb["global"])
+            (wa, ha, ca), (wb, hb, cb), (wc, hc, cc), (wd, hd, cd) = res[dtype]
+            for name, (w, h) in (("separate kernels", (wc, hc)), ("eval+fedavg kernel", (wd, hd))):
+                np.testing.assert_array_equal(w, wb, err_msg=f"{dtype} weights ({name})")
+                np.testing.assert_array_equal(h["global"], hb["global"], err_msg=f"{dtype} metrics ({name})")
+                np.testing.assert_array_equal(h["loss"], hb["loss"], err_msg=f"{dtype} loss ({name})")
             np.testing.assert_array_equal(wa, wb, err_msg=f"{dtype} weights")
             np.testing.assert_array_equal(ha["global"], hb["global"])
             np.testing.assert_array_equal(ha["per_rank"], hb["per_rank"])

@@ -5,7 +5,9 @@ latency of the pulls.  Prints us/round for
 
   * world 1, fused evaluation (what bench.py runs at N = 1);
   * classic evaluation + separate one-shot all-reduce kernel;
-  * the fused evaluation + FedAvg kernel (what N > 1 runs).
+  * the fused evaluation + FedAvg kernel (N > 1 with early stopping);
+  * lagged evaluation: round r scored inside round r+1's train kernel, no evaluation kernel
+    (N > 1 without early stopping: bench.py).
 
     python tools/round_emulate.py [--rounds 2000] [--dtype bf16]
 """
@@ -34,12 +36,15 @@ def main():
     torch.cuda.set_device(dev)
     X, y = bench.synth_shard(a.rows, 0, dev)
     flat = init_flat([14, 50, 200, 2], 0)
-    cases = (("world 1, fused evaluation", True, None), ("eval + one-shot all-reduce", False, False),
-             ("fused eval + FedAvg kernel", False, True))
-    for name, fused, ef in cases:
+    cases = (("world 1, fused evaluation", True, None, False), ("eval + one-shot all-reduce", False, False, False),
+             ("fused eval + FedAvg kernel", False, True, False),
+             ("lagged eval (no eval kernel)", False, True, True))
+    for name, fused, ef, lag in cases:
+        if lag and a.dtype != "bf16":
+            continue
         cfg = EngineConfig(max_rounds=a.rounds + 256, early_stop=False, dtype=a.dtype, graph_rounds=16,
-                           fused_eval=fused, eval_fedavg=bool(ef))
-        e = HipRoundEngine(X, y, 2, cfg, None, flat)
+                           fused_eval=fused, eval_fedavg=bool(ef), lagged_eval=lag)
+        e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=lag)
         h = None
         if ef is not None:
             h = m.PeerAllReduce(1, 0, 0, int(e.params[0].numel()), 10.0)

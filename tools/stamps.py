@@ -20,7 +20,8 @@ e.run(3)
 nb = (rows + R - 1) // R
 dbg = torch.zeros(nb * 16, dtype=torch.int64, device=e.device)
 order = [0, 8, 9, 1, 10, 11, 12, 2, 3, 4, 5, 6, 7, 15]
-for which, name in ((0, "train"), (2, "eval")):
+kinds = [(0, "train"), (2, "eval")] + ([(3, "train, lagged scoring")] if dtype == "bf16" else [])
+for which, name in kinds:
     for rep in range(5):
         dbg.zero_()
         e.engine.set_debug(dbg.data_ptr())
