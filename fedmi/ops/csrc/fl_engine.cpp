@@ -540,6 +540,11 @@ class FLEngine {
             el_.bias_off[l] = e_.bias_off[l] - e_.param_off + el_.param_off;
         }
         el_.lds_bytes = el_.param_off + e_.param_bytes;
+        // ... and the scoring pass's activations: the delta buffers (unused during the
+        // forward pass, same shapes), its logits in a region after the second image
+        for (int l = 1; l < L; ++l) el_.act_off[l] = e_.dlt_off[l];
+        el_.logit_off = el_.lds_bytes;
+        el_.lds_bytes += R * 16 * 4;
     }
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
                       int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr, int fold_mask = FL_FOLD_B) {

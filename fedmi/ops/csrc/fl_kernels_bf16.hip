@@ -186,8 +186,10 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
 // z = act_l . W_l^T + b_l; hidden layers: ReLU -> bf16 act_{l+1} (all kp[l+1] columns, the
 // padding comes out 0); last layer: fp32 logits [R][16].
 template <int RT>
-__device__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// `wave_off` rotates the tile -> wave assignment, so two passes in one phase (lagged
+// scoring) put their tiles on different waves.
+__device__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds, int wave_off = 0) {
+    const int wave = ((threadIdx.x >> 6) + wave_off) % FL_WAVES, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     const bool last = (l + 1 == d.L);
     const int ntiles = last ? ((d.dim[d.L] + 15) >> 4) : (e.kp[l + 1] >> 4);
@@ -317,6 +319,23 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
     }
 }
 
+// Two forward passes in lock step, one phase (barrier) per layer: the training pass on e and
+// the lagged scoring pass on es (previous round's local image; its activations live in the
+// delta buffers, unused until the backward pass, and its logits in a second region).  The
+// phases are latency-bound, so the second pass's tiles on otherwise idle waves cost little.
+template <int RT>
+__device__ void forward2_block_bf16(const MLPDesc& d, const MLPDescB& e, const MLPDescB& es, char* lds,
+                                    unsigned long long* dbg) {
+    for (int l = 0; l < d.L; ++l) {
+        if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
+        const bool last = (l + 1 == d.L);
+        const int ntiles = last ? ((d.dim[d.L] + 15) >> 4) : (e.kp[l + 1] >> 4);
+        fwd_layer_bf16<RT>(d, e, l, lds);
+        fwd_layer_bf16<RT>(d, es, l, lds, FL_WAVES - ntiles % FL_WAVES);
+        lds_barrier();
+    }
+}
+
 template <int RT>
 __device__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg) {
     for (int l = 0; l < d.L; ++l) {
@@ -387,25 +406,23 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     FL_STAMP(1);
     if (!S_sh.live) return;
     float* slab = b.slab + (size_t)blockIdx.x * c.slab_stride;
-    if (lagged) {
-        // score the previous round's local model on these rows (C:148 evaluation, published
-        // one round later): forward on the second image, argmax, counts -> b.cnt
-        forward_block_bf16<RT>(d, el, lds, nullptr);
-        const float* zl = reinterpret_cast<const float*>(lds + e.logit_off);
-        if (threadIdx.x < R && row0 + (int)threadIdx.x < c.n_rows) {
-            const float* zr = zl + threadIdx.x * 16;
+    if (lagged) forward2_block_bf16<RT>(d, e, el, lds, b.dbg);  // + score the previous local model
+    else forward_block_bf16<RT>(d, e, lds, b.dbg);
+    FL_STAMP(2);
+    if (lagged && threadIdx.x >= 64 && threadIdx.x < 64 + R) {
+        // the lagged scoring's argmax (C:148 evaluation, published one round later), on wave 1
+        // while wave 0 runs the loss; counts -> b.cnt after the barrier below
+        const int r = threadIdx.x - 64;
+        if (row0 + r < c.n_rows) {
+            const float* zr = reinterpret_cast<const float*>(lds + el.logit_off) + r * 16;
+            const int yl = b.y[row0 + r];
             int best = 0;
             float bv = zr[0];
             for (int k = 1; k < C; ++k)
                 if (zr[k] > bv) { bv = zr[k]; best = k; }
-            atomicAdd(&cm_s[ylab * C + best], 1);
+            atomicAdd(&cm_s[yl * C + best], 1);
         }
-        lds_barrier();
-        for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
-            if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
     }
-    forward_block_bf16<RT>(d, e, lds, b.dbg);
-    FL_STAMP(2);
 
     // softmax cross-entropy (mean over the shard): D_L = (softmax - onehot) / n, bf16.
     // Fused evaluation: the same logits score the previous round's model (argmax).
@@ -448,7 +465,7 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
         if (threadIdx.x == 0) slab[d.P] = lossv;
     }
     lds_barrier();
-    if (score)
+    if (score || lagged)
         for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
             if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
     FL_STAMP(3);
