@@ -49,7 +49,7 @@ class EngineConfig:
     rtol: float = 1e-5
     max_rounds: int = 300
     metric_mode: str = "mean"       # 'mean' (C:169) | 'pooled' (S:130)
-    rows_per_block: int = 0         # R rows per workgroup of the fused kernels (16 | 32; 0 = auto)
+    rows_per_block: int = 0         # R rows per workgroup of the fused kernels (16 | 32 | 64 (bf16); 0 = auto)
     graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
     seed: int = 0
     debug: bool = False             # eager, synchronised phases + non-finite checks every round

@@ -146,7 +146,7 @@ class FLEngine {
         d_.Pimg = (io + 3) & ~3;
 
         c_.R = cfg["R"].cast<int>();
-        if (c_.R != 16 && c_.R != 32) throw std::runtime_error("FLEngine: R must be 16 or 32");
+        if (c_.R != 16 && c_.R != 32 && c_.R != 64) throw std::runtime_error("FLEngine: R must be 16, 32 or 64");
         int lds = 0;
         for (int l = 0; l <= L; ++l) {
             d_.ld[l] = pick_ld(dims[l]);
@@ -166,6 +166,7 @@ class FLEngine {
         d_.lds_floats = lds;
         dtype_ = cfg.contains("dtype") ? cfg["dtype"].cast<int>() : 0;
         if (dtype_ == 0) {
+            if (c_.R == 64) throw std::runtime_error("FLEngine: R = 64 needs the bf16 kernels");
             if ((size_t)lds * 4 > FL_LDS_DYNAMIC_MAX)
                 throw std::runtime_error("FLEngine: activations exceed LDS; use a smaller R or the layered path");
             HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));

@@ -247,13 +247,16 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
     for (int t = wave; t < otiles * itiles; t += FL_WAVES) {
         const int ot = t / itiles, it = t - ot * itiles;
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        if (RT == 2) {
-            const int r0 = 8 * lg + lq;
-            const char* pa = D + (r0 * ldd + ot * 16 + 4 * lp) * 2;
-            const char* pb = act + (r0 * lda + it * 16 + 4 * lp) * 2;
-            const bf16x8 a = cat8(ld_tr(pa), ld_tr(pa + 4 * ldd * 2));
-            const bf16x8 b = cat8(ld_tr(pb), ld_tr(pb + 4 * lda * 2));
-            acc = mfma32(a, b, acc);
+        if (RT >= 2) {  // 32-row K chunks
+#pragma unroll
+            for (int h = 0; h < RT / 2; ++h) {
+                const int r0 = 32 * h + 8 * lg + lq;
+                const char* pa = D + (r0 * ldd + ot * 16 + 4 * lp) * 2;
+                const char* pb = act + (r0 * lda + it * 16 + 4 * lp) * 2;
+                const bf16x8 a = cat8(ld_tr(pa), ld_tr(pa + 4 * ldd * 2));
+                const bf16x8 b = cat8(ld_tr(pb), ld_tr(pb + 4 * lda * 2));
+                acc = mfma32(a, b, acc);
+            }
         } else {
             const int r0 = 4 * lg + lq;
             const bf16x4 a = ld_tr(D + (r0 * ldd + ot * 16 + 4 * lp) * 2);
@@ -569,6 +572,10 @@ hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLCon
             hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
                                so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask, eloc);
             break;
+        case 64:
+            hipLaunchKernelGGL(fl_train_bf16_kernel<4>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
+                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask, eloc);
+            break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -585,6 +592,10 @@ hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConf
             break;
         case 32:
             hipLaunchKernelGGL(fl_eval_bf16_kernel<2>, dim3(blocks), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
+                               params, cm, st);
+            break;
+        case 64:
+            hipLaunchKernelGGL(fl_eval_bf16_kernel<4>, dim3(blocks), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
                                params, cm, st);
             break;
         default: return hipErrorInvalidValue;
@@ -627,8 +638,8 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
 #define FLB_SET(fn)                                                                                     \
     if (r == hipSuccess)                                                                                \
     r = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, v)
-    FLB_SET(fl_train_bf16_kernel<1>); FLB_SET(fl_train_bf16_kernel<2>);
-    FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>);
+    FLB_SET(fl_train_bf16_kernel<1>); FLB_SET(fl_train_bf16_kernel<2>); FLB_SET(fl_train_bf16_kernel<4>);
+    FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>); FLB_SET(fl_eval_bf16_kernel<4>);
     FLB_SET(fl_eval_fedavg_bf16_kernel<1>); FLB_SET(fl_eval_fedavg_bf16_kernel<2>);
 #undef FLB_SET
     return r;

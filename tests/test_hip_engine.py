@@ -307,7 +307,7 @@ def test_hip_debug_mode_and_profile():
         g.run(1)
 
 
-@pytest.mark.parametrize("R", [16, 32])
+@pytest.mark.parametrize("R", [16, 32, 64])
 @pytest.mark.parametrize("hidden", [(50, 200), (7,), (33, 17, 9)])
 def test_bf16_engine_tracks_fp32_oracle(R, hidden):
     """bf16 MFMA operands (fp32 accumulate / master weights): one round's update matches the
