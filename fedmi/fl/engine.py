@@ -362,7 +362,7 @@ class TorchRoundEngine(RoundEngineBase):
 # ---------------------------------------------------------------------------------------
 _STATE_DTYPE = np.dtype([("next_round", "<i4"), ("finalized", "<i4"), ("stopped", "<i4"), ("live", "<i4"),
                          ("cur_round", "<i4"), ("count", "<i4"), ("has_prev", "<i4"), ("stop_round", "<i4"),
-                         ("prev", "<f8", (4,))])
+                         ("calls", "<u4"), ("pad0", "<i4"), ("prev", "<f8", (4,))])
 
 
 class HipRoundEngine(RoundEngineBase):
@@ -471,7 +471,9 @@ class HipRoundEngine(RoundEngineBase):
         if self.world > 1 and comm_buffers is None and getattr(comm, "peer_allreduce", False):
             from ..parallel.peer import make_peer_allreduce
             torch.cuda.synchronize(dev)
-            self._peer = make_peer_allreduce(comm, comm_len, dev)
+            # lagged rounds reduce inside the Adam kernel: one chunk flag per Adam block + tails
+            n_chunks = (self.P + 63) // 64 + 1 if (self._lag and int(cfg.local_steps) == 1) else 0
+            self._peer = make_peer_allreduce(comm, comm_len, dev, n_chunks=n_chunks)
             if self._peer is not None:
                 self.engine.attach_peer(self._peer)
         self._graph_ready = False
@@ -482,7 +484,7 @@ class HipRoundEngine(RoundEngineBase):
         if self.world == 1:
             return "none"
         if self._peer is not None:
-            return "xgmi-oneshot"
+            return "xgmi-oneshot+adam" if self.engine.adam_exchange else "xgmi-oneshot"
         return "rccl" if self._native_comm is not None else "host"
 
     # -- execution --
@@ -710,6 +712,8 @@ class HipRoundEngine(RoundEngineBase):
             rec["prev"] = np.asarray(es["prev"], np.float64)
             rec["stopped"] = int(bool(es["stopped"]))
             rec["stop_round"] = int(es["stop_round"])
+            # the peer exchange's call counter stays monotonic (peers' flags hold past calls)
+            rec["calls"] = max(int(self.state[q].cpu().numpy().view(_STATE_DTYPE)[0]["calls"]) for q in (0, 1))
             self.state[r & 1].copy_(torch.as_tensor(rec.view(np.uint8).copy()).to(dev))
             self._load_history(st["history"])
             n = self.hist.rounds_run

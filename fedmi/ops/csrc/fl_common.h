@@ -115,6 +115,8 @@ struct FLState {
     int count;          // patience counter (termination_count, C:125)
     int has_prev;
     int stop_round;     // round index at which the stop took effect (-1 = none)
+    unsigned calls;     // Adam-fused FedAvg exchanges done (call index of the chunk flags, peer_device.h)
+    int pad0;
     double prev[4];     // prev_metric (C:126)
 };
 
@@ -169,6 +171,8 @@ struct FLBuffers {
 #define FL_CM_FLAG (FL_MAX_CLASSES * FL_MAX_CLASSES)
 #define FL_CM_INTS (FL_CM_FLAG + 4)
 
+struct PeerArgs;  // peer_device.h
+struct PeerPack;
 // Launchers (fl_kernels.hip). `pg` = image the round trains from (the previous round's
 // all-reduced comm buffer), `comm` = buffer this round publishes into (Pimg + tail floats).
 // `cm_out` = this rank's confusion slots of pg's tail (FL_EVAL_FUSED only).
@@ -183,7 +187,7 @@ hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
                           const float* pin, const float* anchor, float* comm,
                           const FLState* st, int local_step, hipStream_t s,
                           const MLPDescB* e = nullptr, FLState* st_out = nullptr, int fold = 0,
-                          int tail_a = 0, int fold_mask = FL_FOLD_B);
+                          int tail_a = 0, int fold_mask = FL_FOLD_B, const PeerArgs* xchg = nullptr);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
@@ -203,8 +207,6 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes);
 // Local evaluation + FedAvg in one kernel (world > 1 with the one-shot xGMI all-reduce,
 // peer_device.h): the all-reduce of the call described by `a` runs in extra blocks beside
 // the evaluation of `params` into this rank's tail slot of `comm` (the call's send buffer).
-struct PeerArgs;
-struct PeerPack;
 hipError_t fl_launch_eval_fedavg(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* params,
                                  float* comm, const FLState* st, const PeerArgs& a, const PeerPack& pk,
                                  hipStream_t s);

@@ -366,6 +366,7 @@ class FLEngine {
         return fused_ ? cm_in_tail_ : pending_cm_;
     }
     bool lagged() const { return lagged_; }
+    bool adam_exchange() const { return xchg_; }
     bool fused() const { return fused_; }
 
     // The host wrote the global weights (set_weights / resume): the next round repacks them.
@@ -392,6 +393,9 @@ class FLEngine {
         drop_graph();
         peer_ = &p;
         p.prepare_eval((c_.n_rows + c_.R - 1) / c_.R);
+        // lagged rounds reduce inside the Adam kernel when the communicator has a chunk-flag
+        // table for every Adam block (+ the tail block); one local step per round
+        xchg_ = lagged_ && c_.local_steps == 1 && p.n_chunks() >= (d_.P + 63) / 64 + 1;
         std::memset(&pp_, 0, sizeof(pp_));
         if (dtype_ == 1) {
             pp_.pk = b_.pk_global;
@@ -567,9 +571,9 @@ class FLEngine {
     }
     void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
                      hipStream_t s, FLState* st_out = nullptr, int fold = 0, int tail_a = 0,
-                     int fold_mask = FL_FOLD_B) {
+                     int fold_mask = FL_FOLD_B, const PeerArgs* xchg = nullptr) {
         HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr, st_out,
-                                 fold, tail_a, fold_mask));
+                                 fold, tail_a, fold_mask, xchg));
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
@@ -581,7 +585,8 @@ class FLEngine {
     // Lagged rounds (FL_EVAL_LAGGED): the train kernel scores the previous round's local model
     // iff that round had no evaluation of its own; its fold consumes region A when the previous
     // round scored ITS predecessor and region B when the previous round was evaluated.
-    void issue_train(int r, hipStream_t s, bool fused) {
+    // `xchg`: this round's FedAvg runs inside its Adam kernel (peer_device.h chunk exchange).
+    void issue_train(int r, hipStream_t s, bool fused, bool xchg = false) {
         float* pg = pbuf_[r & 1];
         float* cb = comm_buf(r);
         FLState* si = st_[r & 1];
@@ -598,7 +603,12 @@ class FLEngine {
         for (int ls = 0; ls < c_.local_steps; ++ls) {
             const bool first = ls == 0;
             launch_train(pg, first ? si : so, so, ls, s, first ? mode : FL_EVAL_CLASSIC, cm_out, mask);
-            if (first) launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask);
+            if (first && xchg) {
+                const PeerArgs pa = peer_->args((r + 1) & 1, pbuf_[(r + 1) & 1]);
+                launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask, &pa);
+            } else if (first) {
+                launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask);
+            }
             else launch_adam(b_.local, pg, cb, so, ls, s);
         }
         pending_cm_ = fused;
@@ -631,10 +641,11 @@ class FLEngine {
         const bool fused = fused_ && allow_fused;
         lag = lag && lagged_ && !fused;
         if (!fused) flush_pending_eval(r, s);
-        issue_train(r, s, fused);
+        const bool xchg = lag && xchg_;
+        issue_train(r, s, fused, xchg);
         prev_lagged_ = lag;
         if (lag) {
-            issue_allreduce(r, s, comm);
+            if (!xchg) issue_allreduce(r, s, comm);
             return;
         }
         if (!fused && peer_ != nullptr && eval_fedavg_fits()) {
@@ -685,6 +696,7 @@ class FLEngine {
     float* lagbuf_ = nullptr;  // FL_EVAL_LAGGED count + loss carry-over
     long long comm_len_ = 0;   // floats of a comm buffer: image + tails (+ lag region)
     bool lagged_ = false;      // several clients: evaluation scored one round later (no eval kernel)
+    bool xchg_ = false;        // lagged rounds: FedAvg inside the Adam kernel (no all-reduce kernel)
     bool prev_lagged_ = false; // the last issued round had no evaluation of its own
     bool prev_scored_ = false; // the last issued round's train kernel scored its predecessor
     bool need_pack_ = true;  // host changed the global weights: repack before the next round
@@ -755,6 +767,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("needs_eager_round", &FLEngine::needs_eager_round)
         .def_property_readonly("fused", &FLEngine::fused)
         .def_property_readonly("lagged", &FLEngine::lagged)
+        .def_property_readonly("adam_exchange", &FLEngine::adam_exchange)
         .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);

@@ -400,11 +400,48 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
 // written (it stays 0 in every buffer).  The last block writes this rank's metric tail.
 #define ADAM_WAVES 16
 #define ADAM_DEPTH 16
+// Adam step of one parameter (wave 0 lane of fl_adam_kernel) from the block's partial sums.
+__device__ __forceinline__ void adam_update(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
+                                            const MLPDescB& e, const float* __restrict__ pin,
+                                            const float* __restrict__ anchor, float* __restrict__ comm,
+                                            const FLState& S, int local_step, int last_local_step, int pack, int j,
+                                            int pk, bool is_bias, float (*part)[64], int lane) {
+    float g = 0.f;
+#pragma unroll
+    for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
+    float p = pin[j];
+    if (c.weight_decay != 0.f) g += c.weight_decay * p;
+    if (c.prox_mu != 0.f) g += c.prox_mu * (p - anchor[j]);
+    // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
+    // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
+    // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
+    const int t = S.cur_round * c.local_steps + local_step + 1;
+    const float step_size = b.sched[2 * (t - 1)];
+    const float bc2_sqrt = b.sched[2 * (t - 1) + 1];
+    float m = b.m[j], v = b.v[j];
+    m = m + c.omb1 * (g - m);
+    v = v * c.beta2f + c.omb2 * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + c.eps;
+    p = p + (-step_size) * (m / denom);
+    b.m[j] = m;
+    b.v[j] = v;
+    b.local[j] = p;
+    if (pack) {
+        if (is_bias) {
+            *reinterpret_cast<float*>(b.pk_local + pk) = p;
+        } else {
+            const uint32_t u = __float_as_uint(p);
+            *reinterpret_cast<uint16_t*>(b.pk_local + pk) = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+        }
+    }
+    if (last_local_step) comm[j] = p * c.agg_scale;
+}
+
 __global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
                const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
-               FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask) {
+               FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, PeerArgs pa, int xchg) {
     __shared__ float part[ADAM_WAVES][64];
     __shared__ FLState S_sh;
     const int last_local_step = (local_step == c.local_steps - 1);
@@ -425,6 +462,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             if (lane == 0) {
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
                 if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
+                if (xchg) S0.calls += 1;  // every rank counts its Adam-fused exchanges alike
                 if (blockIdx.x == 0) *st_out = S0;
             }
         }
@@ -481,6 +519,15 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
                 if (threadIdx.x == 0) b.lbuf[0] = loss;
             }
         }
+        if (xchg) {
+            // Adam-fused FedAvg of the metric tails (chunk nparam_blocks, peer_device.h)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // every wave's tail stores are acknowledged
+            if (wave == 0) {
+                peer_chunk_exchange_wait(pa, nparam_blocks, st->calls + 1);
+                for (int i = d.Pimg + lane; i < (int)pa.n; i += 64) pa.out[i] = peer_pull_sum(pa, i);
+            }
+        }
         return;
     }
     const int di = blockIdx.x * 64 + lane;  // dense index
@@ -534,41 +581,33 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     if (!have_state) round_state();
     part[wave][lane] = g;
     lds_barrier();
-    if (wave != 0 || !valid) return;
+    if (wave != 0) return;
     const FLState S = S_sh;
-    if (!S.live) {
-        if (last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
-        return;
-    }
-    g = 0.f;
-#pragma unroll
-    for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
-    float p = pin[j];
-    if (c.weight_decay != 0.f) g += c.weight_decay * p;
-    if (c.prox_mu != 0.f) g += c.prox_mu * (p - anchor[j]);
-    // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
-    // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
-    // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
-    const int t = S.cur_round * c.local_steps + local_step + 1;
-    const float step_size = b.sched[2 * (t - 1)];
-    const float bc2_sqrt = b.sched[2 * (t - 1) + 1];
-    float m = b.m[j], v = b.v[j];
-    m = m + c.omb1 * (g - m);
-    v = v * c.beta2f + c.omb2 * g * g;
-    const float denom = sqrtf(v) / bc2_sqrt + c.eps;
-    p = p + (-step_size) * (m / denom);
-    b.m[j] = m;
-    b.v[j] = v;
-    b.local[j] = p;
-    if (pack) {
-        if (is_bias) {
-            *reinterpret_cast<float*>(b.pk_local + pk) = p;
+    if (valid) {
+        if (!S.live) {
+            if (last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
         } else {
-            const uint32_t u = __float_as_uint(p);
-            *reinterpret_cast<uint16_t*>(b.pk_local + pk) = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+            adam_update(d, c, b, e, pin, anchor, comm, S, local_step, last_local_step, pack, j, pk, is_bias,
+                        part, lane);
         }
     }
-    if (last_local_step) comm[j] = p * c.agg_scale;
+    if (xchg) {
+        // Adam-fused FedAvg of this block's 64 parameters (peer_device.h): publish, wait for
+        // every rank's chunk, pull + sum in rank order; global image + packed bf16 image
+        peer_chunk_exchange_wait(pa, blockIdx.x, st->calls + 1);
+        if (valid) {
+            const float gsum = peer_pull_sum(pa, j);
+            pa.out[j] = gsum;
+            if (pack) {
+                if (is_bias) {
+                    *reinterpret_cast<float*>(b.pk_global + pk) = gsum;
+                } else {
+                    const uint32_t u = __float_as_uint(gsum);
+                    *reinterpret_cast<uint16_t*>(b.pk_global + pk) = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+                }
+            }
+        }
+    }
 }
 
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,
@@ -731,13 +770,21 @@ hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers&
 
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
                           const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s,
-                          const MLPDescB* e, FLState* st_out, int fold, int tail_a, int fold_mask) {
+                          const MLPDescB* e, FLState* st_out, int fold, int tail_a, int fold_mask,
+                          const PeerArgs* xchg) {
     if (fold && st_out == nullptr) return hipErrorInvalidValue;
+    // the exchange's call index advances in the folded state: fused exchange needs the fold
+    if (xchg != nullptr && (!fold || local_step != c.local_steps - 1 || xchg->n_chunks < (d.P + 63) / 64 + 1))
+        return hipErrorInvalidValue;
+    PeerArgs pa;
+    PeerArgs zero_pa = {};
+    pa = zero_pa;
+    if (xchg != nullptr) pa = *xchg;
     const int blocks = (d.P + 63) / 64 + 1;
     MLPDescB ee = {};
     if (e != nullptr) ee = *e;
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
-                       local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask);
+                       local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask, pa, xchg != nullptr ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -12,7 +12,8 @@
 
 class PeerAllReduce {
   public:
-    PeerAllReduce(int world, int rank, int device, long long n_floats, double timeout_s);
+    // n_chunks > 0: chunk-flag table for the Adam-fused exchange (peer_device.h)
+    PeerAllReduce(int world, int rank, int device, long long n_floats, double timeout_s, int n_chunks = 0);
     ~PeerAllReduce();
     PeerAllReduce(const PeerAllReduce&) = delete;
     PeerAllReduce& operator=(const PeerAllReduce&) = delete;
@@ -36,12 +37,14 @@ class PeerAllReduce {
     long long n_floats() const { return n_; }
     int world() const { return world_; }
     int rank() const { return rank_; }
+    int n_chunks() const { return n_chunks_; }
     bool is_open() const { return open_; }
     void close();
 
   private:
     int world_, rank_, device_;
     long long n_;
+    int n_chunks_ = 0;
     size_t buf_bytes_ = 0, total_ = 0;
     char* base_ = nullptr;
     std::vector<char*> mapped_;        // peers' allocations, opened from their IPC handles

@@ -64,14 +64,15 @@ __global__ void peer_fill_kernel(float* dst, long long n, int rank, unsigned sal
     dst[i] = (float)(h % 2048u) * 0.25f - 256.f;
 }
 
-PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, double timeout_s)
-    : world_(world), rank_(rank), device_(device), n_(n) {
+PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, double timeout_s, int n_chunks)
+    : world_(world), rank_(rank), device_(device), n_(n), n_chunks_(n_chunks < 0 ? 0 : n_chunks) {
     if (world < 1 || world > PEER_MAX_WORLD) throw std::runtime_error("PeerAllReduce: world must be 1..8");
     if (rank < 0 || rank >= world) throw std::runtime_error("PeerAllReduce: bad rank");
     if (n <= 0 || n * 4 > (1ll << 30)) throw std::runtime_error("PeerAllReduce: 1..2^28 floats");
     PHIP(hipSetDevice(device));
     buf_bytes_ = ((size_t)n * 4 + 255) & ~(size_t)255;
-    total_ = 2 * buf_bytes_ + sizeof(PeerCtl);
+    // [send 0 | send 1 | control block | chunk flags: PEER_MAX_WORLD x n_chunks]
+    total_ = 2 * buf_bytes_ + sizeof(PeerCtl) + (((size_t)PEER_MAX_WORLD * n_chunks_ * 4 + 255) & ~(size_t)255);
     // Uncached device memory (MTYPE UC, what RCCL uses for its xGMI buffers): peers write the
     // flags and read the send buffers over xGMI, and no L2 -- this GPU's or a peer's -- may
     // hold a stale copy of either.  The send buffers are written once per round (~50 KB),
@@ -186,6 +187,13 @@ PeerArgs PeerAllReduce::args(int parity, float* out, long long n_w) const {
     a.eflags = eflags_;
     a.n_eval = n_eval_;
     a.world = world_;
+    a.n_chunks = n_chunks_;
+    if (n_chunks_ > 0) {
+        for (int j = 0; j < world_; ++j)
+            a.cflag_dst[j] = reinterpret_cast<unsigned*>(peer_base_[j] + 2 * buf_bytes_ + sizeof(PeerCtl)) +
+                             (size_t)rank_ * n_chunks_;
+        a.cflags = reinterpret_cast<unsigned*>(base_ + 2 * buf_bytes_ + sizeof(PeerCtl));
+    }
     return a;
 }
 
@@ -203,8 +211,9 @@ hipError_t PeerAllReduce::launch(int parity, float* out, const PeerPack* pack, h
 
 void register_peer(py::module_& m) {
     py::class_<PeerAllReduce>(m, "PeerAllReduce")
-        .def(py::init<int, int, int, long long, double>(), py::arg("world"), py::arg("rank"), py::arg("device"),
-             py::arg("n_floats"), py::arg("timeout_s") = 60.0)
+        .def(py::init<int, int, int, long long, double, int>(), py::arg("world"), py::arg("rank"), py::arg("device"),
+             py::arg("n_floats"), py::arg("timeout_s") = 60.0, py::arg("n_chunks") = 0)
+        .def_property_readonly("n_chunks", &PeerAllReduce::n_chunks)
         .def("handle", &PeerAllReduce::handle)
         .def("open", &PeerAllReduce::open)
         .def("send_ptr", [](const PeerAllReduce& p, int parity) { return reinterpret_cast<uintptr_t>(p.send(parity)); })

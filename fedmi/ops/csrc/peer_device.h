@@ -59,6 +59,11 @@ struct PeerArgs {
     unsigned* eflags;                    // fused calls: per evaluation block, last call it finished
     int n_eval;                          // evaluation blocks of a fused call
     int world;
+    // Adam-fused exchange (chunked flags, call index = FLState::calls): chunk k of call t
+    // published by rank j  <=>  cflags_j... row of rank j in MY chunk-flag table >= t
+    unsigned* cflag_dst[PEER_MAX_WORLD]; // &chunk_flags_j[rank * n_chunks]: my row in rank j's table
+    unsigned* cflags;                    // my table: [world][n_chunks]
+    int n_chunks;
 };
 
 // All-reduce blocks of a fused evaluation + FedAvg kernel (FL_THREADS = 512 threads each):
@@ -249,4 +254,44 @@ __device__ __forceinline__ void peer_eval_done(const PeerArgs& a, unsigned targe
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&a.eflags[blk], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------------
+// Adam-fused exchange: the FedAvg all-reduce inside the Adam kernel (fl_kernels.hip).  The
+// block that updated a chunk of parameters publishes it (its values are in the uncached send
+// buffer once acknowledged), waits for the same chunk from every rank and pulls + sums it:
+// no separate all-reduce kernel, no kernel boundary between the update and the reduction.
+// Executed by one wave; `target` = the call index (device round state, same on every rank).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void peer_chunk_exchange_wait(const PeerArgs& a, int chunk, unsigned target) {
+    const int lane = threadIdx.x & 63;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's send-buffer stores are done
+    if (lane < a.world)
+        __hip_atomic_store(a.cflag_dst[lane] + chunk, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane < a.world) {
+        const unsigned* f = a.cflags + lane * a.n_chunks + chunk;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
+                __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Sum over ranks (rank order) of the send buffers at float position `pos`.
+__device__ __forceinline__ float peer_pull_sum(const PeerArgs& a, int pos) {
+    const int bytes = (int)(a.n * 4);
+    float v[PEER_MAX_WORLD];
+#pragma unroll
+    for (int k = 0; k < PEER_MAX_WORLD; ++k)
+        if (k < a.world) v[k] = peer_load4(a.src[k], bytes, pos * 4);
+    float s = v[0];
+#pragma unroll
+    for (int k = 1; k < PEER_MAX_WORLD; ++k)
+        if (k < a.world) s += v[k];
+    return s;
 }

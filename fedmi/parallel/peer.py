@@ -52,16 +52,19 @@ def selftest(h, comm, device, calls: int = 4, timeout_s: float = 10.0) -> bool:
     return ok
 
 
-def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, check: bool = True):
+def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, check: bool = True,
+                        n_chunks: int = 0):
     """Collective.  Returns a native ``PeerAllReduce`` of ``n_floats`` floats, open and
-    self-tested on every rank, or ``None`` on every rank (then the caller uses RCCL)."""
+    self-tested on every rank, or ``None`` on every rank (then the caller uses RCCL).
+    ``n_chunks``: chunk-flag table for the Adam-fused exchange of the round engine."""
     from ..ops import native
     if comm is None or comm.size < 2 or comm.size > PEER_MAX_WORLD:
         return None
     m = native()
     h, why = None, ""
     try:
-        h = m.PeerAllReduce(comm.size, comm.rank, torch.device(device).index or 0, int(n_floats), float(timeout_s))
+        h = m.PeerAllReduce(comm.size, comm.rank, torch.device(device).index or 0, int(n_floats), float(timeout_s),
+                            int(n_chunks))
         handle = bytes(h.handle())
     except Exception as e:  # noqa: BLE001 -- reported, and every rank falls back together
         handle, why = None, f"rank {comm.rank}: {e}"

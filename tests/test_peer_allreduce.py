@@ -36,8 +36,10 @@ def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = Tr
     cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4, eval_fedavg=eval_fedavg,
                        lagged_eval=lagged)
     e = HipRoundEngine(X, y, 2, cfg, comm, flat)
-    assert e.aggregation == ("xgmi-oneshot" if peer else "host"), e.aggregation
-    assert bool(e.engine.lagged) == (lagged and dtype == "bf16"), (e.engine.lagged, lagged, dtype)
+    lag = lagged and dtype == "bf16"
+    assert e.aggregation == (("xgmi-oneshot+adam" if lag else "xgmi-oneshot") if peer else "host"), e.aggregation
+    assert bool(e.engine.lagged) == lag, (e.engine.lagged, lagged, dtype)
+    assert bool(e.engine.adam_exchange) == (lag and peer)
     e.run(3)                       # eager rounds
     cms = []
     for _ in range(2):             # reference step-by-step API

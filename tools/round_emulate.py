@@ -6,7 +6,8 @@ latency of the pulls.  Prints us/round for
   * world 1, fused evaluation (what bench.py runs at N = 1);
   * classic evaluation + separate one-shot all-reduce kernel;
   * the fused evaluation + FedAvg kernel (N > 1 with early stopping);
-  * lagged evaluation: round r scored inside round r+1's train kernel, no evaluation kernel
+  * lagged evaluation: round r scored inside round r+1's train kernel, no evaluation kernel,
+    with a separate all-reduce kernel or with the FedAvg inside the Adam kernel
     (N > 1 without early stopping: bench.py).
 
     python tools/round_emulate.py [--rounds 2000] [--dtype bf16]
@@ -36,10 +37,11 @@ def main():
     torch.cuda.set_device(dev)
     X, y = bench.synth_shard(a.rows, 0, dev)
     flat = init_flat([14, 50, 200, 2], 0)
-    cases = (("world 1, fused evaluation", True, None, False), ("eval + one-shot all-reduce", False, False, False),
-             ("fused eval + FedAvg kernel", False, True, False),
-             ("lagged eval (no eval kernel)", False, True, True))
-    for name, fused, ef, lag in cases:
+    cases = (("world 1, fused evaluation", True, None, False, 0), ("eval + one-shot all-reduce", False, False, False, 0),
+             ("fused eval + FedAvg kernel", False, True, False, 0),
+             ("lagged eval + all-reduce kernel", False, True, True, 0),
+             ("lagged eval + FedAvg in Adam", False, True, True, 1))
+    for name, fused, ef, lag, adam_x in cases:
         if lag and a.dtype != "bf16":
             continue
         cfg = EngineConfig(max_rounds=a.rounds + 256, early_stop=False, dtype=a.dtype, graph_rounds=16,
@@ -47,7 +49,7 @@ def main():
         e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=lag)
         h = None
         if ef is not None:
-            h = m.PeerAllReduce(1, 0, 0, int(e.params[0].numel()), 10.0)
+            h = m.PeerAllReduce(1, 0, 0, int(e.params[0].numel()), 10.0, (e.P + 63) // 64 + 1 if adam_x else 0)
             h.open([h.handle()])
             h.clear()
             e.engine.attach_peer(h)
