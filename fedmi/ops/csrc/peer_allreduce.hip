@@ -56,6 +56,15 @@ __global__ void __launch_bounds__(PEER_THREADS) peer_allreduce_kernel(PeerArgs a
     peer_finish(a, target, gridDim.x);
 }
 
+// Self-test of the Adam-fused chunk exchange (peer_device.h): block c exchanges chunk c
+// (floats [64c, 64c + 64)) of the send buffers with call index `target`.
+__global__ void __launch_bounds__(64) peer_chunk_test_kernel(PeerArgs a, unsigned target, float* out) {
+    const int c = blockIdx.x;
+    peer_chunk_exchange_wait(a, c, target);
+    const int pos = c * 64 + (int)threadIdx.x;
+    if (pos < a.n) out[pos] = peer_pull_sum(a, pos);
+}
+
 // Self-test payload: exact in fp32 for any summation order (multiples of 1/4 in [-256, 256)).
 __global__ void peer_fill_kernel(float* dst, long long n, int rank, unsigned salt) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -159,6 +168,9 @@ void PeerAllReduce::prepare_eval(int n_eval) {
 void PeerAllReduce::clear() {
     PHIP(hipSetDevice(device_));
     PHIP(hipMemset(base_, 0, 2 * buf_bytes_));
+    // chunk flags restart at 0: the engine's call index starts at 1 (self-test calls used it)
+    if (n_chunks_ > 0)
+        PHIP(hipMemset(base_ + 2 * buf_bytes_ + sizeof(PeerCtl), 0, (size_t)PEER_MAX_WORLD * n_chunks_ * 4));
     PHIP(hipDeviceSynchronize());
 }
 
@@ -220,6 +232,14 @@ void register_peer(py::module_& m) {
         .def("allreduce",
              [](const PeerAllReduce& p, int parity, uintptr_t out, uintptr_t stream) {
                  PHIP(p.launch(parity, reinterpret_cast<float*>(out), nullptr, reinterpret_cast<hipStream_t>(stream)));
+             })
+        .def("chunk_test",
+             [](const PeerAllReduce& p, int parity, unsigned target, uintptr_t out, uintptr_t stream) {
+                 if (p.n_chunks() <= 0) throw std::runtime_error("chunk_test: no chunk-flag table");
+                 const PeerArgs a = p.args(parity, reinterpret_cast<float*>(out));
+                 hipLaunchKernelGGL(peer_chunk_test_kernel, dim3(p.n_chunks()), dim3(64), 0,
+                                    reinterpret_cast<hipStream_t>(stream), a, target, reinterpret_cast<float*>(out));
+                 PHIP(hipGetLastError());
              })
         .def("fill_test",
              [](const PeerAllReduce& p, int parity, unsigned salt, uintptr_t stream) {

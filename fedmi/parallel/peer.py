@@ -48,6 +48,19 @@ def selftest(h, comm, device, calls: int = 4, timeout_s: float = 10.0) -> bool:
         got = out.cpu().numpy()
         expect = sum(fill_values(n, r, salt) for r in range(comm.size)).astype(np.float32)
         ok = ok and bool(np.array_equal(got, expect))
+    # the Adam-fused chunk exchange (peer_device.h): same payload, chunk flags, both parities
+    nc = int(getattr(h, "n_chunks", 0))
+    if nc > 0:
+        m = min(n, nc * 64)
+        out.zero_()
+        for k in range(2):
+            salt = 2000 + k
+            h.fill_test(k & 1, salt, s.cuda_stream)
+            h.chunk_test(k & 1, k + 1, out.data_ptr(), s.cuda_stream)
+            got = out.cpu().numpy()[:m]
+            expect = sum(fill_values(n, r, salt) for r in range(comm.size)).astype(np.float32)[:m]
+            ok = ok and bool(np.array_equal(got, expect))
+            comm.Barrier()  # every rank has read this parity before it is refilled
     ok = ok and h.error() == 0
     return ok
 
