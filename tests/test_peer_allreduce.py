@@ -137,3 +137,60 @@ def test_peer_allreduce_two_ranks_one_gpu():
         np.testing.assert_array_equal(out[0][1][dtype][0][0], out[1][1][dtype][0][0])
     for p in procs:
         assert p.exitcode == 0
+
+
+def _worker4(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        import torch
+        from fedmi.data.synthetic import make_income_like
+        from fedmi.models.mlp import init_flat
+        from fedmi.parallel.comm import Comm
+        from fedmi.parallel.peer import make_peer_allreduce, selftest
+        comm = Comm(backend="xgmi", device="cuda:0", rccl=False)
+        dev = comm.device
+        h = make_peer_allreduce(comm, 3001, dev, timeout_s=30.0, n_chunks=48)
+        ok = h is not None and bool(all(comm.allgather(selftest(h, comm, dev, calls=4))))
+        comm.Barrier()
+        if h is not None:
+            h.close()
+        X, y = make_income_like(900 + 100 * rank, seed=30 + rank)   # unequal shards: n_i / N weights
+        flat = init_flat([14, 50, 200, 2], 5)
+        a = _run_engine(comm, True, "bf16", X, y, flat)
+        # classic rounds over the standalone peer kernel: the same rank-order sums (gloo's
+        # 4-rank reduction order differs, so the host path is not a bitwise reference here)
+        b = _run_engine(comm, True, "bf16", X, y, flat, True, False)
+        torch.cuda.synchronize()
+        comm.Barrier()
+        q.put((rank, (ok, a, b), None))
+        comm.close()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_peer_four_ranks_lagged_adam_exchange():
+    """W = 4 (more ranks than the 2-rank test: the unrolled rank loops and chunk-flag rows):
+    self-tests pass and the lagged engine with FedAvg inside the Adam kernel equals classic
+    rounds over the standalone peer kernel bit for bit, with unequal shard sizes."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker4, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=110) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+    for rank, res, err in out:
+        assert err is None, f"rank {rank}:\n{err}"
+        ok, (wa, ha, ca), (wb, hb, cb) = res
+        assert ok
+        np.testing.assert_array_equal(wa, wb)
+        np.testing.assert_array_equal(ha["global"], hb["global"])
+        np.testing.assert_array_equal(ha["per_rank"], hb["per_rank"])
+        np.testing.assert_array_equal(ca, cb)
+    for r in range(1, world):
+        np.testing.assert_array_equal(out[0][1][1][0], out[r][1][1][0])
