@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import sys
+import time
 
 import numpy as np
 
@@ -122,9 +123,11 @@ def main(argv=None):
         if rank == 0:
             print("Phase timings (us/round, first %d rounds): " % a.profile
                   + ", ".join(f"{k}: {v:.2f}" for k, v in timings.items()), flush=True)
+    t_train = time.perf_counter()
     global_metrics = trainer.train_and_evaluate(comm, rounds=a.rounds, termination_patience=a.patience,
                                                 tolerance=a.tolerance, verbose=not a.quiet,
                                                 fault=parse_fault(a.fault_inject), watchdog_s=a.watchdog_s)
+    t_train = time.perf_counter() - t_train
     if a.mode == "correct":
         test = trainer.evaluate_global(ds.X_test, ds.y_test, comm)
         if rank == 0:
@@ -132,7 +135,16 @@ def main(argv=None):
                   + ", ".join(f"{k}: {v:.4f}" for k, v in test.items()), flush=True)
     if rank == 0 and a.jsonl:
         w = JsonlWriter(a.jsonl)
-        w.history(trainer.history(), clients=size, script="C", timings=timings)
+        # run-level observability: data plane, bytes all-reduced per round and
+        # client, wall-clock throughput of the whole loop (host logging included)
+        eng = trainer.engine
+        h = trainer.history()
+        rounds_run = max(int(h["rounds_run"]), 1)
+        comm_floats = int(eng.params[0].numel()) if hasattr(eng, "params") else int(eng.P + eng.world * eng.tail_stride)
+        w.history(h, clients=size, script="C", timings=timings,
+                  aggregation=getattr(eng, "aggregation", "host"),
+                  allreduce_bytes_per_round=4 * comm_floats if size > 1 else 0,
+                  wall_s=t_train, samples_per_s_per_client=len(trainer.X_local) * rounds_run / max(t_train, 1e-9))
         w.close()
     if a.save:
         save_checkpoint(a.save, trainer)   # collective: every client writes its optimizer state
