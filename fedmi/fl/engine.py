@@ -62,10 +62,11 @@ class EngineConfig:
     # all-reduce in ONE kernel, the weights' all-reduce overlapping the evaluation
     # (fedmi/ops/csrc/peer_device.h); False = separate eval and all-reduce kernels
     eval_fedavg: bool = True
-    # world > 1, early stopping off, bf16: score round r's post-step local model inside round
-    # r+1's train kernel and publish the counts with round r+1's all-reduce -- no evaluation
-    # kernel in the round; the last round of every run() evaluates itself (fl_common.h
-    # FL_EVAL_LAGGED).  Metrics, history and weights are identical to classic rounds.
+    # world > 1, bf16: score round r's post-step local model inside round r+1's train kernel --
+    # no evaluation kernel in the round; the counts are exchanged inside round r+1's Adam
+    # kernel (one-shot xGMI) or, without early stopping, ride round r+1's all-reduce; the
+    # last round of every run() evaluates itself (fl_common.h FL_EVAL_LAGGED).  Metrics,
+    # history, early-stop round and weights are identical to classic rounds.
     lagged_eval: bool = True
 
     def to_dict(self) -> dict:
@@ -397,7 +398,9 @@ class HipRoundEngine(RoundEngineBase):
         self.Pimg = image_layout(self.dims)[2]
         # lagged evaluation carries a second metric region after the tails (fl_common.h)
         # (emulate_clients: one process measures the multi-client round shape, tools/round_emulate.py)
-        self._lag = ((self.world > 1 or emulate_clients) and not cfg.early_stop and cfg.dtype == "bf16"
+        # (with early stopping the native engine runs lagged rounds only with the Adam-fused
+        # exchange, which folds each round's metrics in time)
+        self._lag = ((self.world > 1 or emulate_clients) and cfg.dtype == "bf16"
                      and comm_buffers is None and bool(cfg.lagged_eval))
         comm_len = self.Pimg + self.world * self.tail_stride * (2 if self._lag else 1)
         if comm_buffers is None:
@@ -471,8 +474,9 @@ class HipRoundEngine(RoundEngineBase):
         if self.world > 1 and comm_buffers is None and getattr(comm, "peer_allreduce", False):
             from ..parallel.peer import make_peer_allreduce
             torch.cuda.synchronize(dev)
-            # lagged rounds reduce inside the Adam kernel: one chunk flag per Adam block + tails
-            n_chunks = (self.P + 63) // 64 + 1 if (self._lag and int(cfg.local_steps) == 1) else 0
+            # lagged rounds reduce inside the Adam kernel: one chunk flag per Adam block + the
+            # two metric-tail chunks
+            n_chunks = (self.P + 63) // 64 + 2 if (self._lag and int(cfg.local_steps) == 1) else 0
             self._peer = make_peer_allreduce(comm, comm_len, dev, n_chunks=n_chunks)
             if self._peer is not None:
                 self.engine.attach_peer(self._peer)

@@ -187,7 +187,8 @@ hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
                           const float* pin, const float* anchor, float* comm,
                           const FLState* st, int local_step, hipStream_t s,
                           const MLPDescB* e = nullptr, FLState* st_out = nullptr, int fold = 0,
-                          int tail_a = 0, int fold_mask = FL_FOLD_B, const PeerArgs* xchg = nullptr);
+                          int tail_a = 0, int fold_mask = FL_FOLD_B, const PeerArgs* peer = nullptr, int wx = 0,
+                          int afold = 0);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,

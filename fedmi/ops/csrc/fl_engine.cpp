@@ -218,9 +218,11 @@ class FLEngine {
         if (lag_req) c_.lag_off = d_.Pimg + c_.tail_len;
         comm_len_ = d_.Pimg + c_.tail_len * (lag_req ? 2 : 1);
         const bool emulate = cfg.contains("emulate_clients") && cfg["emulate_clients"].cast<bool>();
-        lagged_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !c_.es_enabled && !fused_ &&
+        // (with early stopping the rounds are lagged only when the FedAvg runs inside the Adam
+        // kernel, which then also exchanges and folds the metrics in time: see lagged())
+        lag_ok_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !fused_ &&
                   (size_t)el_.lds_bytes <= FL_LDS_DYNAMIC_MAX;
-        if (lagged_) HIP_CHECK(fl_set_lds_limit_bf16((size_t)el_.lds_bytes));
+        if (lag_ok_) HIP_CHECK(fl_set_lds_limit_bf16((size_t)el_.lds_bytes));
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
@@ -277,7 +279,7 @@ class FLEngine {
     // `close`, the last, which evaluates itself: after it every metric is in the buffers.
     void run(int r0, int n, uintptr_t stream, RcclComm* comm, bool close = true) {
         hipStream_t s = as_stream(stream);
-        for (int r = r0; r < r0 + n; ++r) issue_round(r, s, comm, true, lagged_ && !(close && r == r0 + n - 1));
+        for (int r = r0; r < r0 + n; ++r) issue_round(r, s, comm, true, lagged() && !(close && r == r0 + n - 1));
     }
 
     // Local part of round r (no all-reduce; the caller reduces a shared buffer).
@@ -309,7 +311,7 @@ class FLEngine {
         flush_pending_eval(r, s);
         if (prev_lagged_)
             throw std::runtime_error("finalize: the last round is lagged (its metrics need one more round)");
-        const int mask = (prev_scored_ ? FL_FOLD_A : 0) | FL_FOLD_B;
+        const int mask = (prev_scored_ && !prev_afold_ ? FL_FOLD_A : 0) | FL_FOLD_B;
         HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s, mask));
         cm_in_tail_ = false;
     }
@@ -322,10 +324,11 @@ class FLEngine {
         if (needs_eager_round()) throw std::runtime_error("capture: issue one eager round first");
         drop_graph();
         hipStream_t s = as_stream(stream);
-        const bool pend = pending_cm_, tail = cm_in_tail_, plag = prev_lagged_, pscore = prev_scored_;
+        const bool pend = pending_cm_, tail = cm_in_tail_, plag = prev_lagged_, pscore = prev_scored_,
+                   pafold = prev_afold_;
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
-            for (int r = 0; r < n; ++r) issue_round(r, s, comm, true, lagged_);
+            for (int r = 0; r < n; ++r) issue_round(r, s, comm, true, lagged());
         } catch (...) {
             hipGraph_t g;
             hipStreamEndCapture(s, &g);
@@ -334,6 +337,7 @@ class FLEngine {
             cm_in_tail_ = tail;
             prev_lagged_ = plag;
             prev_scored_ = pscore;
+            prev_afold_ = pafold;
             throw;
         }
         HIP_CHECK(hipStreamEndCapture(s, &graph_));
@@ -343,6 +347,7 @@ class FLEngine {
         cm_in_tail_ = tail;
         prev_lagged_ = plag;
         prev_scored_ = pscore;
+        prev_afold_ = pafold;
     }
 
     void replay(uintptr_t stream) {
@@ -351,8 +356,9 @@ class FLEngine {
         HIP_CHECK(hipGraphLaunch(exec_, as_stream(stream)));
         pending_cm_ = fused_;
         cm_in_tail_ = !fused_;
-        prev_lagged_ = lagged_;
-        prev_scored_ = lagged_;
+        prev_lagged_ = lagged();
+        prev_scored_ = lagged();
+        prev_afold_ = lagged() && xchg_;
     }
 
     int graph_rounds() const { return graph_rounds_; }
@@ -362,10 +368,12 @@ class FLEngine {
     // not behind a fused one (whose counts were never computed).
     // A lagged graph must start behind a lagged round (its rounds score their predecessor).
     bool needs_eager_round() const {
-        if (lagged_) return !prev_lagged_;
+        if (lagged()) return !prev_lagged_;
         return fused_ ? cm_in_tail_ : pending_cm_;
     }
-    bool lagged() const { return lagged_; }
+    // Lagged rounds: allowed by the layout, and either no early stopping (metrics may be
+    // folded one round late) or the Adam-fused exchange (which folds them in time).
+    bool lagged() const { return lag_ok_ && (!c_.es_enabled || xchg_); }
     bool adam_exchange() const { return xchg_; }
     bool fused() const { return fused_; }
 
@@ -378,6 +386,7 @@ class FLEngine {
         cm_in_tail_ = false;
         prev_lagged_ = false;
         prev_scored_ = false;
+        prev_afold_ = false;
     }
 
     // Aggregate with the one-shot xGMI all-reduce (peer_allreduce.hip) instead of RCCL: every
@@ -395,7 +404,8 @@ class FLEngine {
         p.prepare_eval((c_.n_rows + c_.R - 1) / c_.R);
         // lagged rounds reduce inside the Adam kernel when the communicator has a chunk-flag
         // table for every Adam block (+ the tail block); one local step per round
-        xchg_ = lagged_ && c_.local_steps == 1 && p.n_chunks() >= (d_.P + 63) / 64 + 1;
+        // (chunks: every Adam block, the tail block and the early lag-region chunk)
+        xchg_ = lag_ok_ && c_.local_steps == 1 && p.n_chunks() >= (d_.P + 63) / 64 + 2;
         std::memset(&pp_, 0, sizeof(pp_));
         if (dtype_ == 1) {
             pp_.pk = b_.pk_global;
@@ -493,7 +503,7 @@ class FLEngine {
         o["tail_stride"] = c_.tail_stride;
         o["tail_len"] = c_.tail_len;
         o["comm_len"] = comm_len_;
-        o["lagged_eval"] = lagged_;
+        o["lagged_eval"] = lagged();
         o["state_bytes"] = (int)sizeof(FLState);
         return o;
     }
@@ -571,9 +581,9 @@ class FLEngine {
     }
     void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
                      hipStream_t s, FLState* st_out = nullptr, int fold = 0, int tail_a = 0,
-                     int fold_mask = FL_FOLD_B, const PeerArgs* xchg = nullptr) {
+                     int fold_mask = FL_FOLD_B, const PeerArgs* peer = nullptr, int wx = 0, int afold = 0) {
         HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr, st_out,
-                                 fold, tail_a, fold_mask, xchg));
+                                 fold, tail_a, fold_mask, peer, wx, afold));
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
@@ -598,14 +608,19 @@ class FLEngine {
         const bool score = !fused && prev_lagged_;
         int mode = (fused && !cm_in_tail_) ? FL_EVAL_FUSED : FL_EVAL_FUSED_SKIP;
         if (score) mode = FL_EVAL_LAGGED;
-        const int mask = fused ? FL_FOLD_B : ((prev_scored_ ? FL_FOLD_A : 0) | (prev_lagged_ ? 0 : FL_FOLD_B));
+        // metrics of the previous round: region B of its all-reduce (it evaluated itself), or
+        // region A one round later (lagged, FedAvg outside Adam); with the Adam-fused exchange
+        // a lagged predecessor is folded inside this Adam kernel from the exchanged region A
+        const bool afold = score && xchg_;  // fold the lagged predecessor in this Adam kernel
+        const int mask = fused ? FL_FOLD_B
+                               : ((prev_scored_ && !prev_afold_ ? FL_FOLD_A : 0) | (prev_lagged_ ? 0 : FL_FOLD_B));
         float* cm_out = score ? b_.cnt : pg + c_.tail_off + c_.rank * c_.tail_stride;
         for (int ls = 0; ls < c_.local_steps; ++ls) {
             const bool first = ls == 0;
             launch_train(pg, first ? si : so, so, ls, s, first ? mode : FL_EVAL_CLASSIC, cm_out, mask);
-            if (first && xchg) {
+            if (first && (xchg || afold)) {
                 const PeerArgs pa = peer_->args((r + 1) & 1, pbuf_[(r + 1) & 1]);
-                launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask, &pa);
+                launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask, &pa, xchg ? 1 : 0, afold ? 1 : 0);
             } else if (first) {
                 launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask);
             }
@@ -614,6 +629,7 @@ class FLEngine {
         pending_cm_ = fused;
         cm_in_tail_ = false;
         prev_scored_ = score;
+        prev_afold_ = afold;
     }
     void issue_eval(int r, hipStream_t s) {
         launch_eval(b_.local, comm_buf(r), st_[(r + 1) & 1], s);
@@ -639,7 +655,7 @@ class FLEngine {
     // `lag`: a lagged round -- no evaluation; the next round's train kernel scores it.
     void issue_round(int r, hipStream_t s, RcclComm* comm, bool allow_fused, bool lag = false) {
         const bool fused = fused_ && allow_fused;
-        lag = lag && lagged_ && !fused;
+        lag = lag && lagged() && !fused;
         if (!fused) flush_pending_eval(r, s);
         const bool xchg = lag && xchg_;
         issue_train(r, s, fused, xchg);
@@ -695,10 +711,11 @@ class FLEngine {
     float* sched_ = nullptr;  // Adam/StepLR scalars per optimizer step
     float* lagbuf_ = nullptr;  // FL_EVAL_LAGGED count + loss carry-over
     long long comm_len_ = 0;   // floats of a comm buffer: image + tails (+ lag region)
-    bool lagged_ = false;      // several clients: evaluation scored one round later (no eval kernel)
+    bool lag_ok_ = false;      // lagged rounds possible (layout, clients, bf16): see lagged()
     bool xchg_ = false;        // lagged rounds: FedAvg inside the Adam kernel (no all-reduce kernel)
     bool prev_lagged_ = false; // the last issued round had no evaluation of its own
     bool prev_scored_ = false; // the last issued round's train kernel scored its predecessor
+    bool prev_afold_ = false;  // ... and its Adam kernel folded that predecessor (exchanged in-kernel)
     bool need_pack_ = true;  // host changed the global weights: repack before the next round
     PeerAllReduce* peer_ = nullptr;  // one-shot xGMI all-reduce (nullptr: RCCL)
     PeerPack pp_;                    // its bf16 pack epilogue (bf16 mode)

@@ -437,43 +437,76 @@ __device__ __forceinline__ void adam_update(const MLPDesc& d, const FLConfig& c,
     if (last_local_step) comm[j] = p * c.agg_scale;
 }
 
+// Chunk ids of the Adam-fused exchange (peer_device.h): the final metric tails, the early lag
+// region A (in-kernel fold of a lagged predecessor), then one per block of 64 parameters.
+#define ADAM_CHUNK_TAIL 0
+#define ADAM_CHUNK_LAG 1
+#define ADAM_CHUNK_W0 2
+
+// Block 0 is the tail block (dispatched first: with the in-kernel fold every other block may
+// wait for its lag chunk); blocks 1.. own 64 dense parameters each.
 __global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
                const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
-               FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, PeerArgs pa, int xchg) {
+               FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, PeerArgs pa, int xchg,
+               int afold) {
     __shared__ float part[ADAM_WAVES][64];
     __shared__ FLState S_sh;
+    __shared__ float lag_s[PEER_MAX_WORLD * (FL_MAX_CLASSES * FL_MAX_CLASSES + 1)];
     const int last_local_step = (local_step == c.local_steps - 1);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nparam_blocks = (d.P + 63) / 64;
+    const unsigned target = st->calls + 1;  // call index of this kernel's exchanges
     // Round state.  Fused evaluation (fl_common.h): wave 0 of EVERY block folds the previous
     // round's tail (anchor = this round's input image) into the previous state and decides
     // whether this round is live -- the same deterministic computation everywhere, so no
     // block waits for another; block 0 publishes it.  Without early stopping the fold cannot
     // change the decision and only block 0 (history) runs it.  Called after the wave issued
-    // its first slab loads, so the fold's double-precision metrics overlap them.
+    // its first slab loads, so the fold's double-precision metrics overlap them.  `afold`: the
+    // previous round was lagged; its metrics are region A of every rank's send buffer,
+    // exchanged right here (chunk ADAM_CHUNK_LAG), so the live decision is taken in time.
     auto round_state = [&]() {
         if (wave != 0) return;
         FLState S0 = *st;
         if (fold) {
-            if (c.es_enabled || blockIdx.x == 0)
+            const bool need = c.es_enabled || blockIdx.x == 0;
+            if (afold) {
+                if (need) {
+                    peer_chunk_wait(pa, ADAM_CHUNK_LAG, target);
+                    for (int i = lane; i < c.tail_len; i += 64) lag_s[i] = peer_pull_sum(pa, c.lag_off + i);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    S0 = fold_round(d, c, b, lag_s, S0.next_round - 1, S0, blockIdx.x == 0);
+                }
+            } else if (need) {
                 S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0, fold_mask);
+            }
             if (lane == 0) {
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
                 if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
-                if (xchg) S0.calls += 1;  // every rank counts its Adam-fused exchanges alike
+                if (xchg || afold) S0.calls += 1;  // every rank counts its exchange calls alike
                 if (blockIdx.x == 0) *st_out = S0;
             }
         }
         if (lane == 0) S_sh = S0;
     };
-    if (blockIdx.x >= nparam_blocks) {
+    if (blockIdx.x == 0) {
         // tail block: this rank's confusion slots are zeroed (the eval pass accumulates
         // into them); its loss slot gets the per-workgroup CE partials, summed in a fixed order
         if (!last_local_step) {
             round_state();
             return;
+        }
+        const int CC = c.tail_stride - 1;
+        if (afold) {
+            // lag region A first -- the previous round's counts (scored by this round's train
+            // kernel) and loss -- published at once: every block of every rank folds from it
+            for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
+                const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
+                comm[c.lag_off + jj] = (k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (wave == 0) peer_chunk_publish(pa, ADAM_CHUNK_LAG, target);
         }
         float lp = 0.f;
         for (int s = threadIdx.x; s < c.n_slabs; s += blockDim.x) lp += b.slab[(size_t)s * c.slab_stride + d.P];
@@ -500,37 +533,39 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             comm[i] = (k == c.rank && e == c.tail_stride - 1) ? loss : 0.f;
         }
         if (c.lag_off > 0) {
-            // lag region A (FL_EVAL_LAGGED): the previous round's counts (scored by this round's
-            // train kernel) and loss, when `tail_a`; then this round's loss is kept for the next
-            // round and the count buffer cleared for the next train kernel
-            const int CC = c.tail_stride - 1;
-            for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
-                const int i = c.lag_off + jj;
-                if (!S.live) {
-                    comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
-                    continue;
+            // lag region A (FL_EVAL_LAGGED, FedAvg outside this kernel): the previous round's
+            // counts and loss when `tail_a`, folded one round later from the all-reduce
+            if (!afold)
+                for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
+                    const int i = c.lag_off + jj;
+                    if (!S.live) {
+                        comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
+                        continue;
+                    }
+                    const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
+                    comm[i] = (tail_a && k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
                 }
-                const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
-                comm[i] = (tail_a && k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
-            }
             __syncthreads();  // every read of cnt / lbuf is done
+            // this round's loss is kept for the next round; the counts cleared for the next
+            // train kernel
             if (S.live) {
                 for (int e = threadIdx.x; e < CC; e += blockDim.x) b.cnt[e] = 0.f;
                 if (threadIdx.x == 0) b.lbuf[0] = loss;
             }
         }
         if (xchg) {
-            // Adam-fused FedAvg of the metric tails (chunk nparam_blocks, peer_device.h)
+            // Adam-fused FedAvg of the metric tails (peer_device.h)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // every wave's tail stores are acknowledged
             if (wave == 0) {
-                peer_chunk_exchange_wait(pa, nparam_blocks, st->calls + 1);
+                peer_chunk_exchange_wait(pa, ADAM_CHUNK_TAIL, target);
                 for (int i = d.Pimg + lane; i < (int)pa.n; i += 64) pa.out[i] = peer_pull_sum(pa, i);
             }
         }
         return;
     }
-    const int di = blockIdx.x * 64 + lane;  // dense index
+    const int pblk = blockIdx.x - 1;
+    const int di = pblk * 64 + lane;  // dense index
     const bool valid = di < d.P;
     // dense index -> image index (and, in bf16 mode, -> packed bf16 LDS-layout position)
     int j = 0, pk = 0;
@@ -594,7 +629,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     if (xchg) {
         // Adam-fused FedAvg of this block's 64 parameters (peer_device.h): publish, wait for
         // every rank's chunk, pull + sum in rank order; global image + packed bf16 image
-        peer_chunk_exchange_wait(pa, blockIdx.x, st->calls + 1);
+        peer_chunk_exchange_wait(pa, ADAM_CHUNK_W0 + pblk, target);
         if (valid) {
             const float gsum = peer_pull_sum(pa, j);
             pa.out[j] = gsum;
@@ -771,20 +806,23 @@ hipError_t fl_launch_train(const MLPDesc& d, const FLConfig& c, const FLBuffers&
 hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
                           const float* anchor, float* comm, const FLState* st, int local_step, hipStream_t s,
                           const MLPDescB* e, FLState* st_out, int fold, int tail_a, int fold_mask,
-                          const PeerArgs* xchg) {
+                          const PeerArgs* peer, int wx, int afold) {
     if (fold && st_out == nullptr) return hipErrorInvalidValue;
-    // the exchange's call index advances in the folded state: fused exchange needs the fold
-    if (xchg != nullptr && (!fold || local_step != c.local_steps - 1 || xchg->n_chunks < (d.P + 63) / 64 + 1))
+    // the exchanges' call index advances in the folded state: an exchange needs the fold
+    if ((wx || afold) &&
+        (peer == nullptr || !fold || local_step != c.local_steps - 1 || peer->n_chunks < (d.P + 63) / 64 + 2 ||
+         (afold && (!tail_a || c.lag_off <= 0))))
         return hipErrorInvalidValue;
     PeerArgs pa;
     PeerArgs zero_pa = {};
     pa = zero_pa;
-    if (xchg != nullptr) pa = *xchg;
+    if (peer != nullptr) pa = *peer;
     const int blocks = (d.P + 63) / 64 + 1;
     MLPDescB ee = {};
     if (e != nullptr) ee = *e;
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
-                       local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask, pa, xchg != nullptr ? 1 : 0);
+                       local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask, pa, wx ? 1 : 0,
+                       afold ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -263,11 +263,14 @@ __device__ __forceinline__ void peer_eval_done(const PeerArgs& a, unsigned targe
 // no separate all-reduce kernel, no kernel boundary between the update and the reduction.
 // Executed by one wave; `target` = the call index (device round state, same on every rank).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void peer_chunk_exchange_wait(const PeerArgs& a, int chunk, unsigned target) {
+__device__ __forceinline__ void peer_chunk_publish(const PeerArgs& a, int chunk, unsigned target) {
     const int lane = threadIdx.x & 63;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's send-buffer stores are done
     if (lane < a.world)
         __hip_atomic_store(a.cflag_dst[lane] + chunk, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void peer_chunk_wait(const PeerArgs& a, int chunk, unsigned target) {
+    const int lane = threadIdx.x & 63;
     if (lane < a.world) {
         const unsigned* f = a.cflags + lane * a.n_chunks + chunk;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -280,6 +283,10 @@ __device__ __forceinline__ void peer_chunk_exchange_wait(const PeerArgs& a, int 
         }
     }
     __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void peer_chunk_exchange_wait(const PeerArgs& a, int chunk, unsigned target) {
+    peer_chunk_publish(a, chunk, target);
+    peer_chunk_wait(a, chunk, target);
 }
 
 // Sum over ranks (rank order) of the send buffers at float position `pos`.

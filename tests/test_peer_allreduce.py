@@ -51,11 +51,15 @@ def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = Tr
     return e.global_flat(), e.history(), np.stack(cms)
 
 
-def _run_early_stop(comm, peer: bool, X, y, flat):
+def _run_early_stop(comm, peer: bool, X, y, flat, lagged: bool = True):
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
     comm.peer_allreduce = peer
-    cfg = EngineConfig(max_rounds=200, patience=4, tolerance=2e-3, dtype="bf16", graph_rounds=8)
+    cfg = EngineConfig(max_rounds=200, patience=4, tolerance=2e-3, dtype="bf16", graph_rounds=8,
+                       lagged_eval=lagged)
     e = HipRoundEngine(X, y, 2, cfg, comm, flat)
+    # with the peer data plane, early stopping runs lagged rounds (metrics exchanged and
+    # folded inside the next round's Adam kernel)
+    assert bool(e.engine.lagged) == (peer and lagged)
     e.run(200)
     return e.global_flat(), e.history()
 
@@ -91,7 +95,8 @@ def _worker(rank, port, q):
             d = _run_engine(comm, True, dtype, X, y, flat, True, False)       # fused eval + all-reduce kernel
             res[dtype] = (a, b, c, d)
         # early stop: rounds past the stop (non-live) must reproduce the stop round's model
-        res["es"] = (_run_early_stop(comm, True, X, y, flat), _run_early_stop(comm, False, X, y, flat))
+        res["es"] = (_run_early_stop(comm, True, X, y, flat), _run_early_stop(comm, False, X, y, flat),
+                     _run_early_stop(comm, True, X, y, flat, lagged=False))
         torch.cuda.synchronize()
         comm.Barrier()
         q.put((rank, res, None))
@@ -127,11 +132,14 @@ def test_peer_allreduce_two_ranks_one_gpu():
             np.testing.assert_array_equal(ha["loss"], hb["loss"])
             np.testing.assert_array_equal(ca, cb)
             assert ha["rounds_run"] == 14
-        (we, he), (wf, hf) = res["es"]
+        (we, he), (wf, hf), (wg, hg) = res["es"]
         assert he["stop_round"] > 0 and he["stop_round"] == hf["stop_round"], (he["stop_round"], hf["stop_round"])
-        assert he["rounds_run"] == hf["rounds_run"]
+        assert he["rounds_run"] == hf["rounds_run"] == hg["rounds_run"]
         np.testing.assert_array_equal(we, wf)
+        np.testing.assert_array_equal(wg, wf)
         np.testing.assert_array_equal(he["global"], hf["global"])
+        np.testing.assert_array_equal(he["loss"], hf["loss"])
+        np.testing.assert_array_equal(hg["global"], hf["global"])
     # both ranks hold the same global model
     for dtype in ("fp32", "bf16"):
         np.testing.assert_array_equal(out[0][1][dtype][0][0], out[1][1][dtype][0][0])

@@ -49,7 +49,7 @@ def main():
         e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=lag)
         h = None
         if ef is not None:
-            h = m.PeerAllReduce(1, 0, 0, int(e.params[0].numel()), 10.0, (e.P + 63) // 64 + 1 if adam_x else 0)
+            h = m.PeerAllReduce(1, 0, 0, int(e.params[0].numel()), 10.0, (e.P + 63) // 64 + 2 if adam_x else 0)
             h.open([h.handle()])
             h.clear()
             e.engine.attach_peer(h)
