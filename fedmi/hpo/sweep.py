@@ -45,14 +45,32 @@ def run_sweep(X_local, y_local, comm, hidden_grid: Sequence = HIDDEN_GRID, lr_gr
     best: Optional[TrialResult] = None
     classes = np.unique(y_local)
     n_cls = max(2, len(classes))
-    for hl in hidden_grid:
-        ests = [MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=max_iter,
-                              random_state=random_state, backend=backend) for lr in lr_grid]
-        if packed:
+    groups = [[MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=max_iter,
+                             random_state=random_state, backend=backend) for lr in lr_grid] for hl in hidden_grid]
+    # Training needs no communication (every trial fits from scratch, Q8): on the GPU the
+    # packed jobs of all hidden configs run concurrently, one host thread + stream each (the
+    # native epoch loop releases the GIL; each job's kernels are far too small to fill the
+    # GPU alone).  Averaging and pooled metrics then follow in the reference's trial order,
+    # so every rank issues its collectives in the same sequence.
+    if packed and groups and groups[0][0]._resolve_backend() == "hip" and len(groups) > 1:
+        import torch
+        from concurrent.futures import ThreadPoolExecutor
+        dev = torch.cuda.current_device()
+
+        def fit_group(ests):
+            torch.cuda.set_device(dev)
+            return fit_packed(ests, X_local, y_local)
+
+        with ThreadPoolExecutor(max_workers=len(groups)) as ex:
+            list(ex.map(fit_group, groups))
+    elif packed:
+        for ests in groups:
             fit_packed(ests, X_local, y_local)
-        else:
+    else:
+        for ests in groups:
             for e in ests:
                 e.fit(X_local, y_local)
+    for hl, ests in zip(hidden_grid, groups):
         for lr, est in zip(lr_grid, ests):
             y_pred = est.predict(X_local)
             local = metrics_from_confusion(confusion_matrix(y_local, y_pred, n_cls))

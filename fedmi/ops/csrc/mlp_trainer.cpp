@@ -339,7 +339,7 @@ void register_trainer(py::module_& m) {
     py::class_<MLPTrainer>(m, "MLPTrainer")
         .def(py::init<std::vector<int>, int, py::dict, py::dict>())
         .def("run", &MLPTrainer::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
-             py::arg("use_graph") = true)
+             py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
         .def("predict_logits", &MLPTrainer::predict_logits)
         .def_property_readonly("P", &MLPTrainer::P);
     m.def("gemm", &gemm_py);

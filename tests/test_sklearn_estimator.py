@@ -111,3 +111,25 @@ def test_hip_packed_equals_single(data):
     for u, v in zip(single.coefs_, packed[1].coefs_):
         np.testing.assert_allclose(u, v, rtol=1e-6, atol=1e-7)
     assert packed[1].n_iter_ == single.n_iter_
+
+
+@pytest.mark.gpu
+def test_hip_sweep_concurrent_groups_equal_sequential():
+    """run_sweep trains the packed jobs of all hidden configs concurrently (threads + streams):
+    results equal the same jobs fitted one after another."""
+    from fedmi.hpo.sweep import run_sweep
+    from fedmi.models.sklearn_mlp import MLPClassifier, fit_packed
+    from fedmi.data.synthetic import make_income_like
+    X, y = make_income_like(1200, seed=3)
+    hidden, lrs = [(16,), (12, 8), (20, 6)], [0.004, 0.02]
+    best, res = run_sweep(X, y, None, hidden, lrs, max_iter=15, backend="hip")
+    assert len(res) == 6
+    for i, hl in enumerate(hidden):
+        ests = [MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=15, random_state=42,
+                              backend="hip") for lr in lrs]
+        fit_packed(ests, X, y)
+        for j, e in enumerate(ests):
+            r = res[i * len(lrs) + j]
+            assert r.hidden == tuple(hl) and r.lr == lrs[j] and r.n_iter == e.n_iter_
+            for a, b in zip(r.weights, list(e.coefs_) + list(e.intercepts_)):
+                np.testing.assert_array_equal(a, b)
