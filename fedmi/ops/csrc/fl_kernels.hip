@@ -1,23 +1,29 @@
 // Fused federated-round kernels for gfx950 (MI355X / CDNA4).
 //
 // The reference round (FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:130-201)
-// is ~20 ATen launches + 6 H2D/D2H copies + pickled MPI gather/bcast per round.  Here a
-// round is three kernels and one all-reduce on one stream:
+// is ~20 ATen launches + 6 H2D/D2H copies + pickled MPI gather/bcast per round.  Here the
+// classic round is three kernels and one all-reduce on one stream:
 //
-//   fl_train  : finalize(prev round metrics, early stop) ; per-workgroup fwd + CE + bwd
-//               over R rows with the parameter image AND activations in LDS; dense
-//               weight-gradient partials -> slab row              (K2-K17)
-//   fl_adam   : wide deterministic slab reduction (16 waves per 64 parameters) + Adam
+//   fl_train  : per-workgroup fwd + CE + bwd over R rows with the parameter image AND
+//               activations in LDS; dense weight-gradient partials -> slab row (non-temporal)
+//                                                                  (K2-K17)
+//   fl_adam   : fold of the previous round's metrics (history, early stop, live decision);
+//               wide deterministic slab reduction (16 waves per 64 parameters) + Adam
 //               (+L2, +FedProx) + StepLR; writes the local image and the pre-scaled (n_i/N)
 //               FedAvg contribution                                (K18, K22)
 //   fl_eval   : forward of the post-step local model on the local shard, argmax and the
 //               C x C confusion matrix into this rank's tail slot  (K20, Q2)
-//   allreduce : one RCCL SUM over [image*n_i/N | per-rank tails] = gather + average +
-//               bcast of weights, sizes, metrics and stop signal in one collective (§2.4)
+//   allreduce : one SUM over [image*n_i/N | per-rank tails] = gather + average + bcast of
+//               weights, sizes, metrics and stop signal in one collective (§2.4)
+//
+// and the steady-state rounds are TWO kernels (fl_common.h FL_EVAL_*): with one client the
+// train kernel scores the previous round's model from its own forward pass; with several
+// the bf16 train kernel scores it with a second forward pass (lagged) and the FedAvg runs
+// inside fl_adam (one-shot xGMI chunk exchange, peer_device.h).
 //
 // GEMM-shaped work runs on the f32-input MFMA (v_mfma_f32_16x16x4_f32: exact f32 fma chain;
 // the reference trains in fp32).  Work items are 16-wide column tiles spread over the 8
-// waves of a 512-thread workgroup; a wave keeps one accumulator per 16-row tile so a B
+// waves of a 1024-thread workgroup (fl_device.h FL_THREADS); a wave keeps one accumulator per 16-row tile so a B
 // fragment is read once per k and reused RT times, and the next 16-deep k chunk is loaded
 // while the current one is multiplied.  The skinny classifier head (C outputs) runs on the
 // VALU with a fixed-order split-K shuffle reduction.

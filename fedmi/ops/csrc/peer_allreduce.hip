@@ -23,6 +23,11 @@
 //     entered call s + 1, i.e. finished reading call s;
 //   * every wait is bounded (s_memrealtime): on a timeout the kernel sets a sticky error word
 //     instead of hanging the GPU, and the host checks it at each synchronisation point.
+//
+// The same allocation carries a chunk-flag table for the round engine's Adam-fused exchange
+// (peer_device.h): there the call index comes from the device round state and every Adam
+// block publishes / waits for / pulls its own 64-parameter chunk.  Start-up self-tests both
+// protocols on a known payload (fedmi/parallel/peer.py) before the engine may use them.
 #include "peer_allreduce.h"
 
 #include <pybind11/stl.h>
