@@ -22,9 +22,10 @@
 // inside fl_adam (one-shot xGMI chunk exchange, peer_device.h).
 //
 // GEMM-shaped work runs on the f32-input MFMA (v_mfma_f32_16x16x4_f32: exact f32 fma chain;
-// the reference trains in fp32).  Work items are 16-wide column tiles spread over the 8
-// waves of a 1024-thread workgroup (fl_device.h FL_THREADS); a wave keeps one accumulator per 16-row tile so a B
-// fragment is read once per k and reused RT times, and the next 16-deep k chunk is loaded
+// the reference trains in fp32).  Work items are 16-wide column tiles spread over the 16
+// waves of a 1024-thread workgroup (fl_device.h FL_THREADS); a wave keeps one accumulator
+// per 16-row tile so a B fragment is read once per k and reused RT times, and the next
+// 16-deep k chunk is loaded
 // while the current one is multiplied.  The skinny classifier head (C outputs) runs on the
 // VALU with a fixed-order split-K shuffle reduction.
 #include "fl_common.h"
