@@ -408,24 +408,23 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
 #define ADAM_WAVES 16
 #define ADAM_DEPTH 16
 // Adam step of one parameter (wave 0 lane of fl_adam_kernel) from the block's partial sums.
-__device__ __forceinline__ void adam_update(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
-                                            const MLPDescB& e, const float* __restrict__ pin,
-                                            const float* __restrict__ anchor, float* __restrict__ comm,
+// `p`, `m`, `v`, `anc`: the parameter, its Adam moments and its anchor value, loaded by the
+// caller at the start of the kernel (their latency hides behind the slab loads).
+__device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& b, float* __restrict__ comm,
                                             const FLState& S, int local_step, int last_local_step, int pack, int j,
-                                            int pk, bool is_bias, float (*part)[64], int lane) {
+                                            int pk, bool is_bias, float (*part)[64], int lane, float p, float m,
+                                            float v, float anc) {
     float g = 0.f;
 #pragma unroll
     for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
-    float p = pin[j];
     if (c.weight_decay != 0.f) g += c.weight_decay * p;
-    if (c.prox_mu != 0.f) g += c.prox_mu * (p - anchor[j]);
+    if (c.prox_mu != 0.f) g += c.prox_mu * (p - anc);
     // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
     // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
     // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
     const int t = S.cur_round * c.local_steps + local_step + 1;
     const float step_size = b.sched[2 * (t - 1)];
     const float bc2_sqrt = b.sched[2 * (t - 1) + 1];
-    float m = b.m[j], v = b.v[j];
     m = m + c.omb1 * (g - m);
     v = v * c.beta2f + c.omb2 * g * g;
     const float denom = sqrtf(v) / bc2_sqrt + c.eps;
@@ -485,7 +484,9 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
                     S0 = fold_round(d, c, b, lag_s, S0.next_round - 1, S0, blockIdx.x == 0);
                 }
             } else if (need) {
+#ifndef FL_DIAG_NO_FOLD
                 S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0, fold_mask);
+#endif
             }
             if (lane == 0) {
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
@@ -515,9 +516,11 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             __syncthreads();
             if (wave == 0) peer_chunk_publish(pa, ADAM_CHUNK_LAG, target);
         }
-        float lp = 0.f;
-        for (int s = threadIdx.x; s < c.n_slabs; s += blockDim.x) lp += b.slab[(size_t)s * c.slab_stride + d.P];
+        // first batch of loss loads in flight before the fold (one per thread up to 1024 slabs)
+        const int s0 = threadIdx.x;
+        float lp = s0 < c.n_slabs ? b.slab[(size_t)s0 * c.slab_stride + d.P] : 0.f;
         round_state();
+        for (int s = s0 + blockDim.x; s < c.n_slabs; s += blockDim.x) lp += b.slab[(size_t)s * c.slab_stride + d.P];
         part[wave][lane] = lp;
         lds_barrier();
         const FLState S = S_sh;
@@ -599,6 +602,14 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         if (wave == 0 && valid && last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
         return;
     }
+    // wave 0's operands of the update, issued before the slab loads so their latency overlaps
+    float p0 = 0.f, m0 = 0.f, v0 = 0.f, a0 = 0.f;
+    if (wave == 0 && valid) {
+        p0 = pin[j];
+        m0 = b.m[j];
+        v0 = b.v[j];
+        a0 = anchor[j];
+    }
     float g = 0.f;
     bool have_state = false;
     {
@@ -609,7 +620,11 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             for (int u = 0; u < ADAM_DEPTH; ++u) {
                 const int s = s0 + u * ADAM_WAVES;
                 // unpredicated; non-temporal: the slab is read once
+#ifndef FL_DIAG_NO_SLAB_READ
                 const float v = __builtin_nontemporal_load(&sp[(size_t)(s < c.n_slabs ? s : 0) * c.slab_stride]);
+#else
+                const float v = (float)s * 1e-30f;
+#endif
                 x[u] = s < c.n_slabs ? v : 0.f;
             }
             if (!have_state) {
@@ -627,10 +642,10 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     const FLState S = S_sh;
     if (valid) {
         if (!S.live) {
-            if (last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
+            if (last_local_step) comm[j] = (c.rank == 0) ? a0 : 0.f;
         } else {
-            adam_update(d, c, b, e, pin, anchor, comm, S, local_step, last_local_step, pack, j, pk, is_bias,
-                        part, lane);
+            adam_update(c, b, comm, S, local_step, last_local_step, pack, j, pk, is_bias, part, lane, p0, m0, v0,
+                        a0);
         }
     }
     if (xchg) {

@@ -30,11 +30,12 @@ def _free_port():
     return p
 
 
-def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = True, lagged: bool = True):
+def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = True, lagged: bool = True,
+                hidden=(50, 200)):
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
     comm.peer_allreduce = peer
-    cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4, eval_fedavg=eval_fedavg,
-                       lagged_eval=lagged)
+    cfg = EngineConfig(hidden=tuple(hidden), max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4,
+                       eval_fedavg=eval_fedavg, lagged_eval=lagged)
     e = HipRoundEngine(X, y, 2, cfg, comm, flat)
     lag = lagged and dtype == "bf16"
     assert e.aggregation == (("xgmi-oneshot+adam" if lag else "xgmi-oneshot") if peer else "host"), e.aggregation
@@ -164,11 +165,14 @@ def _worker4(rank, world, port, q):
         if h is not None:
             h.close()
         X, y = make_income_like(900 + 100 * rank, seed=30 + rank)   # unequal shards: n_i / N weights
-        flat = init_flat([14, 50, 200, 2], 5)
-        a = _run_engine(comm, True, "bf16", X, y, flat)
+        # a small model: the Adam blocks of all four ranks must be resident on the ONE shared GPU
+        # at once (each waits for the others' chunks; on separate GPUs that always holds)
+        hidden = (24, 12)
+        flat = init_flat([14, *hidden, 2], 5)
+        a = _run_engine(comm, True, "bf16", X, y, flat, hidden=hidden)
         # classic rounds over the standalone peer kernel: the same rank-order sums (gloo's
         # 4-rank reduction order differs, so the host path is not a bitwise reference here)
-        b = _run_engine(comm, True, "bf16", X, y, flat, True, False)
+        b = _run_engine(comm, True, "bf16", X, y, flat, True, False, hidden=hidden)
         torch.cuda.synchronize()
         comm.Barrier()
         q.put((rank, (ok, a, b), None))
