@@ -40,11 +40,15 @@ def main():
     cases = (("world 1, fused evaluation", True, None, False, 0), ("eval + one-shot all-reduce", False, False, False, 0),
              ("fused eval + FedAvg kernel", False, True, False, 0),
              ("lagged eval + all-reduce kernel", False, True, True, 0),
-             ("lagged eval + FedAvg in Adam", False, True, True, 1))
+             ("lagged eval + FedAvg in Adam", False, True, True, 1),
+             ("same + early stopping (LAG fold)", False, True, True, 2))
     for name, fused, ef, lag, adam_x in cases:
         if lag and a.dtype != "bf16":
             continue
-        cfg = EngineConfig(max_rounds=a.rounds + 256, early_stop=False, dtype=a.dtype, graph_rounds=16,
+        # adam_x == 2: early stopping on (patience never reached), so every round's Adam blocks
+        # wait for the lagged-metric chunk of the round before (N > 1 with early stopping)
+        cfg = EngineConfig(max_rounds=a.rounds + 256, early_stop=adam_x == 2, patience=10 ** 6,
+                           dtype=a.dtype, graph_rounds=16,
                            fused_eval=fused, eval_fedavg=bool(ef), lagged_eval=lag)
         e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=lag)
         h = None
