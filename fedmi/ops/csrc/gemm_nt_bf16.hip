@@ -157,11 +157,203 @@ gemm_nt_bf16_kernel(NTArgs g) {
     }
 }
 
-static int g_nt_variant = 1;
+// ---------------------------------------------------------------------------------------------
+// 256x256 ping-pong variant (variant 2; M % 256 == N % 256 == 0, K % 64 == 0, K >= 128).
+//
+// 512 threads = 8 waves as 2 (M) x 4 (N), 128x64 outputs per wave (8x4 16x16 tiles, 128 fp32
+// accumulators per lane).  A K-tile (BK = 64) is computed in four PHASES of 16 MFMAs each:
+//     r = 0: rows m0 (first 64 of the wave's 128) x k 0..31     r = 1: rows m1 x k 0..31
+//     r = 2: rows m1 x k 32..63                                r = 3: rows m0 x k 32..63
+// LDS holds two K-tiles (2 x 64 KiB, one __shared__ array), each as k-halves [ks][256][32] of
+// 64-byte rows with the 16-byte chunk index XOR-ed with (row >> 2) & 2: a ds_read_b128 is
+// serviced in four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32), and with this
+// swizzle each group's 16 (row, chunk) pairs hit 16 distinct 16-byte bank slots (a plain
+// (row >> 2) & 3 XOR leaves them 2-way conflicted).  A K-tile is 8 LDS-DMAs per lane (8 KiB
+// per block each), numbered in first-read order: d0 A m0 ks0 | d1,d2 B ks0 | d3 A m1 ks0 |
+// d4 A m1 ks1 | d5,d6 B ks1 | d7 A m0 ks1  (first read in phases 0,0,0,1,2,2,2,3).
+//
+// Schedule, global phase g = 4 * tile + r, each wave:
+//     MEM(g):  2 LDS-DMAs (r = 0: tile+1 d4,d5 | 1: tile+1 d6,d7 | 2: tile+2 d0,d1 |
+//              3: tile+2 d2,d3 -- every slot restaged >= 2 phases after its last read, and
+//              4-6 phases before its first), ds_read phase g's fragments, then
+//              s_waitcnt vmcnt(N) retiring every DMA first read in phase g + 1
+//              (N = DMAs still needed later: 10 for even r, 9 for odd r)
+//     s_barrier; s_waitcnt lgkmcnt(0); 16 MFMAs; s_barrier
+// The second wave row starts one barrier later, so on every SIMD one wave's MFMA cluster runs
+// while the other wave's MEM section (DMA issue, LDS reads, vmcnt wait) runs.  A DMA's data is
+// read at least one barrier after every wave's vmcnt that retires it (group 0: the barrier
+// after the wait; group 1: one barrier later still); a slot is restaged two phases after its
+// last read, i.e. after a barrier that follows every reader's lgkmcnt(0).  The last two
+// K-tiles issue nothing past the end and drain with vmcnt(0).
+#define NT2_BM 256
+#define NT2_THREADS 512
+
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__global__ void __launch_bounds__(NT2_THREADS)
+gemm_nt_bf16_pp_kernel(NTArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
+    const int mt = g.M / NT2_BM, nt = g.N / NT2_BM;
+    const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
+    // grouped tile order: the ~32 blocks an XCD runs at once (consecutive bids after the XCD
+    // remap) cover 8 m-tiles x 4 n-tiles, so each K-slice of A and B is fetched into that XCD's
+    // L2 once per 12 panels instead of once per 33 (m-major order)
+    constexpr int GM = 8;
+    const int grp = bid / (GM * nt), first_m = grp * GM;
+    const int gsz = min(mt - first_m, GM);
+    const int in_grp = bid - grp * GM * nt;
+    const int m0 = (first_m + in_grp % gsz) * NT2_BM, n0 = (in_grp / gsz) * NT2_BM;
+    const __hip_bfloat16* A = reinterpret_cast<const __hip_bfloat16*>(g.A);
+    const __hip_bfloat16* B = reinterpret_cast<const __hip_bfloat16*>(g.B);
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63;
+    const int wr = w >> 2, wc = w & 3;
+    const int lr = l & 15, lg = l >> 4;
+
+    // DMA sources: lane l of wave w fills LDS row (16-row group base) + l/4, physical chunk l%4
+    // = logical chunk (l%4) ^ (((row>>2)&3) & 2) of the row's 64-byte k-half.
+    const int dchunk = ((l & 3) ^ ((l >> 4) & 2)) * 8;
+    const __hip_bfloat16* srcA[2];
+    const __hip_bfloat16* srcB[2];
+    int dstA[2], dstB[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int ra = (w >> 2) * 128 + h * 64 + (w & 3) * 16;  // A piece m-half h
+        srcA[h] = A + (size_t)(m0 + ra + (l >> 2)) * g.lda + dchunk;
+        dstA[h] = ra * 64;
+        const int rb = h * 128 + w * 16;                         // B piece, DMA h of 2
+        srcB[h] = B + (size_t)(n0 + rb + (l >> 2)) * g.ldb + dchunk;
+        dstB[h] = 32768 + rb * 64;
+    }
+    // LDS-DMA d (0..7) of K-tile `tile`, in first-read order: d0 A m0 ks0, d1-d2 B ks0, d3 A m1
+    // ks0, d4 A m1 ks1, d5-d6 B ks1, d7 A m0 ks1 (first read in phases 0,0,0,1,2,2,2,3)
+    auto dma = [&](int tile, int d) {
+        const int ks = (d >= 4) ? 1 : 0;
+        const int k = tile * 64 + ks * 32;
+        char* base = smem + (tile & 1) * 65536 + ks * 16384;
+        if (d == 0 || d == 7) glds16(srcA[0] + k, base + dstA[0]);
+        else if (d == 3 || d == 4) glds16(srcA[1] + k, base + dstA[1]);
+        else if (d == 1 || d == 5) glds16(srcB[0] + k, base + dstB[0]);
+        else glds16(srcB[1] + k, base + dstB[1]);
+    };
+
+    // fragment read offset of this lane inside a 16-row group: row lr, chunk lg swizzled
+    const int foff = lr * 64 + ((lg ^ ((lr >> 2) & 2)) << 4);
+    const int aoff = wr * 128 * 64 + foff, boff = 32768 + wc * 64 * 64 + foff;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[4], bfr[4];
+
+    const int KT = g.K / 64;
+    // prologue: what phases -6 .. -1 would have issued (tile 0, then tile 1's d0-d3); retire
+    // phase 0's DMAs (tile 0 d0-d2), leaving 5 + 4 = 9 in flight
+    dma(0, 0); dma(0, 1); dma(0, 2); dma(0, 3); dma(0, 4); dma(0, 5); dma(0, 6); dma(0, 7);
+    if (KT > 1) { dma(1, 0); dma(1, 1); dma(1, 2); dma(1, 3); }
+    if (KT > 2) vm_wait<9>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+
+    auto phase = [&](int q, int r, bool tail) {
+        const char* buf = smem + ((q >> 2) & 1) * 65536 + ((r >= 2) ? 16384 : 0);
+        const int mh = (r == 1 || r == 2) ? 1 : 0;
+        // two DMAs per phase: r = 0: tile+1 d4,d5; r = 1: tile+1 d6,d7; r = 2: tile+2 d0,d1;
+        // r = 3: tile+2 d2,d3 (each slot restaged >= 2 phases after its last read)
+        {
+            const int tile = (q >> 2) + (r < 2 ? 1 : 2);
+            const int d = (r < 2) ? 4 + 2 * r : 2 * (r - 2);
+            if (!tail || tile < KT) { dma(tile, d); dma(tile, d + 1); }
+        }
+        if ((r & 1) == 0) {
+#pragma unroll
+            for (int y = 0; y < 4; ++y) bfr[y] = *reinterpret_cast<const bf16x8*>(buf + boff + y * 16 * 64);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+            af[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + (mh * 64 + x * 16) * 64);
+        if (tail) vm_wait<0>();
+        else if ((r & 1) == 0) vm_wait<10>();
+        else vm_wait<9>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+                acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr[y], acc[mh * 4 + x][y], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+    };
+
+    int kt = 0;
+    for (; kt + 2 < KT; ++kt) {
+        phase(4 * kt + 0, 0, false);
+        phase(4 * kt + 1, 1, false);
+        phase(4 * kt + 2, 2, false);
+        phase(4 * kt + 3, 3, false);
+    }
+    for (; kt < KT; ++kt) {
+        phase(4 * kt + 0, 0, true);
+        phase(4 * kt + 1, 1, true);
+        phase(4 * kt + 2, 2, true);
+        phase(4 * kt + 3, 3, true);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
+
+    __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
+    __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        const int n = n0 + wc * 64 + 16 * y + lr;
+        const float bv = g.bias != nullptr ? g.bias[n] : 0.f;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) {
+            uint32_t tp[2];  // the lane's 4 consecutive rows of column n, packed for CbT
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int mm = m0 + wr * 128 + 16 * x + 4 * lg + j;
+                float v = acc[x][y][j] * g.alpha + bv;
+                if (g.relu) v = fmaxf(v, 0.f);
+                if (g.mask != nullptr) {
+                    const __hip_bfloat16 mk = reinterpret_cast<const __hip_bfloat16*>(g.mask)[(size_t)mm * g.ldmask + n];
+                    v = __bfloat162float(mk) > 0.f ? v : 0.f;
+                }
+                if (g.C != nullptr) {
+                    float* cp = g.C + (size_t)mm * g.ldc + n;
+                    if (g.beta != 0.f) v += g.beta * *cp;
+                    *cp = v;
+                }
+                const __hip_bfloat16 hv = __float2bfloat16(v);
+                if (Cb != nullptr) Cb[(size_t)mm * g.ldcb + n] = hv;
+                const uint32_t hb = __bfloat16_as_ushort(hv);
+                if (j & 1) tp[j >> 1] |= hb << 16;
+                else tp[j >> 1] = hb;
+            }
+            if (CbT != nullptr) {  // 8-byte store: rows mm .. mm+3 are contiguous in CbT's row n
+                const size_t off = (size_t)n * g.ldct + m0 + wr * 128 + 16 * x + 4 * lg;
+                *reinterpret_cast<uint2*>(CbT + off) = make_uint2(tp[0], tp[1]);
+            }
+        }
+    }
+}
+
+static int g_nt_variant = 2;
 void gemm_nt_set_variant(int v) { g_nt_variant = v; }
 
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
     if (g.M % NT_BM || g.N % NT_BN || g.K % NT_BK || g.lda % 8 || g.ldb % 8) return hipErrorInvalidValue;
+    if (g_nt_variant == 2 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 && g.K >= 128 &&
+        (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0))) {
+        const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
+        hipLaunchKernelGGL(gemm_nt_bf16_pp_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
+        return hipGetLastError();
+    }
     const int blocks = (g.M / NT_BM) * (g.N / NT_BN);
     if (g_nt_variant == 0)
         hipLaunchKernelGGL(gemm_nt_bf16_kernel<0>, dim3(blocks), dim3(NT_THREADS), 0, s, g);

@@ -220,6 +220,39 @@ def test_gemm_nt_bf16_epilogues():
     assert ((C - r2).abs().max() / r2.abs().max()).item() < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,pad", [(256, 256, 128, 0), (512, 768, 192, 64), (768, 512, 1024, 0),
+                                       (2048, 1024, 4096, 8)])
+def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
+    """The 256x256 ping-pong main loop (variant 2) against the 128x128 loop (variant 1): same
+    per-element k order, so bit-identical, and both against an fp32 torch reference; row
+    strides wider than K exercise the DMA source addressing."""
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(K)
+    A = torch.randn(M, K + pad, device=dev).to(torch.bfloat16)
+    B = torch.randn(N, K + pad, device=dev).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    outs = []
+    try:
+        for v in (1, 2):
+            m.gemm_nt_set_variant(v)
+            Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            CbT = torch.empty(N, M, dtype=torch.bfloat16, device=dev)
+            C = torch.empty(M, N, device=dev)
+            m.gemm_nt(M, N, K, A.data_ptr(), K + pad, B.data_ptr(), K + pad, C.data_ptr(), N, Cb.data_ptr(), N,
+                      CbT.data_ptr(), M, bias.data_ptr(), 0, 0, 1, 1.0, 0.0, s)
+            torch.cuda.synchronize()
+            outs.append((C, Cb))
+            assert torch.equal(CbT, Cb.t())
+    finally:
+        m.gemm_nt_set_variant(2)
+    ref = (A[:, :K].float() @ B[:, :K].float().t() + bias).clamp_min(0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert ((outs[1][0] - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
 def test_rowsum_and_transpose_bf16():
     m = native()
     dev = torch.device("cuda", 0)
