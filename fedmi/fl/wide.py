@@ -74,6 +74,10 @@ class WideClient:
         self.xq = torch.empty(mb, dims[0], dtype=gdt, device=dev)
         self.scratch = torch.empty(mb * max(dims[1:]), **f32)  # fp32 epilogue target of the generic GEMM
         self.logits = torch.empty(mb, dims[-1], **f32)
+        # split-K slabs of the two skinny weight gradients (layer 0: [H1][14], head: [C][H_last]),
+        # whose 64x64 output tiles alone would leave all but ~64 CUs idle over a long contraction
+        self.wg_splits = max(1, min(16, mb // 1024))
+        self.wg_slab = torch.empty(self.wg_splits * max(dims[0] * dims[1], dims[-1] * dims[-2]), **f32)
         self.dz_out = torch.empty(mb, dims[-1], **f32)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         self.round = 0
@@ -150,6 +154,10 @@ class WideClient:
                     hq[:rows].copy_(self.scratch[:rows * N].view(rows, N))
             inp = hq
 
+    def _wg_split(self, rows: int) -> int:
+        """K-split count of a skinny weight gradient over `rows` contraction rows (>= 1024 rows per split)."""
+        return max(1, min(self.wg_splits, rows // 1024))
+
     def _backward(self, r0: int, rows: int, beta: float):
         m, s, mb, L = self.m, self._s(), self.mb, self.L
         C = self.dims[-1]
@@ -162,7 +170,7 @@ class WideClient:
             dzo[:rows].copy_(self.dz_out[:rows])
         h_in = self.hq[L - 2] if L >= 2 else (self.xq if self.dtype else self.X[r0:r0 + rows])
         m.gemm(C, K, rows, dzo.data_ptr(), C, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0, 0,
-               1.0, beta, self.dtype, 1, 0, 0, s)
+               1.0, beta, self.dtype, self._wg_split(rows), self.wg_slab.data_ptr(), 0, s)
         m.colsum(self.dz_out.data_ptr(), rows, C, C, self.gb[L - 1].data_ptr(), beta, s)
         if L >= 2:
             # dgrad into the last hidden layer (K = C: bandwidth-bound), ReLU-masked
@@ -188,7 +196,7 @@ class WideClient:
                 self.nt_calls += 1
             else:
                 m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), K, 0, self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0,
-                       1.0, beta, self.dtype, 1, 0, 0, s)
+                       1.0, beta, self.dtype, self._wg_split(rows) if l == 0 else 1, self.wg_slab.data_ptr(), 0, s)
             if self.dtype and rows % 8 == 0 and mb % 8 == 0:
                 m.rowsum_bf16(self.dzT[l].data_ptr(), N, rows, mb, self.gb[l].data_ptr(), beta, s)
             else:

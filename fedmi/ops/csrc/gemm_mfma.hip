@@ -300,8 +300,32 @@ hipError_t splitk_reduce_launch(const float* slab, size_t stride, int splits, fl
     return hipGetLastError();
 }
 
+// Column sums of a contiguous [M][N] matrix with few columns (N <= 64, e.g. the logits-head
+// bias gradient): thread t < S = 1024 - 1024 % N reads the flat elements t, t + S, ... (all in
+// column t % N, coalesced across the block), then column n folds the partials t = n, n + N, ...
+// in fixed order.
+__global__ void __launch_bounds__(1024) colsum_flat_kernel(const float* __restrict__ X, size_t total, int N,
+                                                           float* __restrict__ out, float beta) {
+    __shared__ float part[1024];
+    const int t = threadIdx.x, S = 1024 - 1024 % N;
+    float acc = 0.f;
+    if (t < S)
+        for (size_t e = t; e < total; e += S) acc += X[e];
+    part[t] = acc;
+    __syncthreads();
+    if (t < N) {
+        float v = 0.f;
+        for (int i = t; i < S; i += N) v += part[i];
+        out[t] = (beta != 0.f ? beta * out[t] : 0.f) + v;
+    }
+}
+
 hipError_t colsum_launch(const float* X, int M, int N, int ld, float* out, float beta, int batch, long long sX,
                          long long sOut, const int* active, hipStream_t s) {
+    if (N <= 64 && ld == N && batch == 1 && active == nullptr && (size_t)M * N >= 4096) {
+        hipLaunchKernelGGL(colsum_flat_kernel, dim3(1), dim3(1024), 0, s, X, (size_t)M * N, N, out, beta);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, batch), dim3(1024), 0, s, X, M, N, ld, out, beta, sX, sOut,
                        active);
     return hipGetLastError();

@@ -167,12 +167,14 @@ def test_layered_gemm_variants(dtype):
             assert ((C - ref).abs().max() / ref.abs().max()).item() < tol
 
 
-def test_wide_client_fp32_matches_torch():
+@pytest.mark.parametrize("rows,mb", [(1500, 512), (4500, 4096)])
+def test_wide_client_fp32_matches_torch(rows, mb):
+    """Five fp32 rounds vs torch; mb = 4096 runs the skinny weight gradients split-K (4 slabs)."""
     from fedmi.fl.wide import WideClient
     dev = torch.device("cuda", 0)
-    X, y = make_income_like(1500, seed=0)
+    X, y = make_income_like(rows, seed=0)
     Xt, yt = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
-    c = WideClient(Xt, yt, [14, 64, 48, 2], micro_batch=512, dtype="fp32")
+    c = WideClient(Xt, yt, [14, 64, 48, 2], micro_batch=mb, dtype="fp32")
     ref = torch.nn.Sequential(torch.nn.Linear(14, 64), torch.nn.ReLU(), torch.nn.Linear(64, 48), torch.nn.ReLU(),
                               torch.nn.Linear(48, 2)).to(dev)
     with torch.no_grad():
@@ -251,6 +253,20 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
     assert ((outs[1][0] - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("M,N,beta", [(16384, 2, 0.0), (5000, 14, 1.0), (300, 50, 0.5), (700, 100, 1.0)])
+def test_colsum_vs_torch(M, N, beta):
+    """Bias-gradient column sums (flat few-column kernel for N <= 64, wave-per-64-columns otherwise)."""
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    X = torch.randn(M, N, device=dev)
+    out = torch.randn(N, device=dev)
+    ref = X.double().sum(dim=0) + beta * out.double()
+    m.colsum(X.data_ptr(), M, N, N, out.data_ptr(), beta, s)
+    torch.cuda.synchronize()
+    assert (out.double() - ref).abs().max().item() < 1e-3
 
 
 def test_rowsum_and_transpose_bf16():
