@@ -87,6 +87,16 @@ class WideClient:
         # transposed (k = rows) operands need 16-byte aligned rows of the micro-batch buffers
         self._t_ok = bool(self.dtype) and mb % 128 == 0
         self._bucket_ev: List[Optional[torch.cuda.Event]] = [None] * self.L  # pending FedAvg buckets
+        # K-padded (to 64, zeros) operands so the layer-0 forward (K = 14 features) and the head's
+        # dgrad (K = C classes) also run on the NT GEMM with fused epilogues + transposed outputs
+        KP = 64
+        self._pad = (self._t_ok and self.L >= 2 and dims[0] <= KP and dims[-1] <= KP
+                     and self._nt_ok(mb, dims[1], KP) and self._nt_ok(mb, dims[-2], KP))
+        if self._pad:
+            self.xp = torch.empty(mb, KP, dtype=gdt, device=dev)        # bf16 X, zero-padded
+            self.W0p = torch.empty(dims[1], KP, dtype=gdt, device=dev)   # bf16 W0, zero-padded
+            self.dzp = torch.empty(mb, KP, dtype=gdt, device=dev)       # bf16 head delta, padded
+            self.WhTp = torch.empty(dims[-2], KP, dtype=gdt, device=dev)  # bf16 head W^T, padded
         self._quantize()
 
     # ------------------------------------------------------------------
@@ -99,6 +109,12 @@ class WideClient:
         with torch.cuda.stream(stream):
             if self.dtype:
                 self.m.to_bf16(w.data_ptr(), q.data_ptr(), w.numel(), stream.cuda_stream)
+                if getattr(self, "_pad", False):
+                    N, K = w.shape
+                    if l == 0:
+                        self.m.pad_bf16(w.data_ptr(), N, K, K, 1, self.W0p.data_ptr(), 64, stream.cuda_stream)
+                    if l == self.L - 1:  # head W [C][H] -> W^T [H][64]
+                        self.m.pad_bf16(w.data_ptr(), K, N, 1, K, self.WhTp.data_ptr(), 64, stream.cuda_stream)
                 if self.WqT[l] is not None:
                     N, K = w.shape
                     self.m.transpose_bf16(w.data_ptr(), N, K, K, self.WqT[l].data_ptr(), N, stream.cuda_stream)
@@ -125,7 +141,11 @@ class WideClient:
         operand, ReLU mask) and, when training, bf16 transposed (wgrad B operand)."""
         m, s, mb = self.m, self._s(), self.mb
         x = self.X[r0:r0 + rows]
-        if self.dtype:
+        pad = self._pad and rows % 128 == 0
+        if pad:
+            m.pad_bf16(x.data_ptr(), rows, self.dims[0], self.dims[0], 1, self.xp.data_ptr(), 64, s)
+            inp = self.xp
+        elif self.dtype:
             m.to_bf16(x.data_ptr(), self.xq.data_ptr(), x.numel(), s)
             inp = self.xq
         else:
@@ -133,6 +153,13 @@ class WideClient:
         for l in range(self.L):
             K, N = self.dims[l], self.dims[l + 1]
             self._wait_bucket(l)
+            if l == 0 and pad:  # K = 14 zero-padded to 64: NT GEMM, bias + ReLU, bf16 + transposed out
+                hT = self.hT[0].data_ptr() if keep_t else 0
+                m.gemm_nt(rows, N, 64, self.xp.data_ptr(), 64, self.W0p.data_ptr(), 64, 0, 0, self.hq[0].data_ptr(),
+                          N, hT, mb, self.b[0].data_ptr(), 0, 0, 1, 1.0, 0.0, s)
+                self.nt_calls += 1
+                inp = self.hq[0]
+                continue
             if l + 1 == self.L:  # logits head: fp32 output for the loss
                 m.gemm(rows, N, K, inp.data_ptr(), K, 1, self.Wq[l].data_ptr(), K, 1, self.logits.data_ptr(), N, 1,
                        self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
@@ -163,16 +190,26 @@ class WideClient:
         C = self.dims[-1]
         # output layer (N = classes): tiny GEMMs on the generic kernel
         K = self.dims[L - 1]
-        dzo = self.dzq[L - 1]
-        if self.dtype:
+        pad = self._pad and rows % 128 == 0
+        dzo, ldo = self.dzq[L - 1], C
+        if pad:
+            dzo, ldo = self.dzp, 64
+            m.pad_bf16(self.dz_out.data_ptr(), rows, C, C, 1, dzo.data_ptr(), 64, s)
+        elif self.dtype:
             m.to_bf16(self.dz_out.data_ptr(), dzo.data_ptr(), rows * C, s)
         else:
             dzo[:rows].copy_(self.dz_out[:rows])
         h_in = self.hq[L - 2] if L >= 2 else (self.xq if self.dtype else self.X[r0:r0 + rows])
-        m.gemm(C, K, rows, dzo.data_ptr(), C, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0, 0,
+        m.gemm(C, K, rows, dzo.data_ptr(), ldo, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0, 0,
                1.0, beta, self.dtype, self._wg_split(rows), self.wg_slab.data_ptr(), 0, s)
         m.colsum(self.dz_out.data_ptr(), rows, C, C, self.gb[L - 1].data_ptr(), beta, s)
-        if L >= 2:
+        if L >= 2 and pad:
+            # dgrad into the last hidden layer: C classes zero-padded to K = 64 on the NT GEMM,
+            # ReLU-masked, bf16 row-major + transposed outputs
+            m.gemm_nt(rows, K, 64, dzo.data_ptr(), 64, self.WhTp.data_ptr(), 64, 0, 0, self.dzq[L - 2].data_ptr(), K,
+                      self.dzT[L - 2].data_ptr(), mb, 0, self.hq[L - 2].data_ptr(), K, 0, 1.0, 0.0, s)
+            self.nt_calls += 1
+        elif L >= 2:
             # dgrad into the last hidden layer (K = C: bandwidth-bound), ReLU-masked
             m.gemm(rows, K, C, dzo.data_ptr(), C, 1, self.Wq[L - 1].data_ptr(), K, 0, self.scratch.data_ptr(), K, 3, 0,
                    self.hq[L - 2].data_ptr(), K, 1 if self.dtype else 0, 1.0, 0.0, self.dtype, 1, 0,
@@ -185,8 +222,11 @@ class WideClient:
         for l in range(L - 2, -1, -1):
             K, N = self.dims[l], self.dims[l + 1]
             dq = self.dzq[l]
+            ldi = K
             if l == 0:
                 inp = self.xq if self.dtype else self.X[r0:r0 + rows]
+                if pad:
+                    inp, ldi = self.xp, 64
             else:
                 inp = self.hq[l - 1]
             # wgrad (+= over micro-batches): dW[N][K] = dZ^T . in;  bias: row sums of dZ^T
@@ -195,7 +235,7 @@ class WideClient:
                           self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, beta, s)
                 self.nt_calls += 1
             else:
-                m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), K, 0, self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0,
+                m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), ldi, 0, self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0,
                        1.0, beta, self.dtype, self._wg_split(rows) if l == 0 else 1, self.wg_slab.data_ptr(), 0, s)
             if self.dtype and rows % 8 == 0 and mb % 8 == 0:
                 m.rowsum_bf16(self.dzT[l].data_ptr(), N, rows, mb, self.gb[l].data_ptr(), beta, s)

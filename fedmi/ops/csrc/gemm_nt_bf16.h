@@ -18,6 +18,8 @@ struct NTArgs {
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s);
 hipError_t transpose_bf16_launch(const float* in, int R, int C, int ldi, void* out, int ldo, hipStream_t s);
 // out[n] = sum_r dT[n][r] (+ beta * out[n]); dT bf16 [Nrows][ld], M % 8 == 0.
+hipError_t pad_bf16_launch(const float* in, int R, int C, long long rs, long long cs, void* out, int ldo,
+                           hipStream_t s);
 hipError_t rowsum_bf16_launch(const void* dT, int Nrows, int M, int ld, float* out, float beta, hipStream_t s);
 // 0 = single-buffered two-barrier main loop, 1 = double-buffered (default)
 void gemm_nt_set_variant(int v);

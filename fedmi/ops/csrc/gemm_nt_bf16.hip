@@ -158,7 +158,7 @@ gemm_nt_bf16_kernel(NTArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// 256x256 ping-pong variant (variant 2; M % 256 == N % 256 == 0, K % 64 == 0, K >= 128).
+// 256x256 ping-pong variant (variant 2; M % 256 == N % 256 == 0, K % 64 == 0).
 //
 // 512 threads = 8 waves as 2 (M) x 4 (N), 128x64 outputs per wave (8x4 16x16 tiles, 128 fp32
 // accumulators per lane).  A K-tile (BK = 64) is computed in four PHASES of 16 MFMAs each:
@@ -348,7 +348,7 @@ void gemm_nt_set_variant(int v) { g_nt_variant = v; }
 
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
     if (g.M % NT_BM || g.N % NT_BN || g.K % NT_BK || g.lda % 8 || g.ldb % 8) return hipErrorInvalidValue;
-    if (g_nt_variant == 2 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 && g.K >= 128 &&
+    if (g_nt_variant == 2 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
         (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
         hipLaunchKernelGGL(gemm_nt_bf16_pp_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
@@ -381,6 +381,28 @@ __global__ void transpose_bf16_kernel(const float* __restrict__ in, int R, int C
 
 hipError_t transpose_bf16_launch(const float* in, int R, int C, int ldi, void* out, int ldo, hipStream_t s) {
     hipLaunchKernelGGL(transpose_bf16_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, s, in, R, C, ldi,
+                       reinterpret_cast<__hip_bfloat16*>(out), ldo);
+    return hipGetLastError();
+}
+
+// Zero-padded bf16 operand: out[r][c] = bf16(in[r*rs + c*cs]) for c < C, 0 for C <= c < ldo.
+// Pads the K = 14 input features / the C = 2 logit deltas to K = 64 so the layer-0 forward and
+// the head's dgrad run on the NT GEMM (with their fused bias/ReLU/mask and transposed outputs)
+// instead of the generic kernel + an fp32 scratch + a transpose pass; with cs != 1 it also
+// transposes (the head's W^T).
+__global__ void pad_bf16_kernel(const float* __restrict__ in, int R, int C, long long rs, long long cs,
+                                __hip_bfloat16* __restrict__ out, int ldo) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)R * ldo) return;
+    const int r = (int)(i / ldo), c = (int)(i % ldo);
+    out[i] = __float2bfloat16(c < C ? in[r * rs + c * cs] : 0.f);
+}
+
+hipError_t pad_bf16_launch(const float* in, int R, int C, long long rs, long long cs, void* out, int ldo,
+                           hipStream_t s) {
+    if (C > ldo) return hipErrorInvalidValue;
+    const size_t n = (size_t)R * ldo;
+    hipLaunchKernelGGL(pad_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, R, C, rs, cs,
                        reinterpret_cast<__hip_bfloat16*>(out), ldo);
     return hipGetLastError();
 }

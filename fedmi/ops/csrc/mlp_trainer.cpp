@@ -324,6 +324,12 @@ static void transpose_bf16_py(uintptr_t in, int R, int C, int ldi, uintptr_t out
                                    reinterpret_cast<hipStream_t>(stream)));
 }
 
+static void pad_bf16_py(uintptr_t in, int R, int C, long long rs, long long cs, uintptr_t out, int ldo,
+                        uintptr_t stream) {
+    TR_CHECK(pad_bf16_launch(reinterpret_cast<const float*>(in), R, C, rs, cs, reinterpret_cast<void*>(out), ldo,
+                             reinterpret_cast<hipStream_t>(stream)));
+}
+
 static void rowsum_bf16_py(uintptr_t dT, int Nrows, int M, int ld, uintptr_t out, float beta, uintptr_t stream) {
     TR_CHECK(rowsum_bf16_launch(reinterpret_cast<const void*>(dT), Nrows, M, ld, reinterpret_cast<float*>(out), beta,
                                 reinterpret_cast<hipStream_t>(stream)));
@@ -334,6 +340,7 @@ void register_trainer(py::module_& m) {
     m.def("gemm_nt_set_variant", &gemm_nt_set_variant);
     m.def("transpose_bf16", &transpose_bf16_py);
     m.def("rowsum_bf16", &rowsum_bf16_py);
+    m.def("pad_bf16", &pad_bf16_py);
     m.def("xent", &xent_py);
     m.def("adam_flat", &adam_flat_py);
     py::class_<MLPTrainer>(m, "MLPTrainer")
