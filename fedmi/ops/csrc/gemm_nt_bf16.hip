@@ -306,6 +306,20 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
 
+    // ReLU mask tile (dgrad): every wave's LDS reads retired before that last barrier, so the
+    // block DMAs the 256x256 bf16 mask tile into LDS with full-line loads (2 rows per wave
+    // instruction) instead of 128 scattered 2-byte loads per lane
+    if (g.mask != nullptr) {
+        const __hip_bfloat16* Mk = reinterpret_cast<const __hip_bfloat16*>(g.mask);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = i * 16 + w * 2;
+            glds16(Mk + (size_t)(m0 + row + (l >> 5)) * g.ldmask + n0 + (l & 31) * 8, smem + row * 512);
+        }
+        vm_wait<0>();
+        __syncthreads();
+    }
+
     __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
     __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
 #pragma unroll
@@ -321,7 +335,8 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
                 float v = acc[x][y][j] * g.alpha + bv;
                 if (g.relu) v = fmaxf(v, 0.f);
                 if (g.mask != nullptr) {
-                    const __hip_bfloat16 mk = reinterpret_cast<const __hip_bfloat16*>(g.mask)[(size_t)mm * g.ldmask + n];
+                    const int rl = wr * 128 + 16 * x + 4 * lg + j, cl = wc * 64 + 16 * y + lr;
+                    const __hip_bfloat16 mk = *reinterpret_cast<const __hip_bfloat16*>(smem + rl * 512 + cl * 2);
                     v = __bfloat162float(mk) > 0.f ? v : 0.f;
                 }
                 if (g.C != nullptr) {
@@ -349,7 +364,8 @@ void gemm_nt_set_variant(int v) { g_nt_variant = v; }
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
     if (g.M % NT_BM || g.N % NT_BN || g.K % NT_BK || g.lda % 8 || g.ldb % 8) return hipErrorInvalidValue;
     if (g_nt_variant == 2 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
-        (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0))) {
+        (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&
+        (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
         hipLaunchKernelGGL(gemm_nt_bf16_pp_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
         return hipGetLastError();

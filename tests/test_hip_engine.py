@@ -249,6 +249,22 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
             assert torch.equal(CbT, Cb.t())
     finally:
         m.gemm_nt_set_variant(2)
+    # ReLU-mask epilogue (dgrad: the mask tile is staged through LDS by the ping-pong loop)
+    mask = torch.randn(M, N + 8, device=dev).to(torch.bfloat16)
+    mouts = []
+    try:
+        for v in (1, 2):
+            m.gemm_nt_set_variant(v)
+            Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            m.gemm_nt(M, N, K, A.data_ptr(), K + pad, B.data_ptr(), K + pad, 0, 0, Cb.data_ptr(), N, 0, 0, 0,
+                      mask.data_ptr(), N + 8, 0, 1.0, 0.0, s)
+            torch.cuda.synchronize()
+            mouts.append(Cb)
+    finally:
+        m.gemm_nt_set_variant(2)
+    assert torch.equal(mouts[0], mouts[1])
+    mref = torch.where(mask[:, :N].float() > 0, A[:, :K].float() @ B[:, :K].float().t(), torch.zeros(M, N, device=dev))
+    assert ((mouts[1].float() - mref).abs().max() / mref.abs().max()).item() < 1e-2
     ref = (A[:, :K].float() @ B[:, :K].float().t() + bias).clamp_min(0)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
