@@ -97,6 +97,11 @@ class WideClient:
             self.W0p = torch.empty(dims[1], KP, dtype=gdt, device=dev)   # bf16 W0, zero-padded
             self.dzp = torch.empty(mb, KP, dtype=gdt, device=dev)       # bf16 head delta, padded
             self.WhTp = torch.empty(dims[-2], KP, dtype=gdt, device=dev)  # bf16 head W^T, padded
+            # logits head on the NT GEMM: classes zero-padded to N = 256 (fp32 logits, ld 256)
+            self.Whp = torch.zeros(256, dims[-2], dtype=gdt, device=dev)
+            self.bhp = torch.zeros(256, **f32)
+            self.logits_p = torch.empty(mb, 256, **f32)
+            self.logits = self.logits_p[:, :dims[-1]]
         self._quantize()
 
     # ------------------------------------------------------------------
@@ -113,8 +118,10 @@ class WideClient:
                     N, K = w.shape
                     if l == 0:
                         self.m.pad_bf16(w.data_ptr(), N, K, K, 1, self.W0p.data_ptr(), 64, stream.cuda_stream)
-                    if l == self.L - 1:  # head W [C][H] -> W^T [H][64]
+                    if l == self.L - 1:  # head W [C][H] -> W^T [H][64]; W rows 0..C-1 of [256][H]
                         self.m.pad_bf16(w.data_ptr(), K, N, 1, K, self.WhTp.data_ptr(), 64, stream.cuda_stream)
+                        self.m.to_bf16(w.data_ptr(), self.Whp.data_ptr(), w.numel(), stream.cuda_stream)
+                        self.bhp[:N].copy_(self.b[l])
                 if self.WqT[l] is not None:
                     N, K = w.shape
                     self.m.transpose_bf16(w.data_ptr(), N, K, K, self.WqT[l].data_ptr(), N, stream.cuda_stream)
@@ -160,9 +167,14 @@ class WideClient:
                 self.nt_calls += 1
                 inp = self.hq[0]
                 continue
+            if l + 1 == self.L and pad:  # logits head, classes padded to 256: fp32 [rows][256]
+                m.gemm_nt(rows, 256, K, inp.data_ptr(), K, self.Whp.data_ptr(), K, self.logits_p.data_ptr(), 256,
+                          0, 0, 0, 0, self.bhp.data_ptr(), 0, 0, 0, 1.0, 0.0, s)
+                self.nt_calls += 1
+                break
             if l + 1 == self.L:  # logits head: fp32 output for the loss
-                m.gemm(rows, N, K, inp.data_ptr(), K, 1, self.Wq[l].data_ptr(), K, 1, self.logits.data_ptr(), N, 1,
-                       self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
+                m.gemm(rows, N, K, inp.data_ptr(), K, 1, self.Wq[l].data_ptr(), K, 1, self.logits.data_ptr(),
+                       self.logits.stride(0), 1, self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
                 break
             hq = self.hq[l]
             hT = self.hT[l].data_ptr() if (keep_t and self.dtype) else 0
@@ -268,7 +280,8 @@ class WideClient:
                 rows = min(self.mb, self.n - r0)
                 self._forward(r0, rows)
                 # loss head: softmax CE, dZ = (p - onehot) / n (full-batch mean)
-                self.m.xent(self.logits.data_ptr(), C, self.y[r0:].data_ptr(), rows, C, 0, 1.0 / self.n,
+                self.m.xent(self.logits.data_ptr(), self.logits.stride(0), self.y[r0:].data_ptr(), rows, C, 0,
+                            1.0 / self.n,
                             self.dz_out.data_ptr(), C, self.loss_acc.data_ptr(), s)
                 self._backward(r0, rows, 0.0 if r0 == 0 else 1.0)
             # torch Adam + StepLR (scalars computed on host: the schedule is known)
