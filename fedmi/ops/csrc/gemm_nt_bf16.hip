@@ -376,46 +376,50 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
 
-    // ReLU mask tile (dgrad): every wave's LDS reads retired before that last barrier, so the
-    // block DMAs the 256x256 bf16 mask tile into LDS with full-line loads (2 rows per wave
-    // instruction) instead of 128 scattered 2-byte loads per lane
+    // Epilogue.  Every wave's LDS reads retired before that last barrier, so the 128 KiB of LDS
+    // now holds the block's 256x256 bf16 output tile as 512-byte rows whose 16-byte chunk index
+    // is XOR-ed with sw(row) = ((row >> 2) & 3) * 2 (the four 4-row lane groups of a 2-byte
+    // write land on distinct banks; a 16-lane read of 16 chunks of one row stays conflict-free).
+    // Each lane drops its bf16 values into the tile, then the block stores it with full 512-byte
+    // row segments (16 B per lane) instead of 2-byte scattered stores.  The dgrad ReLU mask is
+    // DMA-ed into the same slots first (full-line loads, same swizzle) and overwritten in place
+    // by the lane that reads it.
+    auto sw = [](int row) { return ((row >> 2) & 3) * 2; };
+    auto tile_off = [&](int row, int col) { return row * 512 + ((((col >> 3) ^ sw(row))) << 4) + (col & 7) * 2; };
+    __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
+    __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
     if (g.mask != nullptr) {
         const __hip_bfloat16* Mk = reinterpret_cast<const __hip_bfloat16*>(g.mask);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const int row = i * 16 + w * 2;
-            glds16(Mk + (size_t)(m0 + row + (l >> 5)) * g.ldmask + n0 + (l & 31) * 8, smem + row * 512);
+            const int row = i * 16 + w * 2, rr = row + (l >> 5);
+            glds16(Mk + (size_t)(m0 + rr) * g.ldmask + n0 + (((l & 31) ^ sw(rr)) << 3), smem + row * 512);
         }
         vm_wait<0>();
         __syncthreads();
     }
 
-    __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
-    __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-        const int n = n0 + wc * 64 + 16 * y + lr;
+        const int cl = wc * 64 + 16 * y + lr, n = n0 + cl;
         const float bv = g.bias != nullptr ? g.bias[n] : 0.f;
 #pragma unroll
         for (int x = 0; x < 8; ++x) {
             uint32_t tp[2];  // the lane's 4 consecutive rows of column n, packed for CbT
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int mm = m0 + wr * 128 + 16 * x + 4 * lg + j;
+                const int rl = wr * 128 + 16 * x + 4 * lg + j, mm = m0 + rl;
+                __hip_bfloat16* slot = reinterpret_cast<__hip_bfloat16*>(smem + tile_off(rl, cl));
                 float v = acc[x][y][j] * g.alpha + bv;
                 if (g.relu) v = fmaxf(v, 0.f);
-                if (g.mask != nullptr) {
-                    const int rl = wr * 128 + 16 * x + 4 * lg + j, cl = wc * 64 + 16 * y + lr;
-                    const __hip_bfloat16 mk = *reinterpret_cast<const __hip_bfloat16*>(smem + rl * 512 + cl * 2);
-                    v = __bfloat162float(mk) > 0.f ? v : 0.f;
-                }
+                if (g.mask != nullptr) v = __bfloat162float(*slot) > 0.f ? v : 0.f;
                 if (g.C != nullptr) {
                     float* cp = g.C + (size_t)mm * g.ldc + n;
                     if (g.beta != 0.f) v += g.beta * *cp;
                     *cp = v;
                 }
                 const __hip_bfloat16 hv = __float2bfloat16(v);
-                if (Cb != nullptr) Cb[(size_t)mm * g.ldcb + n] = hv;
+                if (Cb != nullptr) *slot = hv;
                 const uint32_t hb = __bfloat16_as_ushort(hv);
                 if (j & 1) tp[j >> 1] |= hb << 16;
                 else tp[j >> 1] = hb;
@@ -424,6 +428,15 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
                 const size_t off = (size_t)n * g.ldct + m0 + wr * 128 + 16 * x + 4 * lg;
                 *reinterpret_cast<uint2*>(CbT + off) = make_uint2(tp[0], tp[1]);
             }
+        }
+    }
+    if (Cb != nullptr) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int rr = i * 16 + w * 2 + (l >> 5), p = l & 31;
+            const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * 512 + p * 16);
+            *reinterpret_cast<uint4*>(Cb + (size_t)(m0 + rr) * g.ldcb + n0 + ((p ^ sw(rr)) << 3)) = d;
         }
     }
 }
@@ -435,7 +448,8 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
     if (g.M % NT_BM || g.N % NT_BN || g.K % NT_BK || g.lda % 8 || g.ldb % 8) return hipErrorInvalidValue;
     if (g_nt_variant == 2 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
         (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&
-        (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0))) {
+        (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
+        (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
         hipLaunchKernelGGL(gemm_nt_bf16_pp_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
         return hipGetLastError();
