@@ -73,7 +73,8 @@ def parse_args(argv=None):
                     help="BASELINE config 3: layer-by-layer wide-MLP client (e.g. --hidden 4096 4096 4096) on "
                          "device-generated synthetic shards of --synthetic-rows rows per client")
     ap.add_argument("--synthetic-rows", type=int, default=131072, help="rows per client for --wide")
-    ap.add_argument("--micro-batch", type=int, default=16384, help="rows per micro-batch for --wide")
+    ap.add_argument("--micro-batch", type=int, default=131072,
+                    help="rows per micro-batch for --wide (about 112 KiB of activation buffers per row at 4096 wide: 14 GiB of HBM)")
     ap.add_argument("--eval-every", type=int, default=0, help="--wide: local accuracy every N rounds")
     return ap.parse_args(argv)
 

@@ -28,7 +28,7 @@ from ..models.mlp import init_flat, param_layout
 
 class WideClient:
     def __init__(self, X: torch.Tensor, y: torch.Tensor, dims: Sequence[int], comm=None, n_total: Optional[int] = None,
-                 micro_batch: int = 8192, lr: float = 0.004, betas=(0.9, 0.999), eps: float = 1e-8,
+                 micro_batch: int = 131072, lr: float = 0.004, betas=(0.9, 0.999), eps: float = 1e-8,
                  step_size: int = 30, gamma: float = 0.5, seed: int = 0, dtype: str = "bf16",
                  eval_rows: int = 0):
         from ..ops import native
@@ -340,7 +340,7 @@ class WideClient:
         return 6.0 * self.n * macs
 
 
-def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int, micro_batch: int = 16384,
+def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int, micro_batch: int = 131072,
                     dtype: str = "bf16", lr: float = 0.004, eval_every: int = 0, seed: int = 7,
                     verbose: bool = True) -> dict:
     """BASELINE config 3 driver: every rank is one client holding ``rows_per_client``

@@ -60,10 +60,13 @@ for dt_, dims in (("fp32", [14, 64, 48, 2]), ("bf16", [14, 64, 48, 2]), ("bf16",
           flush=True)
 rows = 1 << 17
 Xw = torch.randn(rows, 14, device=dev); yw = torch.randint(0, 2, (rows,), device=dev)
-c = WideClient(Xw, yw, [14, 4096, 4096, 4096, 2], micro_batch=16384, dtype="bf16")
-c.run_round(); torch.cuda.synchronize()
-t = time.time(); n = 3
-for _ in range(n): c.run_round()
-torch.cuda.synchronize(); dt = (time.time() - t) / n
-print(f"wide bf16: rows={rows} {dt*1e3:.1f} ms/round, {c.flops_per_round/dt/1e12:.1f} TFLOP/s, "
-      f"{rows/dt/1e6:.2f} M samples/s", flush=True)
+for mb in [int(a) for a in sys.argv[1:]] or [16384]:
+    c = WideClient(Xw, yw, [14, 4096, 4096, 4096, 2], micro_batch=mb, dtype="bf16")
+    c.run_round(); torch.cuda.synchronize()
+    t = time.time(); n = 3
+    for _ in range(n): c.run_round()
+    torch.cuda.synchronize(); dt = (time.time() - t) / n
+    print(f"wide bf16: rows={rows} micro-batch {mb}: {dt*1e3:.1f} ms/round, {c.flops_per_round/dt/1e12:.1f} TFLOP/s, "
+          f"{rows/dt/1e6:.2f} M samples/s", flush=True)
+    del c
+    torch.cuda.empty_cache()

@@ -1,5 +1,5 @@
 """Wide-MLP round profiling driver (rocprofv3 --kernel-trace --stats): 14-4096^3-2, 131072 rows,
-micro-batch 16384, bf16, one warm-up round + 3 rounds."""
+micro-batch = argv[1] rows (default: the whole shard), bf16, 4 rounds."""
 import sys
 import torch
 sys.path.insert(0, ".")
@@ -9,7 +9,8 @@ dev = torch.device("cuda", 0)
 rows = 1 << 17
 X = torch.randn(rows, 14, device=dev)
 y = torch.randint(0, 2, (rows,), device=dev)
-c = WideClient(X, y, [14, 4096, 4096, 4096, 2], micro_batch=16384, dtype="bf16")
+mb = int(sys.argv[1]) if len(sys.argv) > 1 else rows
+c = WideClient(X, y, [14, 4096, 4096, 4096, 2], micro_batch=mb, dtype="bf16")
 for _ in range(4):
     c.run_round()
 torch.cuda.synchronize()
