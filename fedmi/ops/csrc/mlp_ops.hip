@@ -77,37 +77,56 @@ xent_kernel(XentArgs a) {
 // style 1: sklearn AdamOptimizer (lr_t = lr sqrt(1-b2^t)/(1-b1^t), update -lr_t m/(sqrt(v)+eps)).
 // L2: g += wd * p on entries with wd_mask (sklearn: alpha/batch on coefs only), and the
 // sklearn loss term 0.5*alpha*sum(coef^2) (of the pre-update weights) is added to loss_acc.
+#define ADAM_EPT 4
+
 __global__ void __launch_bounds__(256)
 adam_kernel(AdamArgs a) {
     __shared__ double red[256];
+    __shared__ float coef[2];
     const int t = blockIdx.y;
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool run = a.active == nullptr || a.active[t] != 0;
+    // the trial's bias-corrected step factors, once per block (fp64 pow/sqrt per element made
+    // this kernel compute-bound: 454 us for the 33.6 M-parameter wide MLP)
+    if (threadIdx.x == 0) {
+        const long long step = a.step != nullptr ? a.step[t] : a.step_scalar;
+        const double lr = a.lr != nullptr ? a.lr[t] : a.lr_scalar;
+        if (a.style == 0) {
+            coef[0] = (float)(lr / (1.0 - pow(a.beta1, (double)step)));
+            coef[1] = (float)sqrt(1.0 - pow(a.beta2, (double)step));
+        } else {
+            coef[0] = (float)(lr * sqrt(1.0 - pow(a.beta2, (double)step)) / (1.0 - pow(a.beta1, (double)step)));
+            coef[1] = 0.f;
+        }
+    }
+    __syncthreads();
+    const float c0 = coef[0], c1 = coef[1];
+    const float omb1 = (float)(1.0 - a.beta1), b1 = (float)a.beta1;
+    const float omb2 = (float)(1.0 - a.beta2), b2 = (float)a.beta2;
+    const float eps = (float)a.eps, wd = (float)a.wd, mu = (float)a.mu;
     double sq = 0.0;
-    if (run && i < a.n) {
+    // ADAM_EPT elements per thread, strided by the block size (coalesced, independent chains)
+#pragma unroll
+    for (int e = 0; e < ADAM_EPT; ++e) {
+        const size_t i = ((size_t)blockIdx.x * ADAM_EPT + e) * blockDim.x + threadIdx.x;
+        if (!run || i >= a.n) continue;
         const size_t j = (size_t)t * a.n + i;
         float p = a.p[j];
         float g = a.g[j];
         const bool decay = a.wd_mask == nullptr || a.wd_mask[i] != 0;
         if (decay) {
-            sq = (double)p * (double)p;
-            if (a.wd != 0.0) g += (float)a.wd * p;
+            sq += (double)p * (double)p;
+            if (a.wd != 0.0) g += wd * p;
         }
-        if (a.mu != 0.0) g += (float)a.mu * (p - a.anchor[j]);
-        const long long step = a.step != nullptr ? a.step[t] : a.step_scalar;
-        const double lr = a.lr != nullptr ? a.lr[t] : a.lr_scalar;
+        if (a.mu != 0.0) g += mu * (p - a.anchor[j]);
         float m = a.m[j], v = a.v[j];
         if (a.style == 0) {
-            m = m + (float)(1.0 - a.beta1) * (g - m);
-            v = v * (float)a.beta2 + (float)(1.0 - a.beta2) * g * g;
-            const float step_size = (float)(lr / (1.0 - pow(a.beta1, (double)step)));
-            const float bc2_sqrt = (float)sqrt(1.0 - pow(a.beta2, (double)step));
-            p = p + (-step_size) * (m / (sqrtf(v) / bc2_sqrt + (float)a.eps));
+            m = m + omb1 * (g - m);
+            v = v * b2 + omb2 * g * g;
+            p = p + (-c0) * (m / (sqrtf(v) / c1 + eps));
         } else {
-            m = (float)a.beta1 * m + (float)(1.0 - a.beta1) * g;
-            v = (float)a.beta2 * v + (float)(1.0 - a.beta2) * g * g;
-            const float lr_t = (float)(lr * sqrt(1.0 - pow(a.beta2, (double)step)) / (1.0 - pow(a.beta1, (double)step)));
-            p = p - lr_t * m / (sqrtf(v) + (float)a.eps);
+            m = b1 * m + omb1 * g;
+            v = b2 * v + omb2 * g * g;
+            p = p - c0 * m / (sqrtf(v) + eps);
         }
         a.m[j] = m;
         a.v[j] = v;
@@ -172,7 +191,7 @@ hipError_t xent_launch(const XentArgs& a, int T, hipStream_t s) {
 }
 
 hipError_t adam_launch(const AdamArgs& a, int T, hipStream_t s) {
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((a.n + 255) / 256), T), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((a.n + 256 * ADAM_EPT - 1) / (256 * ADAM_EPT)), T), dim3(256), 0, s, a);
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
     return hipSuccess;
 }
