@@ -78,6 +78,13 @@ class WideClient:
         # whose 64x64 output tiles alone would leave all but ~64 CUs idle over a long contraction
         self.wg_splits = max(1, min(16, mb // 1024))
         self.wg_slab = torch.empty(self.wg_splits * max(dims[0] * dims[1], dims[-1] * dims[-2]), **f32)
+        # bf16: the two skinny gradients run on a bandwidth-bound kernel instead (8 columns x C
+        # accumulators per thread, up to 256 row splits, fixed-order slab reduction)
+        self._skinny = (bool(self.dtype) and self.L >= 2 and dims[0] == 14 and dims[-1] == 2
+                        and dims[1] % 8 == 0 and dims[-2] % 8 == 0)
+        self.sk_splits = max(1, min(256, mb // 256))
+        self.sk_slab = (torch.empty(self.sk_splits * max(dims[0] * dims[1], dims[-1] * dims[-2]), **f32)
+                        if self._skinny else None)
         self.dz_out = torch.empty(mb, dims[-1], **f32)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         self.round = 0
@@ -197,6 +204,10 @@ class WideClient:
         """K-split count of a skinny weight gradient over `rows` contraction rows (>= 1024 rows per split)."""
         return max(1, min(self.wg_splits, rows // 1024))
 
+    def _sk_split(self, rows: int) -> int:
+        """Row splits of the skinny-gradient kernel (>= 256 rows per split)."""
+        return max(1, min(self.sk_splits, rows // 256))
+
     def _backward(self, r0: int, rows: int, beta: float):
         m, s, mb, L = self.m, self._s(), self.mb, self.L
         C = self.dims[-1]
@@ -212,8 +223,12 @@ class WideClient:
         else:
             dzo[:rows].copy_(self.dz_out[:rows])
         h_in = self.hq[L - 2] if L >= 2 else (self.xq if self.dtype else self.X[r0:r0 + rows])
-        m.gemm(C, K, rows, dzo.data_ptr(), ldo, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0, 0,
-               1.0, beta, self.dtype, self._wg_split(rows), self.wg_slab.data_ptr(), 0, s)
+        if self._skinny:
+            m.skinny_wgrad(h_in.data_ptr(), K, K, dzo.data_ptr(), ldo, C, rows, 0, self._sk_split(rows),
+                           self.sk_slab.data_ptr(), self.gW[L - 1].data_ptr(), beta, s)
+        else:
+            m.gemm(C, K, rows, dzo.data_ptr(), ldo, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0,
+                   0, 1.0, beta, self.dtype, self._wg_split(rows), self.wg_slab.data_ptr(), 0, s)
         m.colsum(self.dz_out.data_ptr(), rows, C, C, self.gb[L - 1].data_ptr(), beta, s)
         if L >= 2 and pad:
             # dgrad into the last hidden layer: C classes zero-padded to K = 64 on the NT GEMM,
@@ -246,6 +261,9 @@ class WideClient:
                 m.gemm_nt(N, K, rows, self.dzT[l].data_ptr(), mb, self.hT[l - 1].data_ptr(), mb,
                           self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, beta, s)
                 self.nt_calls += 1
+            elif l == 0 and self._skinny:
+                m.skinny_wgrad(dq.data_ptr(), N, N, inp.data_ptr(), ldi, K, rows, 1, self._sk_split(rows),
+                               self.sk_slab.data_ptr(), self.gW[0].data_ptr(), beta, s)
             else:
                 m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), ldi, 0, self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0,
                        1.0, beta, self.dtype, self._wg_split(rows) if l == 0 else 1, self.wg_slab.data_ptr(), 0, s)

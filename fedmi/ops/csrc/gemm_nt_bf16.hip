@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "gemm_nt_bf16.h"
+#include "gemm_mfma.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
@@ -532,4 +533,82 @@ hipError_t rowsum_bf16_launch(const void* dT, int Nrows, int M, int ld, float* o
     hipLaunchKernelGGL(rowsum_bf16_kernel, dim3((Nrows + 3) / 4), dim3(256), 0, s,
                        reinterpret_cast<const __hip_bfloat16*>(dT), Nrows, M, ld, out, beta);
     return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Skinny weight gradient over a long contraction (the wide MLP's layer 0, 14 input features, and
+// its logits head, C classes), bandwidth-bound:  out = beta*out + sum_rows S[row][c] * W[row][n]
+// for c < C, n < Nw.  W: [rows][ldw] bf16 (the wide side: 4096 deltas or activations), S:
+// [rows][lds] bf16 (the skinny side, row-uniform, so the compiler reads it with scalar loads).
+// A thread owns 8 consecutive n (one 16-byte load per row) x C fp32 accumulators; a block of 256
+// threads spans 2048 columns; blockIdx.y = z contracts rows [z*rc, (z+1)*rc) into slab[z], and
+// splitk_reduce folds the slabs in fixed order (deterministic).  TRANS = 0 writes out[c][n]
+// (ld Nw: the head's dW[C][H]), TRANS = 1 out[n][c] (ld C: layer 0's dW[H][14]).  Replaces the
+// MFMA tile GEMM there, whose 64-row tiles over C <= 14 wasted the matrix core and streamed the
+// wide operand at ~1.3 TB/s.
+template <int C, int TRANS>
+__global__ void __launch_bounds__(256)
+skinny_wgrad_kernel(const __hip_bfloat16* __restrict__ W, int ldw, int Nw, const __hip_bfloat16* __restrict__ S,
+                    int lds, int rows, int rc, float* __restrict__ slab) {
+    const int n0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+    const int z = blockIdx.y;
+    const int r0 = z * rc, r1 = min(rows, r0 + rc);
+    float acc[C][8];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[c][e] = 0.f;
+    if (n0 < Nw) {
+#pragma unroll 4
+        for (int r = r0; r < r1; ++r) {
+            const uint4 wv = *reinterpret_cast<const uint4*>(W + (size_t)r * ldw + n0);
+            const uint32_t wu[4] = {wv.x, wv.y, wv.z, wv.w};
+            float wf[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                wf[2 * q] = __uint_as_float(wu[q] << 16);
+                wf[2 * q + 1] = __uint_as_float(wu[q] & 0xffff0000u);
+            }
+            const __hip_bfloat16* srow = S + (size_t)r * lds;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const float sc = __bfloat162float(srow[c]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[c][e] = fmaf(sc, wf[e], acc[c][e]);
+            }
+        }
+    }
+    if (n0 >= Nw) return;
+    float* out = slab + (size_t)z * C * Nw;
+    if (TRANS == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            float4* o = reinterpret_cast<float4*>(out + (size_t)c * Nw + n0);
+            o[0] = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+            o[1] = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int c = 0; c < C; ++c) out[(size_t)(n0 + e) * C + c] = acc[c][e];
+    }
+}
+
+hipError_t skinny_wgrad_launch(const void* W, int ldw, int Nw, const void* S, int lds, int C, int rows, int trans,
+                               int splits, float* slab, float* out, float beta, hipStream_t s) {
+    if (Nw % 8 || ldw % 8 || (reinterpret_cast<uintptr_t>(W) & 15) || splits < 1 || lds < C) return hipErrorInvalidValue;
+    const int rc = (rows + splits - 1) / splits;
+    const dim3 grid((unsigned)((Nw / 8 + 255) / 256), (unsigned)splits);
+    const __hip_bfloat16* w = reinterpret_cast<const __hip_bfloat16*>(W);
+    const __hip_bfloat16* sk = reinterpret_cast<const __hip_bfloat16*>(S);
+    if (C == 2 && trans == 0)
+        hipLaunchKernelGGL((skinny_wgrad_kernel<2, 0>), grid, dim3(256), 0, s, w, ldw, Nw, sk, lds, rows, rc, slab);
+    else if (C == 14 && trans == 1)
+        hipLaunchKernelGGL((skinny_wgrad_kernel<14, 1>), grid, dim3(256), 0, s, w, ldw, Nw, sk, lds, rows, rc, slab);
+    else
+        return hipErrorInvalidValue;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return splitk_reduce_launch(slab, (size_t)C * Nw, splits, out, (size_t)C * Nw, beta, s);
 }

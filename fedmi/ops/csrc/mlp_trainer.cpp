@@ -335,7 +335,15 @@ static void rowsum_bf16_py(uintptr_t dT, int Nrows, int M, int ld, uintptr_t out
                                 reinterpret_cast<hipStream_t>(stream)));
 }
 
+static void skinny_wgrad_py(uintptr_t W, int ldw, int Nw, uintptr_t S, int lds, int C, int rows, int trans,
+                            int splits, uintptr_t slab, uintptr_t out, float beta, uintptr_t stream) {
+    TR_CHECK(skinny_wgrad_launch(reinterpret_cast<const void*>(W), ldw, Nw, reinterpret_cast<const void*>(S), lds, C,
+                                 rows, trans, splits, reinterpret_cast<float*>(slab), reinterpret_cast<float*>(out),
+                                 beta, reinterpret_cast<hipStream_t>(stream)));
+}
+
 void register_trainer(py::module_& m) {
+    m.def("skinny_wgrad", &skinny_wgrad_py);
     m.def("gemm_nt", &gemm_nt_py);
     m.def("gemm_nt_set_variant", &gemm_nt_set_variant);
     m.def("transpose_bf16", &transpose_bf16_py);

@@ -222,6 +222,30 @@ def test_gemm_nt_bf16_epilogues():
     assert ((C - r2).abs().max() / r2.abs().max()).item() < 1e-5
 
 
+@pytest.mark.parametrize("C,trans,rows,splits", [(2, 0, 1000, 3), (14, 1, 4096, 16), (2, 0, 256, 1)])
+def test_skinny_wgrad_bf16(C, trans, rows, splits):
+    """Skinny weight gradient (wide MLP layer 0 / logits head) vs an fp32 torch reference of the
+    same bf16 operands, accumulating into a non-zero output (beta = 1)."""
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(C + rows)
+    Nw, lds = 2048 + 512, 64
+    W = torch.randn(rows, Nw, device=dev).to(torch.bfloat16)
+    S = torch.randn(rows, lds, device=dev).to(torch.bfloat16)
+    ref = S[:, :C].float().t() @ W.float()          # [C][Nw]
+    if trans:
+        ref = ref.t().contiguous()                   # [Nw][C]
+    out0 = torch.randn_like(ref)
+    out = out0.clone()
+    slab = torch.empty(splits * C * Nw, device=dev)
+    m.skinny_wgrad(W.data_ptr(), Nw, Nw, S.data_ptr(), lds, C, rows, trans, splits, slab.data_ptr(), out.data_ptr(),
+                   1.0, s)
+    torch.cuda.synchronize()
+    exp = out0 + ref
+    assert ((out - exp).abs().max() / exp.abs().max()).item() < 1e-5
+
+
 @pytest.mark.parametrize("M,N,K,pad", [(256, 512, 64, 0), (256, 256, 128, 0), (512, 768, 192, 64), (768, 512, 1024, 0),
                                        (2048, 1024, 4096, 8)])
 def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
