@@ -83,7 +83,7 @@ class WideClient:
         self._skinny = (bool(self.dtype) and self.L >= 2 and dims[0] == 14 and dims[-1] == 2
                         and dims[1] % 8 == 0 and dims[-2] % 8 == 0)
         self.sk_splits = max(1, min(256, mb // 256))
-        self.sk_slab = (torch.empty(self.sk_splits * max(dims[0] * dims[1], dims[-1] * dims[-2]), **f32)
+        self.sk_slab = (torch.empty(self.sk_splits * max((dims[0] + 1) * dims[1], dims[-1] * dims[-2]), **f32)
                         if self._skinny else None)
         self.dz_out = torch.empty(mb, dims[-1], **f32)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -225,7 +225,7 @@ class WideClient:
         h_in = self.hq[L - 2] if L >= 2 else (self.xq if self.dtype else self.X[r0:r0 + rows])
         if self._skinny:
             m.skinny_wgrad(h_in.data_ptr(), K, K, dzo.data_ptr(), ldo, C, rows, 0, self._sk_split(rows),
-                           self.sk_slab.data_ptr(), self.gW[L - 1].data_ptr(), beta, s)
+                           self.sk_slab.data_ptr(), self.gW[L - 1].data_ptr(), beta, 0, s)
         else:
             m.gemm(C, K, rows, dzo.data_ptr(), ldo, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0,
                    0, 1.0, beta, self.dtype, self._wg_split(rows), self.wg_slab.data_ptr(), 0, s)
@@ -262,12 +262,15 @@ class WideClient:
                           self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, beta, s)
                 self.nt_calls += 1
             elif l == 0 and self._skinny:
+                # + layer 0's bias gradient (column sums of dZ0) from the same loads
                 m.skinny_wgrad(dq.data_ptr(), N, N, inp.data_ptr(), ldi, K, rows, 1, self._sk_split(rows),
-                               self.sk_slab.data_ptr(), self.gW[0].data_ptr(), beta, s)
+                               self.sk_slab.data_ptr(), self.gW[0].data_ptr(), beta, self.gb[0].data_ptr(), s)
             else:
                 m.gemm(N, K, rows, dq.data_ptr(), N, 0, inp.data_ptr(), ldi, 0, self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0,
                        1.0, beta, self.dtype, self._wg_split(rows) if l == 0 else 1, self.wg_slab.data_ptr(), 0, s)
-            if self.dtype and rows % 8 == 0 and mb % 8 == 0:
+            if l == 0 and self._skinny:
+                pass  # bias gradient produced by the skinny weight-gradient kernel above
+            elif self.dtype and rows % 8 == 0 and mb % 8 == 0:
                 m.rowsum_bf16(self.dzT[l].data_ptr(), N, rows, mb, self.gb[l].data_ptr(), beta, s)
             else:
                 dzf = dq[:rows].float()

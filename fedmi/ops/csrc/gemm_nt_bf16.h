@@ -22,8 +22,9 @@ hipError_t pad_bf16_launch(const float* in, int R, int C, long long rs, long lon
                            hipStream_t s);
 hipError_t rowsum_bf16_launch(const void* dT, int Nrows, int M, int ld, float* out, float beta, hipStream_t s);
 // Skinny weight gradient, out = beta*out + sum_r S[r][c] W[r][n] (C = 2 with trans = 0: out[c][n];
-// C = 14 with trans = 1: out[n][c]), split over `splits` row ranges into slab[splits][C*Nw].
+// C = 14 with trans = 1: out[n][c]), split over `splits` row ranges into slab[splits][(C + b) * Nw];
+// bias_out (C = 14 only; b = 1) also gets beta*bias_out + the column sums of W.
 hipError_t skinny_wgrad_launch(const void* W, int ldw, int Nw, const void* S, int lds, int C, int rows, int trans,
-                               int splits, float* slab, float* out, float beta, hipStream_t s);
+                               int splits, float* slab, float* out, float beta, float* bias_out, hipStream_t s);
 // 0 = single-buffered two-barrier main loop, 1 = double-buffered (default)
 void gemm_nt_set_variant(int v);

@@ -545,15 +545,18 @@ hipError_t rowsum_bf16_launch(const void* dT, int Nrows, int M, int ld, float* o
 // splitk_reduce folds the slabs in fixed order (deterministic).  TRANS = 0 writes out[c][n]
 // (ld Nw: the head's dW[C][H]), TRANS = 1 out[n][c] (ld C: layer 0's dW[H][14]).  Replaces the
 // MFMA tile GEMM there, whose 64-row tiles over C <= 14 wasted the matrix core and streamed the
-// wide operand at ~1.3 TB/s.
-template <int C, int TRANS>
+// wide operand at ~1.3 TB/s.  BIAS = 1 also sums the wide operand's columns (layer 0's bias
+// gradient, sum over rows of dZ0) into slab[z][C*Nw + n], from the same loads.
+template <int C, int TRANS, int BIAS>
 __global__ void __launch_bounds__(256)
 skinny_wgrad_kernel(const __hip_bfloat16* __restrict__ W, int ldw, int Nw, const __hip_bfloat16* __restrict__ S,
                     int lds, int rows, int rc, float* __restrict__ slab) {
     const int n0 = (blockIdx.x * 256 + threadIdx.x) * 8;
     const int z = blockIdx.y;
     const int r0 = z * rc, r1 = min(rows, r0 + rc);
-    float acc[C][8];
+    float acc[C][8], bsum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -569,6 +572,10 @@ skinny_wgrad_kernel(const __hip_bfloat16* __restrict__ W, int ldw, int Nw, const
                 wf[2 * q] = __uint_as_float(wu[q] << 16);
                 wf[2 * q + 1] = __uint_as_float(wu[q] & 0xffff0000u);
             }
+            if (BIAS) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bsum[e] += wf[e];
+            }
             const __hip_bfloat16* srow = S + (size_t)r * lds;
 #pragma unroll
             for (int c = 0; c < C; ++c) {
@@ -579,7 +586,12 @@ skinny_wgrad_kernel(const __hip_bfloat16* __restrict__ W, int ldw, int Nw, const
         }
     }
     if (n0 >= Nw) return;
-    float* out = slab + (size_t)z * C * Nw;
+    float* out = slab + (size_t)z * (C + BIAS) * Nw;
+    if (BIAS) {
+        float4* o = reinterpret_cast<float4*>(out + (size_t)C * Nw + n0);
+        o[0] = make_float4(bsum[0], bsum[1], bsum[2], bsum[3]);
+        o[1] = make_float4(bsum[4], bsum[5], bsum[6], bsum[7]);
+    }
     if (TRANS == 0) {
 #pragma unroll
         for (int c = 0; c < C; ++c) {
@@ -596,19 +608,25 @@ skinny_wgrad_kernel(const __hip_bfloat16* __restrict__ W, int ldw, int Nw, const
 }
 
 hipError_t skinny_wgrad_launch(const void* W, int ldw, int Nw, const void* S, int lds, int C, int rows, int trans,
-                               int splits, float* slab, float* out, float beta, hipStream_t s) {
+                               int splits, float* slab, float* out, float beta, float* bias_out, hipStream_t s) {
     if (Nw % 8 || ldw % 8 || (reinterpret_cast<uintptr_t>(W) & 15) || splits < 1 || lds < C) return hipErrorInvalidValue;
     const int rc = (rows + splits - 1) / splits;
     const dim3 grid((unsigned)((Nw / 8 + 255) / 256), (unsigned)splits);
     const __hip_bfloat16* w = reinterpret_cast<const __hip_bfloat16*>(W);
     const __hip_bfloat16* sk = reinterpret_cast<const __hip_bfloat16*>(S);
-    if (C == 2 && trans == 0)
-        hipLaunchKernelGGL((skinny_wgrad_kernel<2, 0>), grid, dim3(256), 0, s, w, ldw, Nw, sk, lds, rows, rc, slab);
+    const int nb = bias_out != nullptr ? 1 : 0;
+    if (C == 2 && trans == 0 && !nb)
+        hipLaunchKernelGGL((skinny_wgrad_kernel<2, 0, 0>), grid, dim3(256), 0, s, w, ldw, Nw, sk, lds, rows, rc, slab);
+    else if (C == 14 && trans == 1 && !nb)
+        hipLaunchKernelGGL((skinny_wgrad_kernel<14, 1, 0>), grid, dim3(256), 0, s, w, ldw, Nw, sk, lds, rows, rc, slab);
     else if (C == 14 && trans == 1)
-        hipLaunchKernelGGL((skinny_wgrad_kernel<14, 1>), grid, dim3(256), 0, s, w, ldw, Nw, sk, lds, rows, rc, slab);
+        hipLaunchKernelGGL((skinny_wgrad_kernel<14, 1, 1>), grid, dim3(256), 0, s, w, ldw, Nw, sk, lds, rows, rc, slab);
     else
         return hipErrorInvalidValue;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return splitk_reduce_launch(slab, (size_t)C * Nw, splits, out, (size_t)C * Nw, beta, s);
+    const size_t stride = (size_t)(C + nb) * Nw;
+    e = splitk_reduce_launch(slab, stride, splits, out, (size_t)C * Nw, beta, s);
+    if (e != hipSuccess || !nb) return e;
+    return splitk_reduce_launch(slab + (size_t)C * Nw, stride, splits, bias_out, (size_t)Nw, beta, s);
 }

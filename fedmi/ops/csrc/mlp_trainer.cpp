@@ -336,10 +336,11 @@ static void rowsum_bf16_py(uintptr_t dT, int Nrows, int M, int ld, uintptr_t out
 }
 
 static void skinny_wgrad_py(uintptr_t W, int ldw, int Nw, uintptr_t S, int lds, int C, int rows, int trans,
-                            int splits, uintptr_t slab, uintptr_t out, float beta, uintptr_t stream) {
+                            int splits, uintptr_t slab, uintptr_t out, float beta, uintptr_t bias_out,
+                            uintptr_t stream) {
     TR_CHECK(skinny_wgrad_launch(reinterpret_cast<const void*>(W), ldw, Nw, reinterpret_cast<const void*>(S), lds, C,
                                  rows, trans, splits, reinterpret_cast<float*>(slab), reinterpret_cast<float*>(out),
-                                 beta, reinterpret_cast<hipStream_t>(stream)));
+                                 beta, reinterpret_cast<float*>(bias_out), reinterpret_cast<hipStream_t>(stream)));
 }
 
 void register_trainer(py::module_& m) {

@@ -238,12 +238,17 @@ def test_skinny_wgrad_bf16(C, trans, rows, splits):
         ref = ref.t().contiguous()                   # [Nw][C]
     out0 = torch.randn_like(ref)
     out = out0.clone()
-    slab = torch.empty(splits * C * Nw, device=dev)
+    slab = torch.empty(splits * (C + 1) * Nw, device=dev)
+    b0 = torch.randn(Nw, device=dev)
+    bias = b0.clone()
     m.skinny_wgrad(W.data_ptr(), Nw, Nw, S.data_ptr(), lds, C, rows, trans, splits, slab.data_ptr(), out.data_ptr(),
-                   1.0, s)
+                   1.0, bias.data_ptr() if trans else 0, s)
     torch.cuda.synchronize()
     exp = out0 + ref
     assert ((out - exp).abs().max() / exp.abs().max()).item() < 1e-5
+    if trans:  # layer 0: bias gradient = column sums of the wide operand, from the same loads
+        bexp = b0 + W.float().sum(0)
+        assert ((bias - bexp).abs().max() / bexp.abs().max()).item() < 1e-5
 
 
 @pytest.mark.parametrize("M,N,K,pad", [(256, 512, 64, 0), (256, 256, 128, 0), (512, 768, 192, 64), (768, 512, 1024, 0),
