@@ -245,6 +245,21 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
         sbB[h] = reinterpret_cast<const char*>(B + (size_t)(n0 + rb) * g.ldb);
         dstB[h] = 32768 + rb * 64;
     }
+#if NT2_EXP == 3
+    // timing experiment only (wrong results): every DMA reads 8 full 128-byte lines instead of
+    // 16 half lines (same bytes per K-tile), to price the per-line cost of the DMA issue
+    const uint32_t vxA = (uint32_t)((l >> 3) * g.lda * 2 + (l & 7) * 16);
+    const uint32_t vxB = (uint32_t)((l >> 3) * g.ldb * 2 + (l & 7) * 16);
+    auto dma = [&](int tile, int d) {
+        const int ks = (d >= 4) ? 1 : 0;
+        const int kb = tile * 128;
+        char* base = smem + (tile & 1) * 65536 + ks * 16384;
+        if (d == 0 || d == 7) glds16(sbA[0] + kb + vxA + ks * 8 * g.lda * 2, base + dstA[0]);
+        else if (d == 3 || d == 4) glds16(sbA[1] + kb + vxA + ks * 8 * g.lda * 2, base + dstA[1]);
+        else if (d == 1 || d == 5) glds16(sbB[0] + kb + vxB + ks * 8 * g.ldb * 2, base + dstB[0]);
+        else glds16(sbB[1] + kb + vxB + ks * 8 * g.ldb * 2, base + dstB[1]);
+    };
+#else
     auto dma = [&](int tile, int d) {
         const int ks = (d >= 4) ? 1 : 0;
         const int kb = (tile * 64 + ks * 32) * 2;
@@ -254,6 +269,7 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
         else if (d == 1 || d == 5) glds16(sbB[0] + kb + voB, base + dstB[0]);
         else glds16(sbB[1] + kb + voB, base + dstB[1]);
     };
+#endif
 #else
     const __hip_bfloat16* srcA[2];
     const __hip_bfloat16* srcB[2];
