@@ -229,7 +229,11 @@ class WideClient:
         else:
             m.gemm(C, K, rows, dzo.data_ptr(), ldo, 0, h_in.data_ptr(), K, 0, self.gW[L - 1].data_ptr(), K, 0, 0, 0, 0,
                    0, 1.0, beta, self.dtype, self._wg_split(rows), self.wg_slab.data_ptr(), 0, s)
-        m.colsum(self.dz_out.data_ptr(), rows, C, C, self.gb[L - 1].data_ptr(), beta, s)
+        if self._skinny:  # head bias gradient, rows split 256 ways (the slab is free again here)
+            m.colsum_split(self.dz_out.data_ptr(), rows, C, self._sk_split(rows), self.sk_slab.data_ptr(),
+                           self.gb[L - 1].data_ptr(), beta, s)
+        else:
+            m.colsum(self.dz_out.data_ptr(), rows, C, C, self.gb[L - 1].data_ptr(), beta, s)
         if L >= 2 and pad:
             # dgrad into the last hidden layer: C classes zero-padded to K = 64 on the NT GEMM,
             # ReLU-masked, bf16 row-major + transposed outputs

@@ -29,6 +29,10 @@ struct GemmArgs {
 
 hipError_t gemm_launch(const GemmArgs& g, int dtype /*0 f32, 1 bf16*/, int a_kcontig, int b_kcontig, int epi,
                        int splits, int batch, hipStream_t s);
+// out[n] = beta*out[n] + sum_m X[m][n] for contiguous X [M][N], N <= 64, rows split `splits` ways
+// into slab[splits][N] and folded in fixed order.
+hipError_t colsum_split_launch(const float* X, int M, int N, int splits, float* slab, float* out, float beta,
+                               hipStream_t s);
 hipError_t splitk_reduce_launch(const float* slab, size_t stride, int splits, float* out, size_t n, float beta,
                                 hipStream_t s);
 hipError_t colsum_launch(const float* X, int M, int N, int ld, float* out, float beta, int batch, long long sX,

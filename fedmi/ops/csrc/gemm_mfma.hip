@@ -320,6 +320,38 @@ __global__ void __launch_bounds__(1024) colsum_flat_kernel(const float* __restri
     }
 }
 
+// The same few-column sums split over row ranges: block z folds rows [z*rc, (z+1)*rc) into
+// slab[z][N] (rc*N is a multiple of N, so element e of the range is still in column e % N), and
+// splitk_reduce folds the slabs in fixed order.  One block streaming 1 MiB alone took 130 us.
+__global__ void __launch_bounds__(1024) colsum_split_kernel(const float* __restrict__ X, int M, int N, int rc,
+                                                            float* __restrict__ slab) {
+    __shared__ float part[1024];
+    const int t = threadIdx.x, S = 1024 - 1024 % N, z = blockIdx.x;
+    const size_t e0 = (size_t)z * rc * N;
+    const size_t e1 = (size_t)min(M, (z + 1) * rc) * N;
+    float acc = 0.f;
+    if (t < S)
+        for (size_t e = e0 + t; e < e1; e += S) acc += X[e];
+    part[t] = acc;
+    __syncthreads();
+    if (t < N) {
+        float v = 0.f;
+        for (int i = t; i < S; i += N) v += part[i];
+        slab[(size_t)z * N + t] = v;
+    }
+}
+
+hipError_t colsum_split_launch(const float* X, int M, int N, int splits, float* slab, float* out, float beta,
+                               hipStream_t s) {
+    if (N < 1 || N > 64 || splits < 1 || M < 1) return hipErrorInvalidValue;
+    const int rc = (M + splits - 1) / splits;
+    splits = (M + rc - 1) / rc;
+    hipLaunchKernelGGL(colsum_split_kernel, dim3((unsigned)splits), dim3(1024), 0, s, X, M, N, rc, slab);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return splitk_reduce_launch(slab, (size_t)N, splits, out, (size_t)N, beta, s);
+}
+
 hipError_t colsum_launch(const float* X, int M, int N, int ld, float* out, float beta, int batch, long long sX,
                          long long sOut, const int* active, hipStream_t s) {
     if (N <= 64 && ld == N && batch == 1 && active == nullptr && (size_t)M * N >= 4096) {

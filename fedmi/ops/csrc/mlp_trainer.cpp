@@ -343,7 +343,14 @@ static void skinny_wgrad_py(uintptr_t W, int ldw, int Nw, uintptr_t S, int lds, 
                                  beta, reinterpret_cast<float*>(bias_out), reinterpret_cast<hipStream_t>(stream)));
 }
 
+static void colsum_split_py(uintptr_t X, int M, int N, int splits, uintptr_t slab, uintptr_t out, float beta,
+                            uintptr_t stream) {
+    TR_CHECK(colsum_split_launch(reinterpret_cast<const float*>(X), M, N, splits, reinterpret_cast<float*>(slab),
+                                 reinterpret_cast<float*>(out), beta, reinterpret_cast<hipStream_t>(stream)));
+}
+
 void register_trainer(py::module_& m) {
+    m.def("colsum_split", &colsum_split_py);
     m.def("skinny_wgrad", &skinny_wgrad_py);
     m.def("gemm_nt", &gemm_nt_py);
     m.def("gemm_nt_set_variant", &gemm_nt_set_variant);

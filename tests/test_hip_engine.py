@@ -222,6 +222,23 @@ def test_gemm_nt_bf16_epilogues():
     assert ((C - r2).abs().max() / r2.abs().max()).item() < 1e-5
 
 
+@pytest.mark.parametrize("M,N,splits", [(1000, 2, 7), (131072, 2, 256), (300, 14, 300)])
+def test_colsum_split(M, N, splits):
+    """Split few-column sums (wide head bias gradient) vs torch fp32, beta = 1."""
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(M)
+    X = torch.randn(M, N, device=dev)
+    out0 = torch.randn(N, device=dev)
+    out = out0.clone()
+    slab = torch.empty(splits * N, device=dev)
+    m.colsum_split(X.data_ptr(), M, N, splits, slab.data_ptr(), out.data_ptr(), 1.0, s)
+    torch.cuda.synchronize()
+    exp = out0 + X.double().sum(0).float()
+    assert torch.allclose(out, exp, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("C,trans,rows,splits", [(2, 0, 1000, 3), (14, 1, 4096, 16), (2, 0, 256, 1)])
 def test_skinny_wgrad_bf16(C, trans, rows, splits):
     """Skinny weight gradient (wide MLP layer 0 / logits head) vs an fp32 torch reference of the
