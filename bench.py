@@ -89,7 +89,14 @@ def main(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"],
                     help="MFMA operand type of the fused kernels (fp32 accumulate, fp32 master weights)")
     ap.add_argument("--no-convergence", action="store_true")
+    ap.add_argument("--config", default="c", choices=["c", "wide"],
+                    help="c: the reference [C] workload (default, the headline metric) | wide: BASELINE config 3, "
+                         "MLP 14-4096-4096-4096-2 on --wide-rows synthetic rows per client, bf16 NT GEMMs, "
+                         "per-layer FedAvg buckets over RCCL")
+    ap.add_argument("--wide-rows", type=int, default=131072)
     a = ap.parse_args(argv)
+    if a.config == "wide":
+        return main_wide(a)
 
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
     from fedmi.models.mlp import init_flat
@@ -158,6 +165,57 @@ def main(argv=None):
             "rounds_to_target": rtt,
         }
         print(json.dumps(rec), flush=True)
+    comm.close()
+
+
+def main_wide(a) -> None:
+    """BASELINE config 3 under the same contract: a step is one federated round of the wide
+    client (full-batch local Adam step over the shard + per-layer FedAvg buckets)."""
+    from fedmi.fl.wide import WideClient
+    from fedmi.parallel.comm import get_world
+    import torch.distributed as dist
+
+    comm = get_world(backend="rccl" if a.backend == "xgmi" else a.backend, device="cuda")
+    N = comm.size
+    if N != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
+    dims = [14, 4096, 4096, 4096, 2]
+    X, y = synth_shard(a.wide_rows, comm.rank, comm.device)
+    c = WideClient(X, y, dims, comm=comm if N > 1 else None, n_total=a.wide_rows * N, dtype="bf16", seed=0)
+
+    def barrier():
+        if N > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        c.run_round()
+    c.sync()
+    torch.cuda.synchronize(comm.device)
+    barrier()
+    torch.cuda.synchronize(comm.device)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        c.run_round()
+    c.sync()
+    torch.cuda.synchronize(comm.device)
+    barrier()
+    dt = time.perf_counter() - t0
+    if N > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = a.wide_rows * N * a.steps / dt
+    if comm.rank == 0:
+        print(json.dumps({
+            "metric": "train samples/s, wide-MLP FedAvg (BASELINE config 3)", "value": value,
+            "unit": "train samples/s (sum over clients; step = 1 federated round: full-batch Adam step + FedAvg)",
+            "n_gpus": N, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": f"synthetic income-shaped (device Philox), {a.wide_rows} rows/client; random-init weights",
+            "config": {"model": "MLP " + "-".join(map(str, dims)), "global_batch": a.wide_rows * N, "seq_len": 1,
+                       "parallelism": f"fedavg{N} (1 client/GPU, per-layer RCCL buckets)"},
+            "tflops_per_client": c.flops_per_round / (dt / a.steps) / 1e12,
+        }), flush=True)
     comm.close()
 
 
