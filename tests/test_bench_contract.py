@@ -1,0 +1,37 @@
+"""bench.py contract: one JSON line with the required keys, for the headline [C] config and
+the wide config (BASELINE config 3), on one GPU with a short run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(args):
+    r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert KEYS <= set(rec), KEYS - set(rec)
+    assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["ms_per_step"] > 0
+    return rec
+
+
+@pytest.mark.gpu
+def test_bench_headline_contract():
+    rec = _run(["--steps", "50", "--warmup", "10", "--no-convergence"])
+    assert rec["steps"] == 50 and rec["warmup"] == 10 and rec["dtype"] == "bf16"
+    assert rec["vs_baseline"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_wide_contract():
+    rec = _run(["--config", "wide", "--steps", "2", "--warmup", "1", "--wide-rows", "2048"])
+    assert rec["config"]["model"] == "MLP 14-4096-4096-4096-2"
+    assert rec["tflops_per_client"] > 0
