@@ -44,6 +44,8 @@ def parse_args(argv=None):
     ap.add_argument("--gamma", type=float, default=0.5)
     ap.add_argument("--local-steps", type=int, default=1)
     ap.add_argument("--fedprox-mu", type=float, default=0.0)
+    ap.add_argument("--participation", type=float, default=1.0,
+                    help="fraction of clients sampled per round (torch engine; 1.0 = all, the reference)")
     ap.add_argument("--patience", type=int, default=10)
     ap.add_argument("--tolerance", type=float, default=1e-4)
     ap.add_argument("--no-early-stop", action="store_true")
@@ -107,7 +109,7 @@ def main(argv=None):
     # every rank derives the same split locally: no broadcast of the table (C:243-246)
     ds = load_tabular(a.data, label=a.label, with_mean=True)
     cfg = EngineConfig(hidden=tuple(a.hidden), lr=a.lr, step_size=a.step_size, gamma=a.gamma,
-                       local_steps=a.local_steps, prox_mu=a.fedprox_mu, early_stop=not a.no_early_stop,
+                       local_steps=a.local_steps, prox_mu=a.fedprox_mu, participation=a.participation, early_stop=not a.no_early_stop,
                        patience=a.patience, tolerance=a.tolerance, max_rounds=a.rounds,
                        rows_per_block=a.rows_per_block, graph_rounds=a.graph_rounds, seed=a.seed,
                        debug=a.debug, dtype=a.dtype)

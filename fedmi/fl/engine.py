@@ -52,6 +52,11 @@ class EngineConfig:
     rows_per_block: int = 0         # R rows per workgroup of the fused kernels (16 | 32 | 64 (bf16); 0 = auto)
     graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
     seed: int = 0
+    # partial participation (client sampling): each round max(1, round(participation * world))
+    # clients, drawn by numpy's default Generator seeded with (seed, round) so every rank
+    # draws the same set, train and are averaged (weights n_i / sum of the sampled n_i); the
+    # others skip the local step and take the new global model.  Torch engine only.
+    participation: float = 1.0
     debug: bool = False             # eager, synchronised phases + non-finite checks every round
     dtype: str = "fp32"             # MFMA operand type of the fused kernels: 'fp32' | 'bf16'
     # one client: score round r's post-step model inside round r+1's train kernel (its forward
@@ -235,8 +240,19 @@ class TorchRoundEngine(RoundEngineBase):
         return confusion_matrix(yt.cpu().numpy(), pred.cpu().numpy(), self.n_classes)
 
     # -- step-by-step API (reference train_one_epoch / evaluate_local / federated_averaging)
+    def participants(self, r: int) -> np.ndarray:
+        """Ranks that train and are averaged in round r (all of them unless sampling)."""
+        frac = float(self.cfg.participation)
+        if frac >= 1.0 or self.world == 1:
+            return np.arange(self.world)
+        k = max(1, int(round(frac * self.world)))
+        rng = np.random.default_rng([int(self.cfg.seed), int(r)])
+        return np.sort(rng.choice(self.world, size=k, replace=False))
+
     def step_train(self) -> None:
-        self._loss = self.train_one_epoch()
+        r = self.rounds_issued
+        self._active = self.rank in self.participants(r)
+        self._loss = self.train_one_epoch() if self._active else 0.0
 
     def step_eval(self) -> np.ndarray:
         self._cm = self.confusion()
@@ -245,13 +261,22 @@ class TorchRoundEngine(RoundEngineBase):
     def step_aggregate(self) -> None:
         r = self.rounds_issued
         # one SUM all-reduce of [w * n_i/N | per-rank (confusion, loss) tails]
-        buf = torch.zeros(self.P + self.world * self.tail_stride, dtype=torch.float32)
-        buf[:self.P] = self.model.flat.detach().cpu() * self.agg_scale
+        sampling = float(self.cfg.participation) < 1.0 and self.world > 1
+        buf = torch.zeros(self.P + self.world * self.tail_stride + int(sampling), dtype=torch.float32)
+        if not sampling:
+            buf[:self.P] = self.model.flat.detach().cpu() * self.agg_scale
+        elif getattr(self, "_active", True):
+            # weights n_i * w_i and, in the last slot, n_i: divided by the sampled total after the sum
+            buf[:self.P] = self.model.flat.detach().cpu() * float(self.n_local)
+            buf[-1] = float(self.n_local)
         t0 = self.P + self.rank * self.tail_stride
         buf[t0:t0 + self.n_classes ** 2] = torch.as_tensor(self._cm.reshape(-1), dtype=torch.float32)
         buf[t0 + self.n_classes ** 2] = self._loss
         if self.comm is not None:
             self.comm.allreduce_(buf)
+        if sampling:
+            buf[:self.P] /= buf[-1]
+            buf = buf[:-1]
         with torch.no_grad():
             self.model.flat.copy_(buf[:self.P].to(self.device))
         self.global_params = self.model.flat.detach().clone()
@@ -375,6 +400,8 @@ class HipRoundEngine(RoundEngineBase):
         """``comm_buffers``: optional pair of float32 device views of length
         :meth:`comm_len` to use as the double-buffered FedAvg buffers (trial packing shares one
         all-reduce between engines by handing each a slice of one allocation)."""
+        if float(cfg.participation) < 1.0 and comm is not None and comm.size > 1:
+            raise NotImplementedError("partial participation runs on the torch engine (--engine torch)")
         from ..ops import native
         self.m = native()
         if device is None:

@@ -74,3 +74,59 @@ def test_fedavg_over_gloo(world):
     for k, r in enumerate(res):
         assert abs(per_rank[0, k, 0] - r[3]["accuracy"]) < 1e-12
     assert res[0][7]["accuracy"] > 0.6
+
+
+def _sampling_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    torch.set_num_threads(1)
+    from fedmi.data.tabular import load_tabular
+    from fedmi.fl.engine import EngineConfig, TorchRoundEngine
+    from fedmi.models.mlp import init_flat
+    from fedmi.parallel.comm import Comm
+    comm = Comm(backend="gloo", device="cpu")
+    ds = load_tabular()
+    idx = np.array_split(np.arange(len(ds.y_train)), world)[rank][: 500 + 300 * rank]  # unequal shards
+    cfg = EngineConfig(max_rounds=4, early_stop=False, participation=0.5, seed=3)
+    e = TorchRoundEngine(ds.X_train[idx], ds.y_train[idx], 2, cfg, comm, init_flat([14, 50, 200, 2], seed=0))
+    out = []
+    for r in range(3):
+        g0 = e.global_flat()
+        e.step_train()
+        local = e.local_flat()
+        e.step_eval()
+        e.step_aggregate()
+        out.append((list(e.participants(r)), g0, local, e.global_flat()))
+    q.put((rank, len(idx), out))
+    comm.close()
+
+
+def test_partial_participation_over_gloo():
+    """Client sampling (participation 0.5 of 4 clients): every rank draws the same 2 clients per
+    round, only they train, and the new global is their n_i-weighted mean."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sampling_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sizes = [r[1] for r in res]
+    for r in range(3):
+        parts = res[0][2][r][0]
+        assert len(parts) == 2 and all(x[2][r][0] == parts for x in res)
+        for k in range(world):
+            if k not in parts:   # skipped the local step
+                np.testing.assert_array_equal(res[k][2][r][2], res[k][2][r][1])
+        n = sum(sizes[k] for k in parts)
+        expect = sum(res[k][2][r][2] * (sizes[k] / n) for k in parts)
+        for x in res:
+            np.testing.assert_allclose(x[2][r][3], expect, rtol=1e-5, atol=1e-6)
+            np.testing.assert_array_equal(x[2][r][3], res[0][2][r][3])
+    # different rounds draw different sets (seeded per round)
+    assert len({tuple(res[0][2][r][0]) for r in range(3)}) > 1
