@@ -578,8 +578,13 @@ class HipRoundEngine(RoundEngineBase):
         self.sync_history()
         return {k + "_us": v / max(n, 1) for k, v in acc.items()}
 
-    def _issue(self, n: int) -> None:
-        """Issue rounds [rounds_issued, rounds_issued + n) on the current stream."""
+    def _issue(self, n: int, close: bool = True) -> None:
+        """Issue rounds [rounds_issued, rounds_issued + n) on the current stream.
+
+        ``close=False`` (lagged engines): the last round stays lagged -- its evaluation is
+        done by the next issued round's train kernel, so every round of the call can be a
+        graph replay.  The host must issue at least one more (closing) round before it reads
+        the history."""
         if self.cfg.debug:
             self._issue_debug(n)
             return
@@ -596,21 +601,48 @@ class HipRoundEngine(RoundEngineBase):
             return
         # lagged engines: graphs hold lagged rounds only, the last round of the call is eager and
         # evaluates itself (then every metric is in the buffers for the host)
-        lag = bool(self.engine.lagged)
+        lag = bool(self.engine.lagged) and close
         r = r0
         while r < r0 + n:
             left = r0 + n - r
             if (g >= 2 and r % 2 == 0 and (left > g if lag else left >= g)
                     and not self.engine.needs_eager_round()):
-                if not self._graph_ready:
-                    self.engine.capture(g, s, self._native_comm)
-                    self._graph_ready = True
+                self._ensure_graph(g)
                 self.engine.replay(s)
                 r += g
             else:
-                self.engine.run(r, 1, s, self._native_comm, close=(r == r0 + n - 1))
+                self.engine.run(r, 1, s, self._native_comm, close=(close and r == r0 + n - 1))
                 r += 1
         self.rounds_issued = r
+
+    def _ensure_graph(self, g: int) -> None:
+        if not self._graph_ready or self.engine.graph_rounds() != g:
+            self.engine.capture(g, self._stream(), self._native_comm)
+            self._graph_ready = True
+
+    def prime_graph(self, g: int) -> int:
+        """Bring the engine to the steady state of a ``g``-round graph before a timed region:
+        issue (uncounted by the caller) eager rounds until the next round is even and may start
+        a graph, capture + instantiate the graph and replay it once.  Afterwards
+        ``_issue(k * g, close=False)`` is ``k`` graph replays.  Returns the rounds issued."""
+        if g < 2 or g % 2:
+            raise ValueError("graph rounds must be an even number >= 2")
+        if self.world > 1 and not self._engine_reduces():
+            raise RuntimeError("prime_graph: rounds aggregated from Python are not captured")
+        self.cfg.graph_rounds = g
+        r0 = self.rounds_issued
+        s = self._stream()
+        for _ in range(4):
+            if self.rounds_issued % 2 == 0 and not self.engine.needs_eager_round():
+                break
+            self.engine.run(self.rounds_issued, 1, s, self._native_comm, close=False)
+            self.rounds_issued += 1
+        else:
+            raise RuntimeError("prime_graph: engine did not reach a graph-capturable state")
+        self._ensure_graph(g)
+        self.engine.replay(s)
+        self.rounds_issued += g
+        return self.rounds_issued - r0
 
     def _read_state(self, idx: int) -> np.ndarray:
         self.stream.synchronize()

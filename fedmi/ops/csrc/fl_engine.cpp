@@ -218,6 +218,7 @@ class FLEngine {
         if (lag_req) c_.lag_off = d_.Pimg + c_.tail_len;
         comm_len_ = d_.Pimg + c_.tail_len * (lag_req ? 2 : 1);
         const bool emulate = cfg.contains("emulate_clients") && cfg["emulate_clients"].cast<bool>();
+        emulate_ = emulate;
         // (with early stopping the rounds are lagged only when the FedAvg runs inside the Adam
         // kernel, which then also exchanges and folds the metrics in time: see lagged())
         lag_ok_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !fused_ &&
@@ -646,7 +647,9 @@ class FLEngine {
     // all-reduce's send buffer, or, for RCCL, the parameter buffer it reduces in place.
     float* comm_buf(int r) const { return peer_ != nullptr ? peer_->send((r + 1) & 1) : pbuf_[(r + 1) & 1]; }
     void issue_allreduce(int r, hipStream_t s, RcclComm* comm) {
-        if (c_.world < 2 && peer_ == nullptr) return;
+        // (one client: FedAvg is the identity; an emulating engine still issues the collective,
+        // e.g. a one-rank RCCL all-reduce, so the multi-client round shape runs on one GPU)
+        if (c_.world < 2 && peer_ == nullptr && !(emulate_ && comm != nullptr)) return;
         if (peer_ != nullptr)
             HIP_CHECK(peer_->launch((r + 1) & 1, pbuf_[(r + 1) & 1], dtype_ == 1 ? &pp_ : nullptr, s));
         else if (comm != nullptr)
@@ -712,6 +715,7 @@ class FLEngine {
     float* lagbuf_ = nullptr;  // FL_EVAL_LAGGED count + loss carry-over
     long long comm_len_ = 0;   // floats of a comm buffer: image + tails (+ lag region)
     bool lag_ok_ = false;      // lagged rounds possible (layout, clients, bf16): see lagged()
+    bool emulate_ = false;     // one process stands in for a multi-client round (measurements, tests)
     bool xchg_ = false;        // lagged rounds: FedAvg inside the Adam kernel (no all-reduce kernel)
     bool prev_lagged_ = false; // the last issued round had no evaluation of its own
     bool prev_scored_ = false; // the last issued round's train kernel scored its predecessor

@@ -12,14 +12,14 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config"}
 
 
-def _run(args):
+def _run(args, n=1):
     r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert KEYS <= set(rec), KEYS - set(rec)
-    assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["ms_per_step"] > 0
+    assert rec["n_gpus"] == n and rec["value"] > 0 and rec["ms_per_step"] > 0
     return rec
 
 
@@ -28,6 +28,17 @@ def test_bench_headline_contract():
     rec = _run(["--steps", "50", "--warmup", "10", "--no-convergence"])
     assert rec["steps"] == 50 and rec["warmup"] == 10 and rec["dtype"] == "bf16"
     assert rec["vs_baseline"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_shared_gpu():
+    """--gpus 2 without torchrun: bench.py starts 2 ranks itself (on one GPU with --share-gpu);
+    the N > 1 round (lagged evaluation, FedAvg inside the Adam kernel over the peer protocol)
+    runs and rank 0 alone prints the JSON line."""
+    rec = _run(["--gpus", "2", "--share-gpu", "--steps", "40", "--warmup", "5", "--no-convergence",
+                "--no-anchor"], n=2)
+    assert rec["config"]["data_plane"] == "xgmi-oneshot+adam", rec["config"]
+    assert rec["config"]["share_gpu"] is True
 
 
 @pytest.mark.gpu

@@ -1,0 +1,124 @@
+"""The engine-owned RCCL communicator (``RcclComm`` in fedmi/ops/csrc/fl_engine.cpp) on the
+one-GPU box: RCCL cannot put two ranks on one device, so these run a ONE-rank communicator --
+every call still goes through ``ncclCommInitRank`` / ``ncclAllReduce`` / ``ncclBroadcast`` /
+``ncclAllGather`` on a real stream, eagerly and inside captured HIP graphs:
+
+* raw collectives (f32 / f64 all-reduce, byte broadcast, all-gather), eager and captured;
+* the fused round engine issuing its FedAvg all-reduce through RCCL (an emulating engine:
+  ``emulate_clients`` keeps the multi-client round shape at world 1), eager and inside
+  ``FLEngine.capture``: bit-identical to the same engine without a collective (a one-rank
+  SUM is the identity);
+* the wide client's per-layer FedAvg buckets through ``Comm.allreduce_`` -> RCCL.
+
+The multi-rank RCCL path itself is exercised by the driver's 8-GPU scaling run
+(``bench.py --backend rccl`` / ``FEDMI_DATA_PLANE=rccl``).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rccl():
+    import torch
+    from fedmi.ops import native
+    m = native()
+    torch.cuda.set_device(0)
+    return m, m.RcclComm(1, 0, m.RcclComm.unique_id(), 0)
+
+
+def test_rccl_raw_collectives_eager_and_graph():
+    import torch
+    m, rc = _rccl()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    x = torch.randn(50003, device=dev)
+    ref = x.clone()
+    xd = torch.randn(1001, dtype=torch.float64, device=dev)
+    refd = xd.clone()
+    b = torch.arange(256, dtype=torch.uint8, device=dev)
+    out = torch.empty_like(x)
+    with torch.cuda.stream(s):
+        rc.allreduce_f32(x.data_ptr(), x.numel(), s.cuda_stream)
+        rc.allreduce_f64(xd.data_ptr(), xd.numel(), s.cuda_stream)
+        rc.broadcast_bytes(b.data_ptr(), b.numel(), 0, s.cuda_stream)
+        rc.allgather_f32(x.data_ptr(), out.data_ptr(), x.numel(), s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(x, ref) and torch.equal(xd, refd) and torch.equal(out, ref)
+    assert torch.equal(b.cpu(), torch.arange(256, dtype=torch.uint8))
+    # captured: all-reduce of a buffer that a captured kernel rewrites before every replay
+    g = torch.cuda.CUDAGraph()
+    y = torch.zeros(4096, device=dev)
+    with torch.cuda.graph(g, stream=s):
+        y.add_(1.0)
+        rc.allreduce_f32(y.data_ptr(), y.numel(), torch.cuda.current_stream(dev).cuda_stream)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert float(y.min()) == float(y.max()) == 3.0  # capture does not execute: 3 replays
+    rc.destroy()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_round_engine_fedavg_through_rccl(dtype):
+    """The engine's RCCL path (issue_allreduce -> ncclAllReduce), eager + graph-captured rounds."""
+    import torch
+    from fedmi.data.synthetic import make_income_like
+    from fedmi.fl.engine import EngineConfig, HipRoundEngine
+    from fedmi.models.mlp import init_flat
+    m, rc = _rccl()
+    X, y = make_income_like(2000, seed=3)
+    flat = init_flat([14, 50, 200, 2], 1)
+    res = []
+    for use_rccl in (True, False):
+        cfg = EngineConfig(max_rounds=40, early_stop=False, dtype=dtype, graph_rounds=4, fused_eval=False)
+        e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=True)
+        if use_rccl:
+            e._native_comm = rc
+        e.run(3)          # eager
+        e.run(13)         # graph chunks (capture passes the communicator)
+        e.sync_history()
+        assert e.history()["rounds_run"] == 16
+        res.append((e.global_flat(), e.history()["global"], e.history()["loss"]))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_array_equal(res[0][2], res[1][2])
+    torch.cuda.synchronize()
+    rc.destroy()
+
+
+def test_wide_aggregate_through_rccl():
+    """WideClient.aggregate: per-layer buckets scaled by n_i/N and all-reduced over RCCL on the
+    comm stream (one rank: the scale is 1, so the weights must come back unchanged)."""
+    import torch
+    from fedmi.data.synthetic import make_income_like
+    from fedmi.fl.wide import WideClient
+    m, rc = _rccl()
+    dev = torch.device("cuda", 0)
+    Xn, yn = make_income_like(1024, seed=5)
+    X, y = torch.as_tensor(Xn, device=dev), torch.as_tensor(yn, device=dev)
+    c = WideClient(X, y, [14, 256, 128, 2], comm=None, micro_batch=512, dtype="bf16")
+    c.local_step()
+    c.stream.synchronize()
+    before = c.params.clone()
+    # force the multi-client aggregate path with the one-rank RCCL communicator
+    c.world, c.comm = 2, _OneRankDevComm(rc)
+    c.aggregate()
+    c.sync()
+    torch.cuda.synchronize()
+    assert c.comm.calls == c.L
+    assert torch.equal(c.params, before)
+    rc.destroy()
+
+
+class _OneRankDevComm:
+    """Comm stand-in whose device all-reduce is the one-rank RCCL communicator."""
+
+    def __init__(self, rc):
+        self.rc, self.calls, self.size, self.rank = rc, 0, 1, 0
+
+    def allreduce_(self, t):
+        import torch
+        self.rc.allreduce_f32(t.data_ptr(), t.numel(), torch.cuda.current_stream(t.device).cuda_stream)
+        self.calls += 1
+        return t
