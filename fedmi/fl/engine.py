@@ -258,9 +258,9 @@ class TorchRoundEngine(RoundEngineBase):
         self._cm = self.confusion()
         return self._cm
 
-    def step_aggregate(self) -> None:
-        r = self.rounds_issued
-        # one SUM all-reduce of [w * n_i/N | per-rank (confusion, loss) tails]
+    def fedavg_contribution(self) -> torch.Tensor:
+        """This client's operand of the round's SUM all-reduce:
+        [w * n_i/N | per-rank (confusion, loss) tails] (+ n_i when sampling clients)."""
         sampling = float(self.cfg.participation) < 1.0 and self.world > 1
         buf = torch.zeros(self.P + self.world * self.tail_stride + int(sampling), dtype=torch.float32)
         if not sampling:
@@ -272,8 +272,19 @@ class TorchRoundEngine(RoundEngineBase):
         t0 = self.P + self.rank * self.tail_stride
         buf[t0:t0 + self.n_classes ** 2] = torch.as_tensor(self._cm.reshape(-1), dtype=torch.float32)
         buf[t0 + self.n_classes ** 2] = self._loss
+        return buf
+
+    def step_aggregate(self) -> None:
+        # one SUM all-reduce of [w * n_i/N | per-rank (confusion, loss) tails]
+        buf = self.fedavg_contribution()
         if self.comm is not None:
             self.comm.allreduce_(buf)
+        self.fedavg_apply(buf)
+
+    def fedavg_apply(self, buf: torch.Tensor) -> None:
+        """Adopt the all-reduced buffer: new global weights, metrics, early-stop rule."""
+        r = self.rounds_issued
+        sampling = float(self.cfg.participation) < 1.0 and self.world > 1
         if sampling:
             buf[:self.P] /= buf[-1]
             buf = buf[:-1]

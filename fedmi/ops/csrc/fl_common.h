@@ -54,17 +54,31 @@ struct MLPDesc {
 // hit 16 distinct bank slots.  W_l has kp[l+1] rows (the dgrad contraction runs over its
 // padded fan-out), activations / deltas have R rows.  Transposed operands (wgrad over rows,
 // dgrad over W's rows) are read with ds_read_b64_tr_b16 from the same images.
+//
+// Split-bf16 forward ("bf16x3").  Every forward pass computes z = a.W^T as
+// a_hi.W_hi^T + (a_lo.W_hi^T + a_hi.W_lo^T) with x_hi = bf16(x), x_lo = bf16(x - x_hi), fp32
+// accumulation: ~16 significant bits per product instead of 8.  The backward pass stays plain
+// bf16 (hi parts).  Reason: the reference's early-stop rule (C:181-192, atol 1e-4 on 8000-row
+// accuracies) needs 10 rounds without a single prediction flip; with 8-bit scoring every
+// bf16 rounding step of a changing weight flips borderline rows and the rule never fires
+// (tools/bf16_es_emulate.py: split-bf16 forward stops at rounds 175-238, the fp32 oracle at
+// 157-227, the reference at 149-243).  The lo images of the weights sit in the parameter
+// region `wlo_delta` bytes after their hi images (same layout); the lo parts of the layer
+// inputs live in `alo_off` buffers (X lo: its own buffer; hidden layers: the backward delta
+// buffers, unused during the forward pass).
 struct MLPDescB {
     int kp[FL_MAX_LAYERS + 1];        // roundup32(dim[l])
     int lda[FL_MAX_LAYERS + 1];       // kp[l] + 8: row stride (elements) of act_l, D_l, and W_l rows
-    int w_off[FL_MAX_LAYERS];         // W_l  bf16 [kp[l+1]][lda[l]]
+    int w_off[FL_MAX_LAYERS];         // W_l  bf16 [kp[l+1]][lda[l]]  (hi parts)
     int bias_off[FL_MAX_LAYERS];      // b_l  fp32 [kp[l+1]] (zero padded)
-    int act_off[FL_MAX_LAYERS + 1];   // act_l bf16 [R][lda[l]]   (l < L)
+    int wlo_delta;                    // W_l lo parts at w_off[l] + wlo_delta (same layout)
+    int act_off[FL_MAX_LAYERS + 1];   // act_l bf16 [R][lda[l]]   (l < L), hi parts
+    int alo_off[FL_MAX_LAYERS + 1];   // act_l lo parts bf16 [R][lda[l]] (l < L; forward pass only)
     int dlt_off[FL_MAX_LAYERS + 1];   // D_l  bf16 [R][lda[l]]    (1 <= l <= L): dLoss/dz_l
     int logit_off;                    // fp32 [R][16] classifier logits
     int cm_off;                       // int [16][16] confusion counters (fused evaluation)
     int item_base[FL_MAX_LAYERS + 1]; // packing: prefix sums of the 8-element items of each W_l
-    int param_off;                    // start of the parameter region (all W_l then all b_l):
+    int param_off;                    // start of the parameter region (all W_l hi, all b_l, all W_l lo):
     int param_bytes;                  // it is stored pre-packed in global memory and staged by a copy
     int lds_bytes;
 };
@@ -155,13 +169,14 @@ struct FLBuffers {
 #define FL_EVAL_CLASSIC 0
 #define FL_EVAL_FUSED 1
 #define FL_EVAL_FUSED_SKIP 2
-//   FL_EVAL_LAGGED  : several clients, early stopping off: the train kernel of round r also
-//                     scores round r-1's post-step LOCAL model (a second forward pass on the
-//                     staged local image) into the local count buffer; the Adam kernel
-//                     publishes those counts (+ round r-1's loss) in region A of round r's
-//                     all-reduce, so no round needs a separate evaluation.  The metrics of
-//                     round r-1 are folded at round r+1 -- one round later, which only
-//                     matters to a stop decision, hence early stopping off.
+//   FL_EVAL_LAGGED  : several clients: the train kernel of round r first scores round r-1's
+//                     post-step LOCAL model (a forward pass on the staged local image, before
+//                     the round's own weights replace it in LDS) into the local count buffer;
+//                     the Adam kernel publishes those counts (+ round r-1's loss) in region A
+//                     of round r's exchange, so no round needs a separate evaluation kernel.
+//                     With the Adam-fused exchange region A is exchanged and folded inside
+//                     round r's Adam kernel (in time for early stopping); riding an external
+//                     all-reduce it is folded one round later (early stopping off).
 #define FL_EVAL_LAGGED 3
 // Metric regions of an all-reduced comm buffer that a fold consumes (fl_device.h).
 #define FL_FOLD_A 1  // lag region: round next_round - 2
@@ -194,13 +209,12 @@ hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                               const float* pg, const FLState* st_in, FLState* st_out,
                               hipStream_t s, int mask = FL_FOLD_B);
-// bf16-operand variants (fp32 accumulate, fp32 master weights / slab / Adam state).
-// `el` (FL_EVAL_LAGGED): layout whose parameter region is the second image (after e's), and
-// whose lds_bytes covers both.
+// bf16-operand variants (split-bf16 forward, bf16 backward, fp32 accumulate, fp32 master
+// weights / slab / Adam state).
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                 const float* pg, const FLState* st_in, FLState* st_out, int local_step,
                                 hipStream_t s, bool stage_local = false, int mode = FL_EVAL_CLASSIC,
-                                float* cm_out = nullptr, int fold_mask = FL_FOLD_B, const MLPDescB* el = nullptr);
+                                float* cm_out = nullptr, int fold_mask = FL_FOLD_B);
 hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_set_lds_limit_bf16(size_t bytes);

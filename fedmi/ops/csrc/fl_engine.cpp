@@ -13,6 +13,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -172,9 +173,10 @@ class FLEngine {
             HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));
         } else {
             build_bf16_layout();
-            if ((size_t)e_.lds_bytes > FL_LDS_DYNAMIC_MAX)
+            const size_t need = (size_t)std::max(e_.lds_bytes, ev_.lds_bytes);
+            if (need > FL_LDS_DYNAMIC_MAX)
                 throw std::runtime_error("FLEngine(bf16): model exceeds LDS; use a smaller R or the layered path");
-            HIP_CHECK(fl_set_lds_limit_bf16((size_t)e_.lds_bytes));
+            HIP_CHECK(fl_set_lds_limit_bf16(need));
         }
 
         c_.n_rows = cfg["n_rows"].cast<int>();
@@ -221,9 +223,8 @@ class FLEngine {
         emulate_ = emulate;
         // (with early stopping the rounds are lagged only when the FedAvg runs inside the Adam
         // kernel, which then also exchanges and folds the metrics in time: see lagged())
-        lag_ok_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !fused_ &&
-                  (size_t)el_.lds_bytes <= FL_LDS_DYNAMIC_MAX;
-        if (lag_ok_) HIP_CHECK(fl_set_lds_limit_bf16((size_t)el_.lds_bytes));
+        // (the lagged train kernel scores the previous local model in the train layout itself)
+        lag_ok_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !fused_;
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
@@ -410,6 +411,7 @@ class FLEngine {
         std::memset(&pp_, 0, sizeof(pp_));
         if (dtype_ == 1) {
             pp_.pk = b_.pk_global;
+            pp_.wlo_delta = e_.wlo_delta;
             pp_.L = d_.L;
             for (int l = 0; l < d_.L; ++l) {
                 const int K = d_.dim[l], N = d_.dim[l + 1];
@@ -524,43 +526,36 @@ class FLEngine {
         for (int l = 1; l <= L; ++l) e_.dlt_off[l] = take(R * e_.lda[l] * 2);
         e_.logit_off = take(R * 16 * 4);
         e_.cm_off = take(FL_CM_INTS * 4);
+        // split-bf16 forward: lo parts of the layer inputs -- X in its own buffer, the hidden
+        // activations in the delta buffers (same [R][lda] shape, free until the backward pass)
+        e_.alo_off[0] = take(R * e_.lda[0] * 2);
+        for (int l = 1; l < L; ++l) e_.alo_off[l] = e_.dlt_off[l];
+        // parameter region: W hi images, biases, W lo images (each W size is a multiple of 16
+        // bytes, so the lo images sit at one constant offset from their hi images)
         e_.param_off = off;
         for (int l = 0; l < L; ++l) e_.w_off[l] = take(e_.kp[l + 1] * e_.lda[l] * 2);
         for (int l = 0; l < L; ++l) e_.bias_off[l] = take(e_.kp[l + 1] * 4);
+        e_.wlo_delta = off - e_.w_off[0];
+        for (int l = 0; l < L; ++l) take(e_.kp[l + 1] * e_.lda[l] * 2);
         e_.param_bytes = off - e_.param_off;
         e_.lds_bytes = off;
         e_.item_base[0] = 0;
         for (int l = 0; l < L; ++l) e_.item_base[l + 1] = e_.item_base[l] + e_.kp[l + 1] * (e_.kp[l] >> 3);
-        // Evaluation kernels run the forward pass only: their layout drops the delta buffers,
-        // which brings a 14-50-200-2 workgroup at R = 32 under half the CU's LDS (two blocks
-        // per CU), so the fused evaluation + FedAvg grid (evaluation blocks + all-reduce
-        // blocks > 256) stays resident in one wave.
+        // Evaluation kernels run the forward pass only: their layout has no delta buffers, so the
+        // lo parts of the hidden activations get buffers of their own.
         ev_ = e_;
         off = 0;
         for (int l = 0; l < L; ++l) ev_.act_off[l] = take(R * e_.lda[l] * 2);
         for (int l = 1; l <= L; ++l) ev_.dlt_off[l] = -1;
         ev_.logit_off = take(R * 16 * 4);
         ev_.cm_off = take(FL_CM_INTS * 4);
+        for (int l = 0; l < L; ++l) ev_.alo_off[l] = take(R * e_.lda[l] * 2);
         ev_.param_off = off;
         for (int l = 0; l < L; ++l) {
             ev_.w_off[l] = e_.w_off[l] - e_.param_off + ev_.param_off;
             ev_.bias_off[l] = e_.bias_off[l] - e_.param_off + ev_.param_off;
         }
         ev_.lds_bytes = ev_.param_off + e_.param_bytes;
-        // FL_EVAL_LAGGED: the train layout plus a second parameter region (the previous
-        // round's local model) after it; el_ addresses that region
-        el_ = e_;
-        el_.param_off = e_.lds_bytes;
-        for (int l = 0; l < L; ++l) {
-            el_.w_off[l] = e_.w_off[l] - e_.param_off + el_.param_off;
-            el_.bias_off[l] = e_.bias_off[l] - e_.param_off + el_.param_off;
-        }
-        el_.lds_bytes = el_.param_off + e_.param_bytes;
-        // ... and the scoring pass's activations: the delta buffers (unused during the
-        // forward pass, same shapes), its logits in a region after the second image
-        for (int l = 1; l < L; ++l) el_.act_off[l] = e_.dlt_off[l];
-        el_.logit_off = el_.lds_bytes;
-        el_.lds_bytes += R * 16 * 4;
     }
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
                       int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr, int fold_mask = FL_FOLD_B) {
@@ -576,8 +571,7 @@ class FLEngine {
             const bool packed = solo || (peer_ != nullptr && !need_pack_);
             if (ls == 0 && !packed) HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
             need_pack_ = false;
-            HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo, mode, cm_out, fold_mask,
-                                           mode == FL_EVAL_LAGGED ? &el_ : nullptr));
+            HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo, mode, cm_out, fold_mask));
         }
     }
     void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
@@ -708,7 +702,6 @@ class FLEngine {
     MLPDesc d_;
     MLPDescB e_;
     MLPDescB ev_;  // evaluation-only layout of e_ (no delta buffers)
-    MLPDescB el_;  // e_ plus a second parameter region (FL_EVAL_LAGGED scoring)
     int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
     char* pk_ = nullptr;
     float* sched_ = nullptr;  // Adam/StepLR scalars per optimizer step

@@ -407,13 +407,28 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
 // written (it stays 0 in every buffer).  The last block writes this rank's metric tail.
 #define ADAM_WAVES 16
 #define ADAM_DEPTH 16
+// bf16 mode: parameter -> packed LDS-layout image(s).  A weight is stored as its bf16 hi part
+// and, `wlo_delta` bytes further, its lo part bf16(p - hi) (split-bf16 forward, fl_common.h);
+// a bias stays fp32.
+__device__ __forceinline__ void pack_store(char* img, int pk, bool is_bias, int wlo_delta, float p) {
+    if (is_bias) {
+        *reinterpret_cast<float*>(img + pk) = p;
+        return;
+    }
+    const uint32_t u = __float_as_uint(p);
+    const uint32_t h = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+    const uint32_t r = __float_as_uint(p - __uint_as_float(h << 16));
+    *reinterpret_cast<uint16_t*>(img + pk) = (uint16_t)h;
+    *reinterpret_cast<uint16_t*>(img + pk + wlo_delta) = (uint16_t)((r + 0x7fffu + ((r >> 16) & 1u)) >> 16);
+}
+
 // Adam step of one parameter (wave 0 lane of fl_adam_kernel) from the block's partial sums.
 // `p`, `m`, `v`, `anc`: the parameter, its Adam moments and its anchor value, loaded by the
 // caller at the start of the kernel (their latency hides behind the slab loads).
 __device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& b, float* __restrict__ comm,
                                             const FLState& S, int local_step, int last_local_step, int pack, int j,
-                                            int pk, bool is_bias, float (*part)[64], int lane, float p, float m,
-                                            float v, float anc) {
+                                            int pk, bool is_bias, int wlo_delta, float (*part)[64], int lane, float p,
+                                            float m, float v, float anc) {
     float g = 0.f;
 #pragma unroll
     for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
@@ -432,14 +447,7 @@ __device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& 
     b.m[j] = m;
     b.v[j] = v;
     b.local[j] = p;
-    if (pack) {
-        if (is_bias) {
-            *reinterpret_cast<float*>(b.pk_local + pk) = p;
-        } else {
-            const uint32_t u = __float_as_uint(p);
-            *reinterpret_cast<uint16_t*>(b.pk_local + pk) = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-        }
-    }
+    if (pack) pack_store(b.pk_local, pk, is_bias, wlo_delta, p);
     if (last_local_step) comm[j] = p * c.agg_scale;
 }
 
@@ -644,8 +652,8 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         if (!S.live) {
             if (last_local_step) comm[j] = (c.rank == 0) ? a0 : 0.f;
         } else {
-            adam_update(c, b, comm, S, local_step, last_local_step, pack, j, pk, is_bias, part, lane, p0, m0, v0,
-                        a0);
+            adam_update(c, b, comm, S, local_step, last_local_step, pack, j, pk, is_bias, e.wlo_delta, part, lane, p0,
+                        m0, v0, a0);
         }
     }
     if (xchg) {
@@ -655,14 +663,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         if (valid) {
             const float gsum = peer_pull_sum(pa, j);
             pa.out[j] = gsum;
-            if (pack) {
-                if (is_bias) {
-                    *reinterpret_cast<float*>(b.pk_global + pk) = gsum;
-                } else {
-                    const uint32_t u = __float_as_uint(gsum);
-                    *reinterpret_cast<uint16_t*>(b.pk_global + pk) = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-                }
-            }
+            if (pack) pack_store(b.pk_global, pk, is_bias, e.wlo_delta, gsum);
         }
     }
 }

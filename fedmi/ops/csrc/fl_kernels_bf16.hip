@@ -3,9 +3,13 @@
 // Same round structure, state machine, slab and Adam kernel as the fp32 path
 // (fl_kernels.hip); only the per-workgroup GEMM work changes:
 //
-//   * the fp32 parameter image (global, all-reduced in fp32) is converted to a bf16 LDS image
-//     while staging; activations and deltas live in LDS as bf16, accumulation is fp32 and the
-//     weight gradients written to the slab are fp32 (fp32 master weights + Adam state);
+//   * the fp32 parameter image (global, all-reduced in fp32) is kept pre-packed as a bf16 LDS
+//     image (hi parts, fp32 biases, lo parts); activations and deltas live in LDS as bf16,
+//     accumulation is fp32 and the weight gradients written to the slab are fp32 (fp32 master
+//     weights + Adam state);
+//   * the forward pass is split-bf16 (fl_common.h): a_hi.W_hi + a_lo.W_hi + a_hi.W_lo, so the
+//     logits that score the model (and drive the early-stop rule) carry ~16 significant bits;
+//     the backward pass multiplies the hi parts only;
 //   * all GEMMs run on v_mfma_f32_16x16x32_bf16 (16x the fp32 MFMA rate per FLOP):
 //       fwd    z  = act . W^T      A = act rows (ds_read_b128), B = W rows (ds_read_b128)
 //       dgrad  D  = D' . W         A = D' rows (ds_read_b128), B = W^T  via ds_read_b64_tr_b16
@@ -35,6 +39,9 @@ __device__ __forceinline__ uint32_t bf16_bits(float x) {
 }
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) { return bf16_bits(a) | (bf16_bits(b) << 16); }
+// lo parts of the split-bf16 representation: bf16(x - bf16(x))
+__device__ __forceinline__ uint32_t lo_bits(float x) { return bf16_bits(x - bf16_to_f32((uint16_t)bf16_bits(x))); }
+__device__ __forceinline__ uint32_t pack_lo_bf16x2(float a, float b) { return lo_bits(a) | (lo_bits(b) << 16); }
 
 __device__ __forceinline__ bf16x8 ld128(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
@@ -72,14 +79,18 @@ __global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restri
         const int n = loc / nch, ch = loc - n * nch;
         const int K16 = (d.dim[l] + 15) & ~15, N16 = (d.dim[l + 1] + 15) & ~15;
         const bool ok = n < N16 && 8 * ch < K16;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        uint4 v = make_uint4(0u, 0u, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
         if (ok) {
             const float4* src = reinterpret_cast<const float4*>(params + d.iw_off[l] + n * fl_ldw(d.dim[l]) + 8 * ch);
-            const float4 lo = src[0], hi = src[1];
-            v = make_uint4(pack_bf16x2(lo.x, lo.y), pack_bf16x2(lo.z, lo.w), pack_bf16x2(hi.x, hi.y),
-                           pack_bf16x2(hi.z, hi.w));
+            const float4 p0 = src[0], p1 = src[1];
+            v = make_uint4(pack_bf16x2(p0.x, p0.y), pack_bf16x2(p0.z, p0.w), pack_bf16x2(p1.x, p1.y),
+                           pack_bf16x2(p1.z, p1.w));
+            w = make_uint4(pack_lo_bf16x2(p0.x, p0.y), pack_lo_bf16x2(p0.z, p0.w), pack_lo_bf16x2(p1.x, p1.y),
+                           pack_lo_bf16x2(p1.z, p1.w));
         }
-        *reinterpret_cast<uint4*>(out + e.w_off[l] - e.param_off + (n * e.lda[l] + 8 * ch) * 2) = v;
+        char* dst = out + e.w_off[l] - e.param_off + (n * e.lda[l] + 8 * ch) * 2;
+        *reinterpret_cast<uint4*>(dst) = v;
+        *reinterpret_cast<uint4*>(dst + e.wlo_delta) = w;
         return;
     }
     int bid = id - total;
@@ -95,16 +106,14 @@ __global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restri
 
 // Stage the packed parameter region AND this block's input rows with every global load in
 // flight before the first LDS store: the two ~1 us L2 latencies overlap instead of adding.
-// Loads beyond STAGE_UNROLL per thread (large models) fall back to a loop.
-#define STAGE_P_UNROLL 4
+// Loads beyond STAGE_UNROLL per thread (large models) fall back to a loop.  The rows go to LDS
+// split: act_0 = bf16(x), alo_0 = bf16(x - bf16(x)).
+#define STAGE_P_UNROLL 8
 #define STAGE_X_UNROLL 2
-// `packed2` (optional): a second packed image staged at `param2_off` in the same load batch
-// (FL_EVAL_LAGGED: the previous round's local model beside this round's input weights).
 template <int RT>
 __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const char* __restrict__ packed,
                                                        const float* __restrict__ X, int n_rows, int F, int row0,
-                                                       char* lds, const char* __restrict__ packed2 = nullptr,
-                                                       int param2_off = 0) {
+                                                       char* lds) {
     const uint4* src = reinterpret_cast<const uint4*>(packed);
     uint4* dst = reinterpret_cast<uint4*>(lds + e.param_off);
     const int n16 = e.param_bytes >> 4;
@@ -112,21 +121,12 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
     const int nx = RT * 16 * kp;
     uint4 pv[STAGE_P_UNROLL];
     float xv[STAGE_X_UNROLL];
-    uint4 pv2[STAGE_P_UNROLL];
-    const uint4* src2 = reinterpret_cast<const uint4*>(packed2 != nullptr ? packed2 : packed);
     // unpredicated loads (clamped indices): a conditionally written register array is
     // demoted to scratch by the compiler
 #pragma unroll
     for (int u = 0; u < STAGE_P_UNROLL; ++u) {
         const int i = threadIdx.x + u * FL_THREADS;
         pv[u] = src[i < n16 ? i : 0];
-    }
-    if (packed2 != nullptr) {
-#pragma unroll
-        for (int u = 0; u < STAGE_P_UNROLL; ++u) {
-            const int i = threadIdx.x + u * FL_THREADS;
-            pv2[u] = src2[i < n16 ? i : 0];
-        }
     }
 #pragma unroll
     for (int u = 0; u < STAGE_X_UNROLL; ++u) {
@@ -149,33 +149,53 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
         const int i = threadIdx.x + u * FL_THREADS;
         if (i < n16) dst[i] = pv[u];
     }
-    if (packed2 != nullptr) {
-        uint4* dst2 = reinterpret_cast<uint4*>(lds + param2_off);
-#pragma unroll
-        for (int u = 0; u < STAGE_P_UNROLL; ++u) asm volatile("" ::"v"(pv2[u].x), "v"(pv2[u].y), "v"(pv2[u].z), "v"(pv2[u].w));
-        for (int i = threadIdx.x + STAGE_P_UNROLL * FL_THREADS; i < n16; i += FL_THREADS) dst2[i] = src2[i];
-#pragma unroll
-        for (int u = 0; u < STAGE_P_UNROLL; ++u) {
-            const int i = threadIdx.x + u * FL_THREADS;
-            if (i < n16) dst2[i] = pv2[u];
-        }
-    }
     uint16_t* a = reinterpret_cast<uint16_t*>(lds + e.act_off[0]);
+    uint16_t* alo = reinterpret_cast<uint16_t*>(lds + e.alo_off[0]);
 #pragma unroll
     for (int u = 0; u < STAGE_X_UNROLL; ++u) {
         const int idx = threadIdx.x + u * FL_THREADS;
         if (idx < nx) {
             const int r = idx / kp, k = idx - r * kp;
             a[r * lda + k] = (uint16_t)bf16_bits(xv[u]);
+            alo[r * lda + k] = (uint16_t)lo_bits(xv[u]);
         }
     }
     for (int idx = threadIdx.x + STAGE_X_UNROLL * FL_THREADS; idx < nx; idx += FL_THREADS) {
         const int r = idx / kp, k = idx - r * kp;
         const int row = row0 + r;
         const bool ok = row < n_rows && k < F;
-        const float v = X[(size_t)(ok ? row : 0) * F + (ok ? k : 0)];
-        a[r * lda + k] = ok ? (uint16_t)bf16_bits(v) : (uint16_t)0;
+        const float v = ok ? X[(size_t)row * F + k] : 0.f;
+        a[r * lda + k] = (uint16_t)bf16_bits(v);
+        alo[r * lda + k] = (uint16_t)lo_bits(v);
     }
+}
+
+// Register half of a parameter-region copy (FL_EVAL_LAGGED: the round's own weights are
+// loaded while the previous local model is scored, and stored once that pass is done).
+struct ParamRegs {
+    uint4 v[STAGE_P_UNROLL];
+};
+__device__ __forceinline__ void params_load(const MLPDescB& e, const char* __restrict__ packed, ParamRegs& pr) {
+    const uint4* src = reinterpret_cast<const uint4*>(packed);
+    const int n16 = e.param_bytes >> 4;
+#pragma unroll
+    for (int u = 0; u < STAGE_P_UNROLL; ++u) {
+        const int i = threadIdx.x + u * FL_THREADS;
+        pr.v[u] = src[i < n16 ? i : 0];
+    }
+}
+__device__ __forceinline__ void params_store(const MLPDescB& e, const char* __restrict__ packed, const ParamRegs& pr,
+                                             char* lds) {
+    const uint4* src = reinterpret_cast<const uint4*>(packed);
+    uint4* dst = reinterpret_cast<uint4*>(lds + e.param_off);
+    const int n16 = e.param_bytes >> 4;
+#pragma unroll
+    for (int u = 0; u < STAGE_P_UNROLL; ++u) {
+        const int i = threadIdx.x + u * FL_THREADS;
+        const uint4 v = pr.v[u];
+        if (i < n16) dst[i] = v;
+    }
+    for (int i = threadIdx.x + STAGE_P_UNROLL * FL_THREADS; i < n16; i += FL_THREADS) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -183,13 +203,12 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
 // and B[8(l>>4)+j][l&15]; C/D col l&15, row 4(l>>4)+j)
 // ---------------------------------------------------------------------------------------
 
-// z = act_l . W_l^T + b_l; hidden layers: ReLU -> bf16 act_{l+1} (all kp[l+1] columns, the
-// padding comes out 0); last layer: fp32 logits [R][16].
+// z = act_l . W_l^T + b_l in split bf16 (fl_common.h): hi.hi in `acc`, the two cross terms in
+// `acl` (independent accumulation chains), z = acc + acl.  Hidden layers: ReLU -> act_{l+1}
+// hi / lo parts (all kp[l+1] columns, the padding comes out 0); last layer: fp32 logits [R][16].
 template <int RT>
-// `wave_off` rotates the tile -> wave assignment, so two passes in one phase (lagged
-// scoring) put their tiles on different waves.
-__device__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds, int wave_off = 0) {
-    const int wave = ((threadIdx.x >> 6) + wave_off) % FL_WAVES, lane = threadIdx.x & 63;
+__device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     const bool last = (l + 1 == d.L);
     const int ntiles = last ? ((d.dim[d.L] + 15) >> 4) : (e.kp[l + 1] >> 4);
@@ -197,20 +216,32 @@ __device__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char*
     const int lda = e.lda[l];
     const char* W = lds + e.w_off[l];
     const char* act = lds + e.act_off[l];
+    const char* alo = lds + e.alo_off[l];
     const float* bias = reinterpret_cast<const float*>(lds + e.bias_off[l]);
     for (int nt = wave; nt < ntiles; nt += FL_WAVES) {
         const char* wrow = W + ((nt * 16 + lr) * lda + 8 * lg) * 2;
-        const char* arow = act + (lr * lda + 8 * lg) * 2;
-        f32x4 acc[RT];
+        const int aoff = (lr * lda + 8 * lg) * 2;
+        f32x4 acc[RT], acl[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int rt = 0; rt < RT; ++rt) {
+            acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            acl[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
         for (int ks = 0; ks < ksteps; ++ks) {
             const bf16x8 bv = ld128(wrow + ks * 64);
-            bf16x8 av[RT];
+            const bf16x8 bl = ld128(wrow + e.wlo_delta + ks * 64);
+            bf16x8 av[RT], al[RT];
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) av[rt] = ld128(arow + rt * 16 * lda * 2 + ks * 64);
+            for (int rt = 0; rt < RT; ++rt) {
+                av[rt] = ld128(act + aoff + rt * 16 * lda * 2 + ks * 64);
+                al[rt] = ld128(alo + aoff + rt * 16 * lda * 2 + ks * 64);
+            }
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(av[rt], bv, acc[rt]);
+            for (int rt = 0; rt < RT; ++rt) {
+                acc[rt] = mfma32(av[rt], bv, acc[rt]);
+                acl[rt] = mfma32(al[rt], bv, acl[rt]);
+                acl[rt] = mfma32(av[rt], bl, acl[rt]);
+            }
         }
         const int n = nt * 16 + lr;
         const float b = bias[n];
@@ -219,15 +250,20 @@ __device__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char*
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) z[(rt * 16 + 4 * lg + j) * 16 + n] = acc[rt][j] + b;
+                for (int j = 0; j < 4; ++j) z[(rt * 16 + 4 * lg + j) * 16 + n] = (acc[rt][j] + acl[rt][j]) + b;
         } else {
             uint16_t* out = reinterpret_cast<uint16_t*>(lds + e.act_off[l + 1]);
+            uint16_t* olo = reinterpret_cast<uint16_t*>(lds + e.alo_off[l + 1]);
             const int ldo = e.lda[l + 1];
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    out[(rt * 16 + 4 * lg + j) * ldo + n] = (uint16_t)bf16_bits(fmaxf(acc[rt][j] + b, 0.f));
+                for (int j = 0; j < 4; ++j) {
+                    const float v = fmaxf((acc[rt][j] + acl[rt][j]) + b, 0.f);
+                    const int o = (rt * 16 + 4 * lg + j) * ldo + n;
+                    out[o] = (uint16_t)bf16_bits(v);
+                    olo[o] = (uint16_t)lo_bits(v);
+                }
         }
     }
 }
@@ -322,25 +358,8 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
     }
 }
 
-// Two forward passes in lock step, one phase (barrier) per layer: the training pass on e and
-// the lagged scoring pass on es (previous round's local image; its activations live in the
-// delta buffers, unused until the backward pass, and its logits in a second region).  The
-// phases are latency-bound, so the second pass's tiles on otherwise idle waves cost little.
 template <int RT>
-__device__ void forward2_block_bf16(const MLPDesc& d, const MLPDescB& e, const MLPDescB& es, char* lds,
-                                    unsigned long long* dbg) {
-    for (int l = 0; l < d.L; ++l) {
-        if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
-        const bool last = (l + 1 == d.L);
-        const int ntiles = last ? ((d.dim[d.L] + 15) >> 4) : (e.kp[l + 1] >> 4);
-        fwd_layer_bf16<RT>(d, e, l, lds);
-        fwd_layer_bf16<RT>(d, es, l, lds, FL_WAVES - ntiles % FL_WAVES);
-        lds_barrier();
-    }
-}
-
-template <int RT>
-__device__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg) {
+__device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg) {
     for (int l = 0; l < d.L; ++l) {
         if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
         fwd_layer_bf16<RT>(d, e, l, lds);
@@ -355,7 +374,7 @@ template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                      const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
-                     int stage_local, int mode, float* __restrict__ cm_out, int fold_mask, MLPDescB el) {
+                     int stage_local, int mode, float* __restrict__ cm_out, int fold_mask) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
@@ -391,10 +410,11 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     const int L = d.L;
     const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
     // FL_EVAL_LAGGED (first local step): the previous round's local model, still intact in
-    // pk_local (this round's Adam has not run), is staged beside the input weights
+    // pk_local (this round's Adam has not run), is staged and scored first; the round's own
+    // weights are loaded meanwhile and replace it in LDS before the training pass
     const bool lagged = mode == FL_EVAL_LAGGED && local_step == 0;
-    stage_params_rows_bf16<RT>(e, (local_step == 0 && !stage_local) ? b.pk_global : b.pk_local, b.X, c.n_rows,
-                               d.dim[0], row0, lds, lagged ? b.pk_local : nullptr, el.param_off);
+    const char* img = (local_step == 0 && !stage_local) ? b.pk_global : b.pk_local;
+    stage_params_rows_bf16<RT>(e, lagged ? b.pk_local : img, b.X, c.n_rows, d.dim[0], row0, lds);
     FL_STAMP(8);
     {   // padding columns [C, kp[L]) of D_L never change: zero them here, off the CE's path
         const int padc = e.kp[L] - C;
@@ -409,23 +429,31 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     FL_STAMP(1);
     if (!S_sh.live) return;
     float* slab = b.slab + (size_t)blockIdx.x * c.slab_stride;
-    if (lagged) forward2_block_bf16<RT>(d, e, el, lds, b.dbg);  // + score the previous local model
-    else forward_block_bf16<RT>(d, e, lds, b.dbg);
-    FL_STAMP(2);
-    if (lagged && threadIdx.x >= 64 && threadIdx.x < 64 + R) {
-        // the lagged scoring's argmax (C:148 evaluation, published one round later), on wave 1
-        // while wave 0 runs the loss; counts -> b.cnt after the barrier below
-        const int r = threadIdx.x - 64;
-        if (row0 + r < c.n_rows) {
-            const float* zr = reinterpret_cast<const float*>(lds + el.logit_off) + r * 16;
-            const int yl = b.y[row0 + r];
-            int best = 0;
-            float bv = zr[0];
-            for (int k = 1; k < C; ++k)
-                if (zr[k] > bv) { bv = zr[k]; best = k; }
-            atomicAdd(&cm_s[yl * C + best], 1);
+    // lagged: pass 0 scores the previous local model (C:148), pass 1 trains; one call site of
+    // the forward pass (inlined, so the prefetched weights stay in registers across it)
+    ParamRegs pr;
+    if (lagged) params_load(e, img, pr);
+    for (int pass = lagged ? 0 : 1; pass < 2; ++pass) {
+        if (pass == 1 && lagged) {
+            if (threadIdx.x < R) {
+                // the scored model's argmax: counts -> b.cnt after the CE barrier below
+                const int r = threadIdx.x;
+                if (row0 + r < c.n_rows) {
+                    const float* zr = reinterpret_cast<const float*>(lds + e.logit_off) + r * 16;
+                    int best = 0;
+                    float bv = zr[0];
+                    for (int k = 1; k < C; ++k)
+                        if (zr[k] > bv) { bv = zr[k]; best = k; }
+                    atomicAdd(&cm_s[ylab * C + best], 1);
+                }
+            }
+            lds_barrier();  // every read of the scored image and its logits is done
+            params_store(e, img, pr, lds);
+            lds_barrier();
         }
+        forward_block_bf16<RT>(d, e, lds, b.dbg);
     }
+    FL_STAMP(2);
 
     // softmax cross-entropy (mean over the shard): D_L = (softmax - onehot) / n, bf16.
     // Fused evaluation: the same logits score the previous round's model (argmax).
@@ -557,24 +585,21 @@ fl_eval_fedavg_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const
 // ---------------------------------------------------------------------------------------
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                 const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
-                                bool stage_local, int mode, float* cm_out, int fold_mask, const MLPDescB* el) {
+                                bool stage_local, int mode, float* cm_out, int fold_mask) {
     if ((mode == FL_EVAL_FUSED || mode == FL_EVAL_LAGGED) && cm_out == nullptr) return hipErrorInvalidValue;
-    if (mode == FL_EVAL_LAGGED && el == nullptr) return hipErrorInvalidValue;
-    const MLPDescB eloc = el != nullptr ? *el : e;
-    // the lagged layout extends the LDS by the second parameter image
-    const size_t lds = el != nullptr ? (size_t)el->lds_bytes : (size_t)e.lds_bytes;
+    const size_t lds = (size_t)e.lds_bytes;
     switch (c.R) {
         case 16:
             hipLaunchKernelGGL(fl_train_bf16_kernel<1>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
-                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask, eloc);
+                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask);
             break;
         case 32:
             hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
-                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask, eloc);
+                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask);
             break;
         case 64:
             hipLaunchKernelGGL(fl_train_bf16_kernel<4>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
-                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask, eloc);
+                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask);
             break;
         default: return hipErrorInvalidValue;
     }

@@ -25,6 +25,7 @@
 // image (fl_common.h layout) and bytes of the packed region.
 struct PeerPack {
     char* pk;                       // packed region (nullptr: no packing)
+    int wlo_delta;                  // split-bf16: lo image of W_l at pk_w[l] + wlo_delta (MLPDescB)
     int L;
     int img4_w[FL_MAX_LAYERS];      // first float4 of W_l in the image
     int img4_b[FL_MAX_LAYERS];      // first float4 of b_l
@@ -101,10 +102,18 @@ __device__ __forceinline__ void peer_pack_store(const PeerPack& p, int i, float4
         if (i < p.img4_b[l]) {
             const int q = i - p.img4_w[l];
             const int n = q / p.ldw4[l], c4 = q - n * p.ldw4[l];
-            if (c4 < p.k4[l])  // columns [roundup16(K), ldw) are the image's zero pad
-                *reinterpret_cast<uint2*>(p.pk + p.pk_w[l] + (n * p.pk_lda[l] + 4 * c4) * 2) =
-                    make_uint2(peer_bf16_rne(s.x) | (peer_bf16_rne(s.y) << 16),
-                               peer_bf16_rne(s.z) | (peer_bf16_rne(s.w) << 16));
+            if (c4 < p.k4[l]) {  // columns [roundup16(K), ldw) are the image's zero pad
+                const uint32_t hx = peer_bf16_rne(s.x), hy = peer_bf16_rne(s.y), hz = peer_bf16_rne(s.z),
+                               hw = peer_bf16_rne(s.w);
+                char* dst = p.pk + p.pk_w[l] + (n * p.pk_lda[l] + 4 * c4) * 2;
+                *reinterpret_cast<uint2*>(dst) = make_uint2(hx | (hy << 16), hz | (hw << 16));
+                // lo parts: bf16(x - hi) (split-bf16 forward, fl_common.h)
+                *reinterpret_cast<uint2*>(dst + p.wlo_delta) =
+                    make_uint2(peer_bf16_rne(s.x - __uint_as_float(hx << 16)) |
+                                   (peer_bf16_rne(s.y - __uint_as_float(hy << 16)) << 16),
+                               peer_bf16_rne(s.z - __uint_as_float(hz << 16)) |
+                                   (peer_bf16_rne(s.w - __uint_as_float(hw << 16)) << 16));
+            }
         } else {
             *reinterpret_cast<float4*>(p.pk + p.pk_b[l] + (i - p.img4_b[l]) * 16) = s;
         }

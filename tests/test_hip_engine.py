@@ -57,10 +57,15 @@ def test_graph_replay_bitwise_equals_eager(shard):
     np.testing.assert_array_equal(out[0][1], out[1][1])
 
 
-def test_device_early_stop_rule_matches_host_rule():
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_device_early_stop_rule_matches_host_rule(dtype):
+    """The device-side stop rule replays the host rule on the device's own metric history, and
+    (real CSV, reference hyperparameters) fires inside 300 rounds in both precisions -- bf16
+    scores with the split-bf16 forward, so borderline rows stop flipping as the LR decays."""
     from fedmi.data.tabular import load_tabular
     ds = load_tabular()
-    e = HipRoundEngine(ds.X_train, ds.y_train, 2, EngineConfig(max_rounds=300), None, init_flat(DIMS, 0))
+    e = HipRoundEngine(ds.X_train, ds.y_train, 2, EngineConfig(max_rounds=300, dtype=dtype), None,
+                       init_flat(DIMS, 0))
     e.run(300)
     h = e.history()
     assert 100 < h["rounds_run"] < 300 and h["stop_round"] == h["rounds_run"]
@@ -428,7 +433,11 @@ def test_bf16_engine_tracks_fp32_oracle(R, hidden):
     flat = init_flat(dims, 3)
     mk = lambda cls, **kw: cls(X, y, 2, EngineConfig(hidden=hidden, max_rounds=60, early_stop=False,
                                                       rows_per_block=R, **kw), None, flat)
-    hb = mk(HipRoundEngine, dtype="bf16")
+    try:
+        hb = mk(HipRoundEngine, dtype="bf16")
+    except RuntimeError as err:  # split-bf16 layout of a big model at R = 64 exceeds the CU's LDS
+        assert "LDS" in str(err) and R == 64
+        pytest.skip(str(err))
     ref = mk(TorchRoundEngine)
     hb.run(1)
     ref.run(1)
@@ -490,8 +499,79 @@ def test_fused_eval_mixed_with_step_api():
     np.testing.assert_array_equal(hist[0][2], hist[1][2])
 
 
-def test_bf16_engine_layout_fits_two_blocks_per_cu():
+def test_bf16_engine_layout_fits_one_cu():
+    """The split-bf16 train layout (hi + lo weight images, lo activation buffers) of the reference
+    model fits one CU's LDS at the bench's 32 rows per workgroup."""
     X, y = make_income_like(500, seed=1)
-    e = HipRoundEngine(X, y, 2, EngineConfig(rows_per_block=16, dtype="bf16"), None, init_flat([14, 50, 200, 2], 0))
+    e = HipRoundEngine(X, y, 2, EngineConfig(rows_per_block=32, dtype="bf16"), None, init_flat(DIMS, 0))
     lay = e.engine.layout()
-    assert lay["dtype"] == 1 and lay["lds_bytes"] <= 80 * 1024, lay["lds_bytes"]
+    assert lay["dtype"] == 1 and lay["lds_bytes"] <= 158 * 1024, lay["lds_bytes"]
+    assert lay["eval_lds_bytes"] <= lay["lds_bytes"]
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(torch.float64)
+
+
+def _split_bf16_reference_grad(flat, X, y, dims):
+    """Host model of the bf16 train kernel's arithmetic (fl_kernels_bf16.hip), in float64:
+    split-bf16 forward (hi.hi + lo.hi + hi.lo, hidden outputs split into hi/lo after ReLU),
+    softmax-CE deltas rounded to bf16, backward on the hi parts with bf16 deltas."""
+    from fedmi.models.mlp import flat_to_dict
+    d = flat_to_dict(flat, dims)
+    L = len(dims) - 1
+    Ws = [torch.as_tensor(d[f"model.{2 * l}.weight"], dtype=torch.float64) for l in range(L)]
+    bs = [torch.as_tensor(d[f"model.{2 * l}.bias"], dtype=torch.float64) for l in range(L)]
+    a = torch.as_tensor(X, dtype=torch.float32).to(torch.float64)
+    yt = torch.as_tensor(y, dtype=torch.long)
+    his, pre = [], []
+    for l in range(L):
+        ah, wh = _bf(a), _bf(Ws[l])
+        al, wl = _bf(a - ah), _bf(Ws[l] - wh)
+        z = ah @ wh.T + (al @ wh.T + ah @ wl.T) + bs[l]
+        his.append(ah)
+        pre.append(z)
+        a = torch.relu(z).to(torch.float32).to(torch.float64)
+    n = len(y)
+    p = torch.softmax(z, 1)
+    dz = p.clone()
+    dz[torch.arange(n), yt] -= 1.0
+    dz = _bf(dz / n)
+    gW, gb = [None] * L, [None] * L
+    for l in range(L - 1, -1, -1):
+        gW[l] = dz.T @ his[l]
+        gb[l] = dz.sum(0)
+        if l:
+            dz = _bf((dz @ _bf(Ws[l])) * (his[l] > 0))
+    return torch.cat([torch.cat([gW[l].reshape(-1), gb[l]]) for l in range(L)]).numpy()
+
+
+@pytest.mark.parametrize("R", [16, 32])
+def test_bf16_train_kernel_gradient(R):
+    """The slab-reduced gradient of ONE fl_train_bf16 launch vs (a) a float64 host model of the
+    kernel's own arithmetic (split-bf16 forward, bf16 backward operands): rel. err <= 1e-3 per
+    tensor, and (b) fp32 torch autograd of the exact model: rel. err <= 1e-2 per tensor."""
+    X, y = make_income_like(4000, seed=21)
+    dims = DIMS
+    flat = init_flat(dims, 8)
+    e = HipRoundEngine(X, y, 2, EngineConfig(max_rounds=4, early_stop=False, rows_per_block=R, dtype="bf16",
+                                             graph_rounds=0), None, flat)
+    e.step_train()
+    e.stream.synchronize()
+    P = e.P
+    stride = int(e.engine.layout()["slab_stride"])
+    g = e.slab.view(-1, stride)[:, :P].double().sum(0).cpu().numpy()
+    ref = _split_bf16_reference_grad(flat, X, y, dims)
+    model = TorchRoundEngine(X, y, 2, EngineConfig(max_rounds=2), None, flat)
+    out = model.model(torch.as_tensor(X))
+    torch.nn.functional.cross_entropy(out, torch.as_tensor(y, dtype=torch.long)).backward()
+    auto = torch.cat([p.grad.reshape(-1) for p in model.model.parameters()]).double().numpy()
+    off = 0
+    for l in range(len(dims) - 1):
+        for n in (dims[l] * dims[l + 1], dims[l + 1]):
+            sl = slice(off, off + n)
+            err_k = np.linalg.norm(g[sl] - ref[sl]) / np.linalg.norm(ref[sl])
+            err_a = np.linalg.norm(g[sl] - auto[sl]) / np.linalg.norm(auto[sl])
+            assert err_k <= 1e-3, (l, n, err_k)
+            assert err_a <= 1e-2, (l, n, err_a)
+            off += n
