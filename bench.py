@@ -129,10 +129,9 @@ def main(argv=None):
     ap.add_argument("--rows-per-block", type=int, default=32)
     ap.add_argument("--graph-rounds", type=int, default=0,
                     help="rounds per captured HIP graph (0: largest even divisor of --steps up to 64)")
-    ap.add_argument("--backend", default=os.environ.get("FEDMI_DATA_PLANE", "xgmi"),
-                    choices=["xgmi", "rccl", "nccl"],
+    ap.add_argument("--backend", default="auto", choices=["auto", "xgmi", "rccl", "nccl"],
                     help="FedAvg data plane: one-shot xGMI peer all-reduce (falls back to RCCL) | RCCL | torch nccl "
-                         "(default: $FEDMI_DATA_PLANE or xgmi)")
+                         "(auto: $FEDMI_DATA_PLANE, default xgmi)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="debug: every rank on cuda:0 (xGMI peer protocol between processes of one GPU, no RCCL), "
                          "so the N > 1 path runs on a one-GPU box")
@@ -156,8 +155,12 @@ def main(argv=None):
     from fedmi.parallel.comm import get_world
     import torch.distributed as dist
 
+    from fedmi.parallel.comm import resolve_backend
+    a.backend = resolve_backend(a.backend, "cuda")
     if a.share_gpu:
-        comm = get_world(backend="xgmi" if a.backend == "xgmi" else a.backend, device="cuda:0", rccl=False)
+        if a.backend != "xgmi":
+            raise SystemExit("--share-gpu runs the xGMI peer protocol (RCCL cannot put two ranks on one GPU)")
+        comm = get_world(backend="xgmi", device="cuda:0", rccl=False)
     else:
         comm = get_world(backend=a.backend, device="cuda")
     N = comm.size
@@ -248,6 +251,8 @@ def main_wide(a) -> None:
     from fedmi.parallel.comm import get_world
     import torch.distributed as dist
 
+    from fedmi.parallel.comm import resolve_backend
+    a.backend = resolve_backend(a.backend, "cuda")
     comm = get_world(backend="rccl" if a.backend == "xgmi" else a.backend, device="cuda")
     N = comm.size
     if N != a.gpus:

@@ -140,6 +140,18 @@ class RoundEngineBase:
         self.hist = _History(cfg.max_rounds, self.world)
         assert init_flat.shape == (self.P,)
 
+    def set_early_stop(self, patience: int, tolerance: float) -> None:
+        """Early-stop parameters of ``train_and_evaluate(termination_patience, tolerance)``
+        (C:122); only before the first round."""
+        if getattr(self, "rounds_issued", 0):
+            raise RuntimeError("early-stop parameters must be set before the first round")
+        self.cfg.patience = int(patience)
+        self.cfg.tolerance = float(tolerance)
+        self._apply_early_stop()
+
+    def _apply_early_stop(self) -> None:
+        raise NotImplementedError
+
     def _allreduce_scalar(self, x: float) -> float:
         if self.world == 1:
             return x
@@ -238,6 +250,10 @@ class TorchRoundEngine(RoundEngineBase):
         with torch.no_grad():
             _, pred = torch.max(model(Xt), 1)
         return confusion_matrix(yt.cpu().numpy(), pred.cpu().numpy(), self.n_classes)
+
+    def _apply_early_stop(self) -> None:
+        cfg = self.cfg
+        self.stopper = EarlyStopper(cfg.patience, cfg.tolerance, cfg.rtol, enabled=cfg.early_stop)
 
     # -- step-by-step API (reference train_one_epoch / evaluate_local / federated_averaging)
     def participants(self, r: int) -> np.ndarray:
@@ -519,6 +535,16 @@ class HipRoundEngine(RoundEngineBase):
             if self._peer is not None:
                 self.engine.attach_peer(self._peer)
         self._graph_ready = False
+
+    def _apply_early_stop(self) -> None:
+        cfg = self.cfg
+        self.engine.set_early_stop(int(cfg.patience), float(cfg.tolerance), float(cfg.rtol))
+        self._graph_ready = False
+        for st in self.state:     # the patience counter starts at the new patience
+            rec = st.cpu().numpy().view(_STATE_DTYPE).copy()
+            rec["count"] = int(cfg.patience)
+            st.copy_(torch.as_tensor(rec.view(np.uint8)).to(st.device))
+        torch.cuda.synchronize(self.device)
 
     @property
     def aggregation(self) -> str:

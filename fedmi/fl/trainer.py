@@ -101,10 +101,8 @@ class FederatedMLPLearning:
         from ..runtime.watchdog import Watchdog
         eng = self.engine
         comm = comm if comm is not None else self.comm
-        if (termination_patience != eng.cfg.patience or tolerance != eng.cfg.tolerance) and eng.rounds_issued:
-            raise RuntimeError("early-stop parameters must be set before the first round")
-        eng.cfg.patience = termination_patience
-        eng.cfg.tolerance = tolerance
+        if termination_patience != eng.cfg.patience or tolerance != eng.cfg.tolerance:
+            eng.set_early_stop(termination_patience, tolerance)   # raises after the first round
         printed = eng.hist.rounds_run
         abort = (comm.Abort if comm is not None and hasattr(comm, "Abort") else (lambda: None))
         wd = Watchdog(watchdog_s, abort, rank=self.rank)

@@ -122,7 +122,7 @@ def _r16(n: int) -> int:
 
 def image_layout(dims: Sequence[int]):
     """Offsets of the padded device parameter image (fedmi/ops/csrc/fl_common.h): per layer
-    W_l as [roundup16(N)][roundup16(K)+2] then b_l as [roundup16(N)], zero padded."""
+    W_l as [roundup16(N)][roundup16(K)+4] then b_l as [roundup16(N)], zero padded."""
     iw, ib, off = [], [], 0
     for l in range(len(dims) - 1):
         K, N = dims[l], dims[l + 1]

@@ -379,6 +379,17 @@ class FLEngine {
     bool adam_exchange() const { return xchg_; }
     bool fused() const { return fused_; }
 
+    // Early-stop parameters (train_and_evaluate(termination_patience, tolerance), C:122): the
+    // kernels take FLConfig by value, so a captured graph is dropped; the caller rewrites the
+    // round state's patience counter before the first round.
+    void set_early_stop(int patience, double atol, double rtol) {
+        if (patience < 1) throw std::runtime_error("set_early_stop: patience must be >= 1");
+        c_.patience = patience;
+        c_.atol = atol;
+        c_.rtol = rtol;
+        drop_graph();
+    }
+
     // The host wrote the global weights (set_weights / resume): the next round repacks them.
     void invalidate() { need_pack_ = true; }
 
@@ -775,6 +786,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("time_kernels", &FLEngine::time_kernels)
         .def("set_debug", &FLEngine::set_debug)
         .def("invalidate", &FLEngine::invalidate)
+        .def("set_early_stop", &FLEngine::set_early_stop)
         .def("reset_pending", &FLEngine::reset_pending)
         .def("attach_peer", &FLEngine::attach_peer, py::keep_alive<1, 2>())
         .def_property_readonly("has_peer", &FLEngine::has_peer)

@@ -492,9 +492,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
                     S0 = fold_round(d, c, b, lag_s, S0.next_round - 1, S0, blockIdx.x == 0);
                 }
             } else if (need) {
-#ifndef FL_DIAG_NO_FOLD
                 S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0, fold_mask);
-#endif
             }
             if (lane == 0) {
                 S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
@@ -628,11 +626,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             for (int u = 0; u < ADAM_DEPTH; ++u) {
                 const int s = s0 + u * ADAM_WAVES;
                 // unpredicated; non-temporal: the slab is read once
-#ifndef FL_DIAG_NO_SLAB_READ
                 const float v = __builtin_nontemporal_load(&sp[(size_t)(s < c.n_slabs ? s : 0) * c.slab_stride]);
-#else
-                const float v = (float)s * 1e-30f;
-#endif
                 x[u] = s < c.n_slabs ? v : 0.f;
             }
             if (!have_state) {

@@ -187,15 +187,6 @@ gemm_nt_bf16_kernel(NTArgs g) {
 // last read, i.e. after a barrier that follows every reader's lgkmcnt(0).  The last two
 // K-tiles issue nothing past the end and drain with vmcnt(0).
 #define NT2_BM 256
-#ifndef NT2_EXP
-#define NT2_EXP 0
-#endif
-#ifndef NT2_SADDR
-#define NT2_SADDR 1
-#endif
-#ifndef NT2_DMA_POS
-#define NT2_DMA_POS 0
-#endif
 #define NT2_THREADS 512
 
 template <int N>
@@ -217,13 +208,10 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
     const __hip_bfloat16* A = reinterpret_cast<const __hip_bfloat16*>(g.A);
     const __hip_bfloat16* B = reinterpret_cast<const __hip_bfloat16*>(g.B);
     const int t = threadIdx.x;
-#if NT2_SADDR
     // wave index in an SGPR: LDS-DMA destinations (M0) and row bases become scalar, each DMA is
-    // one global_load_lds with an SGPR base + 32-bit lane offset (no 64-bit VALU address adds)
+    // one global_load_lds with an SGPR base + 32-bit lane offset (no 64-bit VALU address adds;
+    // measured 1.5-4 % faster than per-lane 64-bit source pointers)
     const int w = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63;
-#else
-    const int w = t >> 6, l = t & 63;
-#endif
     const int wr = w >> 2, wc = w & 3;
     const int lr = l & 15, lg = l >> 4;
 
@@ -231,35 +219,21 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
     // = logical chunk (l%4) ^ (((row>>2)&3) & 2) of the row's 64-byte k-half.
     const int dchunk = ((l & 3) ^ ((l >> 4) & 2)) * 8;
     int dstA[2], dstB[2];
-#if NT2_SADDR
     const char* sbA[2];
     const char* sbB[2];
     const uint32_t voA = (uint32_t)(((l >> 2) * g.lda + dchunk) * 2);
     const uint32_t voB = (uint32_t)(((l >> 2) * g.ldb + dchunk) * 2);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        const int ra = (w >> 2) * 128 + h * 64 + (w & 3) * 16;
+        const int ra = (w >> 2) * 128 + h * 64 + (w & 3) * 16;  // A piece m-half h
         sbA[h] = reinterpret_cast<const char*>(A + (size_t)(m0 + ra) * g.lda);
         dstA[h] = ra * 64;
-        const int rb = h * 128 + w * 16;
+        const int rb = h * 128 + w * 16;                         // B piece, DMA h of 2
         sbB[h] = reinterpret_cast<const char*>(B + (size_t)(n0 + rb) * g.ldb);
         dstB[h] = 32768 + rb * 64;
     }
-#if NT2_EXP == 3
-    // timing experiment only (wrong results): every DMA reads 8 full 128-byte lines instead of
-    // 16 half lines (same bytes per K-tile), to price the per-line cost of the DMA issue
-    const uint32_t vxA = (uint32_t)((l >> 3) * g.lda * 2 + (l & 7) * 16);
-    const uint32_t vxB = (uint32_t)((l >> 3) * g.ldb * 2 + (l & 7) * 16);
-    auto dma = [&](int tile, int d) {
-        const int ks = (d >= 4) ? 1 : 0;
-        const int kb = tile * 128;
-        char* base = smem + (tile & 1) * 65536 + ks * 16384;
-        if (d == 0 || d == 7) glds16(sbA[0] + kb + vxA + ks * 8 * g.lda * 2, base + dstA[0]);
-        else if (d == 3 || d == 4) glds16(sbA[1] + kb + vxA + ks * 8 * g.lda * 2, base + dstA[1]);
-        else if (d == 1 || d == 5) glds16(sbB[0] + kb + vxB + ks * 8 * g.ldb * 2, base + dstB[0]);
-        else glds16(sbB[1] + kb + vxB + ks * 8 * g.ldb * 2, base + dstB[1]);
-    };
-#else
+    // LDS-DMA d (0..7) of K-tile `tile`, in first-read order: d0 A m0 ks0, d1-d2 B ks0, d3 A m1
+    // ks0, d4 A m1 ks1, d5-d6 B ks1, d7 A m0 ks1 (first read in phases 0,0,0,1,2,2,2,3)
     auto dma = [&](int tile, int d) {
         const int ks = (d >= 4) ? 1 : 0;
         const int kb = (tile * 64 + ks * 32) * 2;
@@ -269,31 +243,6 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
         else if (d == 1 || d == 5) glds16(sbB[0] + kb + voB, base + dstB[0]);
         else glds16(sbB[1] + kb + voB, base + dstB[1]);
     };
-#endif
-#else
-    const __hip_bfloat16* srcA[2];
-    const __hip_bfloat16* srcB[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int ra = (w >> 2) * 128 + h * 64 + (w & 3) * 16;  // A piece m-half h
-        srcA[h] = A + (size_t)(m0 + ra + (l >> 2)) * g.lda + dchunk;
-        dstA[h] = ra * 64;
-        const int rb = h * 128 + w * 16;                         // B piece, DMA h of 2
-        srcB[h] = B + (size_t)(n0 + rb + (l >> 2)) * g.ldb + dchunk;
-        dstB[h] = 32768 + rb * 64;
-    }
-    // LDS-DMA d (0..7) of K-tile `tile`, in first-read order: d0 A m0 ks0, d1-d2 B ks0, d3 A m1
-    // ks0, d4 A m1 ks1, d5-d6 B ks1, d7 A m0 ks1 (first read in phases 0,0,0,1,2,2,2,3)
-    auto dma = [&](int tile, int d) {
-        const int ks = (d >= 4) ? 1 : 0;
-        const int k = tile * 64 + ks * 32;
-        char* base = smem + (tile & 1) * 65536 + ks * 16384;
-        if (d == 0 || d == 7) glds16(srcA[0] + k, base + dstA[0]);
-        else if (d == 3 || d == 4) glds16(srcA[1] + k, base + dstA[1]);
-        else if (d == 1 || d == 5) glds16(srcB[0] + k, base + dstB[0]);
-        else glds16(srcB[1] + k, base + dstB[1]);
-    };
-#endif
 
     // fragment read offset of this lane inside a 16-row group: row lr, chunk lg swizzled
     const int foff = lr * 64 + ((lg ^ ((lr >> 2) & 2)) << 4);
@@ -316,28 +265,19 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();
 
-    // two DMAs per phase: r = 0: tile+1 d4,d5; r = 1: tile+1 d6,d7; r = 2: tile+2 d0,d1;
-    // r = 3: tile+2 d2,d3 (each slot restaged >= 2 phases after its last read).  NT2_DMA_POS
-    // places them: 0 both before the fragment reads, 1 both after them, 2 one there and one
-    // inside the MFMA cluster, 3 both inside the MFMA cluster (issued later than the phase's
-    // vmcnt wait, which then keeps correspondingly fewer younger DMAs in flight: the retired
-    // set is the same)
+    // two DMAs per phase, issued before the fragment reads: r = 0: tile+1 d4,d5; r = 1: tile+1
+    // d6,d7; r = 2: tile+2 d0,d1; r = 3: tile+2 d2,d3 (each slot restaged >= 2 phases after its
+    // last read).  (Measured alternatives: after the fragment reads or inside the MFMA cluster,
+    // 1-6 % slower; profiles/nt_ksweep_r1_experiments.log.)
     auto phase = [&](int q, int r, bool tail) {
         const char* buf = smem + ((q >> 2) & 1) * 65536 + ((r >= 2) ? 16384 : 0);
         const int mh = (r == 1 || r == 2) ? 1 : 0;
         const int dtile = (q >> 2) + (r < 2 ? 1 : 2);
         const int dd = (r < 2) ? 4 + 2 * r : 2 * (r - 2);
-        const bool dok = !tail || dtile < KT;
-#if NT2_EXP == 2
-        auto issue = [&](int) {};
-#else
-        auto issue = [&](int i) { if (dok) dma(dtile, dd + i); };
-#endif
-#if NT2_DMA_POS == 0
-        issue(0); issue(1);
-#elif NT2_DMA_POS == 2
-        issue(0);
-#endif
+        if (!tail || dtile < KT) {
+            dma(dtile, dd);
+            dma(dtile, dd + 1);
+        }
         if ((r & 1) == 0) {
 #pragma unroll
             for (int y = 0; y < 4; ++y) bfr[y] = *reinterpret_cast<const bf16x8*>(buf + boff + y * 16 * 64);
@@ -345,35 +285,17 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
 #pragma unroll
         for (int x = 0; x < 4; ++x)
             af[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + (mh * 64 + x * 16) * 64);
-#if NT2_DMA_POS == 1
-        issue(0); issue(1);
-#endif
-        constexpr int NLATE = NT2_DMA_POS == 3 ? 2 : (NT2_DMA_POS == 2 ? 1 : 0);
         if (tail) vm_wait<0>();
-#if NT2_EXP != 0
-        // timing experiments only (wrong results): no steady-state DMA wait / no DMA at all
-#else
-        else if ((r & 1) == 0) vm_wait<10 - NLATE>();
-        else vm_wait<9 - NLATE>();
-#endif
+        else if ((r & 1) == 0) vm_wait<10>();
+        else vm_wait<9>();
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
+        for (int x = 0; x < 4; ++x)
 #pragma unroll
             for (int y = 0; y < 4; ++y)
                 acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr[y], acc[mh * 4 + x][y], 0, 0, 0);
-            if (NLATE == 2 && (x == 0 || x == 2)) {
-                __builtin_amdgcn_sched_barrier(0);
-                issue(x >> 1);
-                __builtin_amdgcn_sched_barrier(0);
-            } else if (NLATE == 1 && x == 1) {
-                __builtin_amdgcn_sched_barrier(0);
-                issue(1);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
     };

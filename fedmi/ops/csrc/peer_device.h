@@ -135,12 +135,23 @@ __device__ __forceinline__ void peer_publish(unsigned* const* dst, int world, un
         __hip_atomic_store(dst[threadIdx.x], target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Memory ordering of the protocol (publisher on GPU j, reader on GPU i):
+//   publisher: data stores (uncached send buffer) -> RELEASE store of the flag at system scope
+//              (the release waits for every earlier store of the wave to be acknowledged and
+//              writes back this GPU's dirty L2 lines), so the data is in j's memory before
+//              the flag can be seen over xGMI;
+//   reader:    relaxed polling of the flag (cheap loop), then ONE system-scope ACQUIRE fence
+//              (invalidates i's non-coherent cache lines) before any read of the data, which
+//              in addition uses cache-bypassing (sc0 sc1) loads.
+// Release / acquire pair at system scope: correct across GPUs by construction, not only on
+// one device where the tests run.
+__device__ __forceinline__ void peer_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+
 // Wait until every rank has published `target` in `flags` (one polling lane per rank,
 // bounded by the timeout: on expiry the sticky error word is set and the wait ends).
 __device__ __forceinline__ void peer_wait(const PeerArgs& a, unsigned* flags, unsigned target) {
     if (threadIdx.x < (unsigned)a.world) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        // relaxed: everything read after the wait uses cache-bypassing loads
         while ((int)(__hip_atomic_load(&flags[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
             if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
                 __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -149,6 +160,7 @@ __device__ __forceinline__ void peer_wait(const PeerArgs& a, unsigned* flags, un
             __builtin_amdgcn_s_sleep(2);
         }
     }
+    peer_acquire();
     __syncthreads();
 }
 
@@ -230,7 +242,10 @@ __device__ __forceinline__ void peer_wait_eval(const PeerArgs& a, unsigned targe
         __syncthreads();
         const int any = pending_s;
         __syncthreads();
-        if (!any) break;
+        if (!any) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with peer_eval_done's release
+            break;
+        }
         if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
             if (threadIdx.x == 0) __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
@@ -262,7 +277,7 @@ __device__ __forceinline__ void peer_fused_reduce(const PeerArgs& a, const PeerP
 __device__ __forceinline__ void peer_eval_done(const PeerArgs& a, unsigned target, int blk) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&a.eflags[blk], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(&a.eflags[blk], target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -272,11 +287,11 @@ __device__ __forceinline__ void peer_eval_done(const PeerArgs& a, unsigned targe
 // no separate all-reduce kernel, no kernel boundary between the update and the reduction.
 // Executed by one wave; `target` = the call index (device round state, same on every rank).
 // ---------------------------------------------------------------------------------------
+// (the caller's stores of the chunk are this wave's: the release store waits for all of them)
 __device__ __forceinline__ void peer_chunk_publish(const PeerArgs& a, int chunk, unsigned target) {
     const int lane = threadIdx.x & 63;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's send-buffer stores are done
     if (lane < a.world)
-        __hip_atomic_store(a.cflag_dst[lane] + chunk, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.cflag_dst[lane] + chunk, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void peer_chunk_wait(const PeerArgs& a, int chunk, unsigned target) {
     const int lane = threadIdx.x & 63;
@@ -292,6 +307,7 @@ __device__ __forceinline__ void peer_chunk_wait(const PeerArgs& a, int chunk, un
         }
     }
     __builtin_amdgcn_wave_barrier();
+    peer_acquire();  // whole wave: every lane reads the chunk next
 }
 __device__ __forceinline__ void peer_chunk_exchange_wait(const PeerArgs& a, int chunk, unsigned target) {
     peer_chunk_publish(a, chunk, target);

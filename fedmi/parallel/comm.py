@@ -40,6 +40,22 @@ def _env_int(name: str, default: int) -> int:
     return int(v) if v not in (None, "") else default
 
 
+DATA_PLANES = ("xgmi", "rccl", "nccl")
+
+
+def resolve_backend(backend: str, device_type: str) -> str:
+    """``auto`` -> gloo on CPU; on GPUs ``$FEDMI_DATA_PLANE`` (xgmi | rccl | nccl, default
+    xgmi), so a launcher can A/B the FedAvg data planes without touching the command line."""
+    if backend != "auto":
+        return backend
+    if device_type != "cuda":
+        return "gloo"
+    plane = os.environ.get("FEDMI_DATA_PLANE", "xgmi").strip().lower() or "xgmi"
+    if plane not in DATA_PLANES:
+        raise ValueError(f"FEDMI_DATA_PLANE={plane!r}: expected one of {DATA_PLANES}")
+    return plane
+
+
 class Comm:
     """``rccl=False`` (with ``backend='xgmi'``) skips the RCCL communicator: device
     all-reduces outside the round engine then go through the host.  That is the setting for
@@ -58,8 +74,7 @@ class Comm:
             self.device = torch.device("cuda", idx)
         else:
             self.device = torch.device("cpu")
-        if backend == "auto":
-            backend = "xgmi" if self.device.type == "cuda" else "gloo"
+        backend = resolve_backend(backend, self.device.type)
         if backend not in ("xgmi", "rccl", "nccl", "gloo"):
             raise ValueError(f"unknown backend {backend!r}")
         if self.device.type == "cpu" and backend != "gloo":

@@ -89,3 +89,22 @@ def test_fedprox_local_steps_changes_trajectory():
                                                early_stop=False), None, init_flat(dims, 0))
     a.run(5); b.run(5)
     assert not np.allclose(a.global_flat(), b.global_flat())
+
+
+@pytest.mark.parametrize("backend", ["torch", pytest.param("hip", marks=pytest.mark.gpu)])
+def test_train_and_evaluate_early_stop_arguments_take_effect(backend):
+    """train_and_evaluate(termination_patience=..., tolerance=...) (C:122) reaches the stop rule
+    the engine runs, not only the printed message: the stop round is the host rule's with
+    the passed patience."""
+    from fedmi.fl.early_stop import EarlyStopper
+    from fedmi.fl.trainer import FederatedMLPLearning
+    torch.set_num_threads(1)
+    X, y = make_income_like(1200, seed=4)
+    tr = FederatedMLPLearning(X, y, 0, 1, config=EngineConfig(max_rounds=120), backend=backend, seed=3)
+    tr.train_and_evaluate(rounds=120, termination_patience=3, tolerance=5e-3, verbose=False)
+    h = tr.history()
+    es = EarlyStopper(3, 5e-3)
+    stop = next(r + 1 for r, v in enumerate(h["global"]) if es.update(v))
+    assert h["stop_round"] == stop == h["rounds_run"]
+    with pytest.raises(RuntimeError):
+        tr.train_and_evaluate(rounds=130, termination_patience=4, verbose=False)

@@ -92,3 +92,20 @@ def test_entrypoint_resume_matches_straight_run(tmp_path):
     for ra, rb in zip(a, b):
         assert ra["round"] == rb["round"]
         assert ra["accuracy"] == rb["accuracy"] and ra["f1"] == rb["f1"]
+
+
+def test_data_plane_env_switch(monkeypatch):
+    """FEDMI_DATA_PLANE selects the GPU FedAvg data plane of backend='auto' (CPU stays gloo)."""
+    from fedmi.parallel.comm import resolve_backend
+    monkeypatch.delenv("FEDMI_DATA_PLANE", raising=False)
+    assert resolve_backend("auto", "cuda") == "xgmi"
+    assert resolve_backend("auto", "cpu") == "gloo"
+    for plane in ("rccl", "xgmi", "nccl"):
+        monkeypatch.setenv("FEDMI_DATA_PLANE", plane.upper())
+        assert resolve_backend("auto", "cuda") == plane
+        assert resolve_backend("auto", "cpu") == "gloo"
+    assert resolve_backend("gloo", "cpu") == "gloo"     # explicit choices are kept
+    monkeypatch.setenv("FEDMI_DATA_PLANE", "tcp")
+    import pytest
+    with pytest.raises(ValueError):
+        resolve_backend("auto", "cuda")
