@@ -45,7 +45,7 @@ def parse_args(argv=None):
     ap.add_argument("--local-steps", type=int, default=1)
     ap.add_argument("--fedprox-mu", type=float, default=0.0)
     ap.add_argument("--participation", type=float, default=1.0,
-                    help="fraction of clients sampled per round (torch engine; 1.0 = all, the reference)")
+                    help="fraction of clients sampled per round (both engines; 1.0 = all, the reference)")
     ap.add_argument("--patience", type=int, default=10)
     ap.add_argument("--tolerance", type=float, default=1e-4)
     ap.add_argument("--no-early-stop", action="store_true")
@@ -101,6 +101,10 @@ def main_wide(a, comm):
 
 def main(argv=None):
     a = parse_args(argv)
+    if not 0.0 < a.participation <= 1.0:
+        raise SystemExit("--participation must be in (0, 1]")
+    if a.wide and a.participation < 1.0:
+        raise SystemExit("--participation < 1 is not supported with --wide (every wide client trains every round)")
     comm = get_world(backend=a.backend, device=a.device)
     if a.wide:
         return main_wide(a, comm)

@@ -7,8 +7,9 @@ format: the ``named_parameters()`` dict ``model.{2i}.weight`` [ou
 
 * ``weights.safetensors``       -- the global (aggregated) model under the reference key
   names, loadable into a plain ``torch.nn`` model of the reference with ``load_state_dict``;
-* ``client{r}.safetensors``     -- per client r: local weights and the flat Adam
-  ``exp_avg`` / ``exp_avg_sq`` (they persist across rounds in the reference, Q6);
+* ``client{r}.safetensors``     -- per client r: local weights, the flat Adam
+  ``exp_avg`` / ``exp_avg_sq`` (they persist across rounds in the reference, Q6) and the
+  client's own Adam step count (client sampling: a client only steps when sampled);
 * ``meta.json``                 -- dims, rounds done (= StepLR counter and Adam step),
   engine config, replicated early-stop state and the metric history.
 
@@ -63,7 +64,9 @@ def save_checkpoint(path: str, trainer) -> None:
     os.makedirs(path, exist_ok=True)
     save_file, _ = _st()
     save_file({"local": np.asarray(st["local"], np.float32), "exp_avg": np.asarray(st["exp_avg"], np.float32),
-               "exp_avg_sq": np.asarray(st["exp_avg_sq"], np.float32)},
+               "exp_avg_sq": np.asarray(st["exp_avg_sq"], np.float32),
+               # this client's own Adam step count (differs from rounds x local_steps when clients are sampled)
+               "opt_steps": np.asarray([int(st.get("opt_steps", 0))], np.int64)},
               os.path.join(path, f"client{eng.rank}.safetensors"))
     if eng.rank == 0:
         save_weights(os.path.join(path, "weights.safetensors"), flat_to_dict(st["global"], eng.dims))
@@ -118,5 +121,7 @@ def resume(path: str, trainer) -> int:
           "history": {"rounds_run": h["rounds_run"], "stop_round": h["stop_round"],
                       "stop_trigger": h["stop_trigger"], "global": np.asarray(h["global"]),
                       "per_rank": np.asarray(h["per_rank"]), "loss": np.asarray(h["loss"])}}
+    if "opt_steps" in c:
+        st["opt_steps"] = int(np.asarray(c["opt_steps"]).reshape(-1)[0])
     eng.load_portable_state(st)
     return st["rounds"]

@@ -20,6 +20,7 @@ weights averaged with weights n_i / N (C:110-116), early stop with patience/atol
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass, field, asdict
 from typing import Dict, List, Optional, Sequence
 
@@ -55,7 +56,9 @@ class EngineConfig:
     # partial participation (client sampling): each round max(1, round(participation * world))
     # clients, drawn by numpy's default Generator seeded with (seed, round) so every rank
     # draws the same set, train and are averaged (weights n_i / sum of the sampled n_i); the
-    # others skip the local step and take the new global model.  Torch engine only.
+    # others skip the local step and take the new global model.  The LR schedule follows the
+    # round index for everyone, Adam's bias correction each client's own step count; global
+    # metrics and loss are the sampled clients'.  Both engines (HIP: a per-round device table).
     participation: float = 1.0
     debug: bool = False             # eager, synchronised phases + non-finite checks every round
     dtype: str = "fp32"             # MFMA operand type of the fused kernels: 'fp32' | 'bf16'
@@ -139,6 +142,22 @@ class RoundEngineBase:
         self.tail_stride = self.n_classes * self.n_classes + 1
         self.hist = _History(cfg.max_rounds, self.world)
         assert init_flat.shape == (self.P,)
+
+    def participants(self, r: int) -> np.ndarray:
+        """Ranks that train and are averaged in round r (all of them unless sampling): the same
+        seeded draw on every rank, so no broadcast is needed."""
+        frac = float(self.cfg.participation)
+        if frac >= 1.0 or self.world == 1:
+            return np.arange(self.world)
+        k = max(1, int(round(frac * self.world)))
+        rng = np.random.default_rng([int(self.cfg.seed), int(r)])
+        return np.sort(rng.choice(self.world, size=k, replace=False))
+
+    def own_steps(self, rounds: int) -> int:
+        """Adam steps this client took in rounds [0, rounds) (it only steps when sampled)."""
+        if float(self.cfg.participation) >= 1.0 or self.world == 1:
+            return rounds * int(self.cfg.local_steps)
+        return sum(int(self.rank in self.participants(r)) for r in range(rounds)) * int(self.cfg.local_steps)
 
     def set_early_stop(self, patience: int, tolerance: float) -> None:
         """Early-stop parameters of ``train_and_evaluate(termination_patience, tolerance)``
@@ -235,8 +254,16 @@ class TorchRoundEngine(RoundEngineBase):
                         p.grad.add_(self.cfg.prox_mu * (p.detach() - anchor[off:off + n].view(shape)))
             self.optimizer.step()
             loss_v = float(loss.detach())
-        self.scheduler.step()
+        self._scheduler_step()
         return loss_v
+
+    def _scheduler_step(self) -> None:
+        """StepLR follows the global round index (C:73 steps it once per round) for every
+        client, sampled or not; only a sampled client's Adam takes a step."""
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)  # "scheduler.step() before optimizer.step()"
+            self.scheduler.step()
 
     def confusion(self, X=None, y=None, flat=None) -> np.ndarray:
         Xt = self.X if X is None else torch.as_tensor(np.asarray(X), dtype=torch.float32, device=self.device)
@@ -256,19 +283,14 @@ class TorchRoundEngine(RoundEngineBase):
         self.stopper = EarlyStopper(cfg.patience, cfg.tolerance, cfg.rtol, enabled=cfg.early_stop)
 
     # -- step-by-step API (reference train_one_epoch / evaluate_local / federated_averaging)
-    def participants(self, r: int) -> np.ndarray:
-        """Ranks that train and are averaged in round r (all of them unless sampling)."""
-        frac = float(self.cfg.participation)
-        if frac >= 1.0 or self.world == 1:
-            return np.arange(self.world)
-        k = max(1, int(round(frac * self.world)))
-        rng = np.random.default_rng([int(self.cfg.seed), int(r)])
-        return np.sort(rng.choice(self.world, size=k, replace=False))
-
     def step_train(self) -> None:
         r = self.rounds_issued
         self._active = self.rank in self.participants(r)
-        self._loss = self.train_one_epoch() if self._active else 0.0
+        if self._active:
+            self._loss = self.train_one_epoch()
+        else:
+            self._loss = 0.0
+            self._scheduler_step()
 
     def step_eval(self) -> np.ndarray:
         self._cm = self.confusion()
@@ -335,13 +357,16 @@ class TorchRoundEngine(RoundEngineBase):
         tails = tail.reshape(self.world, self.tail_stride)
         C = self.n_classes
         per = [metrics_from_confusion(t[:C * C].reshape(C, C)) for t in tails]
+        # global metrics / loss: the round's sampled clients (every client without sampling);
+        # per-client metrics are recorded for all (an unsampled client scores the global model)
+        part = self.participants(r)
         if self.cfg.metric_mode == "mean":
-            g = metric_vector({k: float(np.mean([m[k] for m in per])) for k in METRIC_NAMES})
+            g = metric_vector({k: float(np.mean([per[i][k] for i in part])) for k in METRIC_NAMES})
         else:
-            g = metric_vector(metrics_from_confusion(tails[:, :C * C].sum(0).reshape(C, C)))
+            g = metric_vector(metrics_from_confusion(tails[part, :C * C].sum(0).reshape(C, C)))
         self.hist.glob[r] = g
         self.hist.rank[r] = np.stack([metric_vector(m) for m in per])
-        self.hist.loss[r] = float(tails[:, C * C].mean())
+        self.hist.loss[r] = float(tails[part, C * C].astype(np.float64).sum() / len(part))
         self.hist.rounds_run = r + 1
         if self.stopper.update(g):
             self.hist.stop_trigger = r
@@ -370,9 +395,10 @@ class TorchRoundEngine(RoundEngineBase):
         cat = (lambda ts: np.zeros(self.P, np.float32) if ts[0] is None else
                torch.cat([t.detach().reshape(-1).cpu() for t in ts]).numpy().astype(np.float32))
         sp = self.stopper
+        st0 = self.optimizer.state.get(params[0], {}).get("step")
         return {
             "rounds": int(self.rounds_issued), "global": self.global_flat(), "local": self.local_flat(),
-            "exp_avg": cat(m), "exp_avg_sq": cat(v),
+            "exp_avg": cat(m), "exp_avg_sq": cat(v), "opt_steps": int(st0) if st0 is not None else 0,
             "es": {"count": int(sp.count), "has_prev": sp.prev is not None,
                    "prev": [0.0] * 4 if sp.prev is None else [float(x) for x in sp.prev],
                    "stopped": bool(sp.stopped), "stop_round": int(self.hist.stop_round)},
@@ -385,7 +411,7 @@ class TorchRoundEngine(RoundEngineBase):
         with torch.no_grad():
             self.model.flat.copy_(torch.as_tensor(np.asarray(st["global"], np.float32)))
         self.global_params = self.model.flat.detach().clone()
-        steps = r * int(cfg.local_steps)
+        steps = int(st.get("opt_steps", self.own_steps(r)))   # this client's own Adam steps
         if steps:
             off = 0
             for p in self.model.parameters():
@@ -423,12 +449,12 @@ class HipRoundEngine(RoundEngineBase):
     tensors already on the device (e.g. from the synthetic generator)."""
 
     def __init__(self, X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None, device=None,
-                 comm_buffers=None, emulate_clients: bool = False):
+                 comm_buffers=None, emulate_clients: bool = False, client_sizes=None):
         """``comm_buffers``: optional pair of float32 device views of length
         :meth:`comm_len` to use as the double-buffered FedAvg buffers (trial packing shares one
-        all-reduce between engines by handing each a slice of one allocation)."""
-        if float(cfg.participation) < 1.0 and comm is not None and comm.size > 1:
-            raise NotImplementedError("partial participation runs on the torch engine (--engine torch)")
+        all-reduce between engines by handing each a slice of one allocation).
+        ``client_sizes``: every client's shard size (client sampling weighs the sampled clients
+        by n_i / their sum); gathered over ``comm`` when needed and not given."""
         from ..ops import native
         self.m = native()
         if device is None:
@@ -476,6 +502,11 @@ class HipRoundEngine(RoundEngineBase):
         init["stop_round"] = -1
         st = torch.as_tensor(init.view(np.uint8).copy())
         self.state = [st.to(dev), st.to(dev)]
+        if float(cfg.participation) < 1.0 and self.world > 1 and client_sizes is None:
+            client_sizes = comm.allgather(self.n_local)
+        sched, rtab = self._round_tables(client_sizes)
+        self.sched = torch.as_tensor(sched, device=dev)
+        self.rtab = torch.as_tensor(rtab, device=dev)
         mr = int(cfg.max_rounds)
         self.h_global = torch.zeros(mr * 4, dtype=torch.float64, device=dev)
         self.h_rank = torch.zeros(mr * self.world * 4, dtype=torch.float64, device=dev)
@@ -498,7 +529,8 @@ class HipRoundEngine(RoundEngineBase):
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),
             "local": self.local.data_ptr(), "m": self.mom.data_ptr(), "v": self.vel.data_ptr(),
             "hist_global": self.h_global.data_ptr(), "hist_rank": self.h_rank.data_ptr(),
-            "hist_loss": self.h_loss.data_ptr(), "params0": self.params[0].data_ptr(),
+            "hist_loss": self.h_loss.data_ptr(), "sched": self.sched.data_ptr(), "rtab": self.rtab.data_ptr(),
+            "params0": self.params[0].data_ptr(),
             "params1": self.params[1].data_ptr(), "state0": self.state[0].data_ptr(),
             "state1": self.state[1].data_ptr(),
         }
@@ -535,6 +567,41 @@ class HipRoundEngine(RoundEngineBase):
             if self._peer is not None:
                 self.engine.attach_peer(self._peer)
         self._graph_ready = False
+
+    def _round_tables(self, client_sizes=None):
+        """Host-built device tables (fl_common.h FLBuffers::sched / rtab): per optimizer-step
+        slot the Adam/StepLR scalars of this client's own step count (torch's double arithmetic,
+        rounded to fp32 once), per round its FedAvg weight and the sampled-client set."""
+        cfg = self.cfg
+        mr, LS = max(1, int(cfg.max_rounds)), max(1, int(cfg.local_steps))
+        b1, b2 = float(cfg.betas[0]), float(cfg.betas[1])
+        sched = np.zeros(2 * mr * LS, np.float32)
+        scale = np.zeros(mr, np.float32)
+        count = np.zeros(mr, np.float32)
+        mask = np.zeros((mr, 2), np.uint32)
+        t_own = 0
+        for r in range(mr):
+            part = self.participants(r)
+            active = self.rank in part
+            if len(part) == self.world:
+                w = float(self.n_local) / float(self.n_total)
+            else:
+                w = float(self.n_local) / float(sum(int(client_sizes[k]) for k in part))
+            scale[r] = w if active else 0.0
+            count[r] = len(part)
+            bits = sum(1 << int(k) for k in part)
+            mask[r] = (bits & 0xFFFFFFFF, bits >> 32)
+            lr = float(cfg.lr) * float(cfg.gamma) ** (r // int(cfg.step_size))
+            for ls in range(LS):
+                t_own += int(active)
+                t = max(t_own, 1)
+                sched[2 * (r * LS + ls)] = lr / (1.0 - b1 ** t)
+                sched[2 * (r * LS + ls) + 1] = math.sqrt(1.0 - b2 ** t)
+        rtab = np.zeros((mr, 4), np.uint32)
+        rtab[:, 0] = scale.view(np.uint32)
+        rtab[:, 1] = count.view(np.uint32)
+        rtab[:, 2:] = mask
+        return sched, rtab.reshape(-1).view(np.int32)
 
     def _apply_early_stop(self) -> None:
         cfg = self.cfg
@@ -783,7 +850,7 @@ class HipRoundEngine(RoundEngineBase):
         return {
             "rounds": int(r), "global": self.global_flat(), "local": self.local_flat(),
             "exp_avg": image_to_dense(self.mom.cpu().numpy(), self.dims),
-            "exp_avg_sq": image_to_dense(self.vel.cpu().numpy(), self.dims),
+            "exp_avg_sq": image_to_dense(self.vel.cpu().numpy(), self.dims), "opt_steps": self.own_steps(int(r)),
             "es": {"count": int(st["count"]), "has_prev": bool(st["has_prev"]),
                    "prev": [float(x) for x in st["prev"]], "stopped": bool(st["stopped"]),
                    "stop_round": int(st["stop_round"])},

@@ -40,6 +40,9 @@ class SimRank:
     def __init__(self, size: int, rank: int, device):
         self.size, self.rank, self.device = int(size), int(rank), torch.device(device)
 
+    def Barrier(self) -> None:  # the group's clients run in program order
+        pass
+
 
 class ClientGroup:
     """k clients of one federation in this process."""
@@ -70,7 +73,7 @@ class ClientGroup:
             flat0 = init_flat(dims, seed * 1000003 + r)
             if backend == "hip":
                 e = HipRoundEngine(X[idx[r]], y[idx[r]], n_classes, c, comm, flat0, n_total=n_total,
-                                   device=self.device)
+                                   device=self.device, client_sizes=[len(i) for i in idx])
             elif backend == "torch":
                 e = TorchRoundEngine(X[idx[r]], y[idx[r]], n_classes, c, comm, flat0, n_total=n_total)
             else:

@@ -147,11 +147,19 @@ struct FLBuffers {
     unsigned long long* dbg;  // optional [blocks, 16] s_memrealtime phase stamps (profiling)
     char* pk_global;    // bf16 mode: packed LDS-layout image of the round's input weights
     char* pk_local;     // bf16 mode: packed LDS-layout image of the local (post-Adam) weights
-    // Adam + StepLR scalars per optimizer step t = 1 .. max_rounds * local_steps, computed on
-    // the host in double exactly as torch does (python float pow): [t-1] = {step_size,
-    // sqrt(bias_correction2)} rounded to fp32.  A table lookup instead of three double pow()
-    // on the Adam kernel's critical path.
+    // Adam + StepLR scalars per optimizer step slot t = 1 .. max_rounds * local_steps (slot of
+    // round r, local step ls: r * local_steps + ls + 1), computed on the host in double exactly
+    // as torch does (python float pow): [t-1] = {step_size, sqrt(bias_correction2)} rounded to
+    // fp32, with the bias corrections of the CLIENT'S OWN Adam step count (= t without client
+    // sampling) and the LR of the round.  A table lookup instead of three double pow() on the
+    // Adam kernel's critical path.
     const float* sched;
+    // Per-round FedAvg table [max_rounds][4] = {this client's aggregation weight (n_i / sum of
+    // the round's sampled n_j; 0 when not sampled), sampled-client count, sampled-rank bitmask
+    // bits 0-31, bits 32-63 (bit patterns stored in the float slots)}.  Full participation:
+    // {n_i / N, world, all ones}.  Built on the host from the seeded per-round client sample
+    // (fedmi/fl/engine.py participants()), identical on every rank.
+    const float* rtab;
     float* cnt;         // FL_EVAL_LAGGED: confusion counts of the previous round's local model
     float* lbuf;        // FL_EVAL_LAGGED: the previous round's loss, published one round later
 };

@@ -91,27 +91,39 @@ static __device__ FLState fold_round(const MLPDesc& d, const FLConfig& c, const 
             if (write_hist && r < c.max_rounds)
                 for (int q = 0; q < 4; ++q) b.hist_rank[((size_t)r * c.world + lane) * 4 + q] = mk[q];
         }
+        // the round's sampled clients (all of them without client sampling): the global
+        // metrics and loss are theirs (fl_common.h FLBuffers::rtab)
+        const float* rt = b.rtab + 4 * (size_t)r;
+        const uint32_t m_lo = __float_as_uint(rt[2]), m_hi = __float_as_uint(rt[3]);
+        const double n_act = (double)rt[1];
+        auto sampled = [&](int k) { return ((k < 32 ? (m_lo >> k) : (m_hi >> (k - 32))) & 1u) != 0; };
         double mean[4] = {0, 0, 0, 0};
         double loss = 0;
         for (int k = 0; k < c.world; ++k) {
-            for (int q = 0; q < 4; ++q) mean[q] += __shfl(mk[q], k, 64);
-            loss += __shfl(lk, k, 64);
+            const bool in = sampled(k);
+            for (int q = 0; q < 4; ++q) {
+                const double v = __shfl(mk[q], k, 64);
+                if (in) mean[q] += v;
+            }
+            const double lv = __shfl(lk, k, 64);
+            if (in) loss += lv;
         }
         if (lane != 0) return S;
         if (c.metric_mode == 0) {
-            for (int q = 0; q < 4; ++q) mean[q] /= (double)c.world;
+            for (int q = 0; q < 4; ++q) mean[q] /= n_act;
         } else {
             metrics_from_cm(
                 [&](int t, int p) {
                     double x = 0;
-                    for (int k = 0; k < c.world; ++k) x += (double)tails[k * c.tail_stride + t * C + p];
+                    for (int k = 0; k < c.world; ++k)
+                        if (sampled(k)) x += (double)tails[k * c.tail_stride + t * C + p];
                     return x;
                 },
                 C, mean);
         }
         if (write_hist && r < c.max_rounds) {
             for (int q = 0; q < 4; ++q) b.hist_global[(size_t)r * 4 + q] = mean[q];
-            b.hist_loss[r] = (float)(loss / (double)c.world);
+            b.hist_loss[r] = (float)(loss / n_act);
         }
         if (c.es_enabled) {
             bool close = S.has_prev != 0;

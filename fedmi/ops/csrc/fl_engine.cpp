@@ -239,19 +239,11 @@ class FLEngine {
         pbuf_[1] = as_ptr<float>(bufs["params1"].cast<uintptr_t>());
         st_[0] = as_ptr<FLState>(bufs["state0"].cast<uintptr_t>());
         st_[1] = as_ptr<FLState>(bufs["state1"].cast<uintptr_t>());
+        // Adam/StepLR schedule and per-round FedAvg table (fl_common.h FLBuffers::sched / rtab):
+        // host-built device tables owned by the caller
+        b_.sched = as_ptr<const float>(bufs["sched"].cast<uintptr_t>());
+        b_.rtab = as_ptr<const float>(bufs["rtab"].cast<uintptr_t>());
         {
-            // Adam/StepLR schedule (fl_common.h FLBuffers::sched): torch's host arithmetic
-            const int T = std::max(1, c_.max_rounds) * std::max(1, c_.local_steps);
-            std::vector<float> sch(2 * (size_t)T);
-            for (int t = 1; t <= T; ++t) {
-                const int round = (t - 1) / std::max(1, c_.local_steps);
-                const double lr = c_.lr0 * std::pow(c_.gamma, (double)(round / c_.step_size));
-                sch[2 * (t - 1)] = (float)(lr / (1.0 - std::pow(c_.beta1, (double)t)));
-                sch[2 * (t - 1) + 1] = (float)std::sqrt(1.0 - std::pow(c_.beta2, (double)t));
-            }
-            HIP_CHECK(hipMalloc(&sched_, sch.size() * sizeof(float)));
-            HIP_CHECK(hipMemcpy(sched_, sch.data(), sch.size() * sizeof(float), hipMemcpyHostToDevice));
-            b_.sched = sched_;
             // FL_EVAL_LAGGED: previous round's counts + loss (zero)
             const size_t nlag = FL_MAX_CLASSES * FL_MAX_CLASSES + 4;
             HIP_CHECK(hipMalloc(&lagbuf_, nlag * sizeof(float)));
@@ -271,7 +263,6 @@ class FLEngine {
     ~FLEngine() {
         drop_graph();
         if (pk_) (void)hipFree(pk_);
-        if (sched_) (void)hipFree(sched_);
         if (lagbuf_) (void)hipFree(lagbuf_);
     }
 
@@ -715,7 +706,6 @@ class FLEngine {
     MLPDescB ev_;  // evaluation-only layout of e_ (no delta buffers)
     int dtype_ = 0;  // 0 = fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate / master weights)
     char* pk_ = nullptr;
-    float* sched_ = nullptr;  // Adam/StepLR scalars per optimizer step
     float* lagbuf_ = nullptr;  // FL_EVAL_LAGGED count + loss carry-over
     long long comm_len_ = 0;   // floats of a comm buffer: image + tails (+ lag region)
     bool lag_ok_ = false;      // lagged rounds possible (layout, clients, bf16): see lagged()

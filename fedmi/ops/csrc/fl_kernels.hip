@@ -429,26 +429,32 @@ __device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& 
                                             const FLState& S, int local_step, int last_local_step, int pack, int j,
                                             int pk, bool is_bias, int wlo_delta, float (*part)[64], int lane, float p,
                                             float m, float v, float anc) {
-    float g = 0.f;
+    // this round's FedAvg weight; 0 = the client is not sampled this round: no update, its local
+    // model stays the round's input (global) model and it contributes nothing
+    const float* rt = b.rtab + 4 * (size_t)S.cur_round;
+    const float scale = rt[0];
+    if (scale != 0.f) {
+        float g = 0.f;
 #pragma unroll
-    for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
-    if (c.weight_decay != 0.f) g += c.weight_decay * p;
-    if (c.prox_mu != 0.f) g += c.prox_mu * (p - anc);
-    // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
-    // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
-    // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
-    const int t = S.cur_round * c.local_steps + local_step + 1;
-    const float step_size = b.sched[2 * (t - 1)];
-    const float bc2_sqrt = b.sched[2 * (t - 1) + 1];
-    m = m + c.omb1 * (g - m);
-    v = v * c.beta2f + c.omb2 * g * g;
-    const float denom = sqrtf(v) / bc2_sqrt + c.eps;
-    p = p + (-step_size) * (m / denom);
-    b.m[j] = m;
-    b.v[j] = v;
+        for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
+        if (c.weight_decay != 0.f) g += c.weight_decay * p;
+        if (c.prox_mu != 0.f) g += c.prox_mu * (p - anc);
+        // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
+        // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
+        // p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).  StepLR steps once per round.
+        const int t = S.cur_round * c.local_steps + local_step + 1;
+        const float step_size = b.sched[2 * (t - 1)];
+        const float bc2_sqrt = b.sched[2 * (t - 1) + 1];
+        m = m + c.omb1 * (g - m);
+        v = v * c.beta2f + c.omb2 * g * g;
+        const float denom = sqrtf(v) / bc2_sqrt + c.eps;
+        p = p + (-step_size) * (m / denom);
+        b.m[j] = m;
+        b.v[j] = v;
+    }
     b.local[j] = p;
     if (pack) pack_store(b.pk_local, pk, is_bias, wlo_delta, p);
-    if (last_local_step) comm[j] = p * c.agg_scale;
+    if (last_local_step) comm[j] = p * scale;
 }
 
 // Chunk ids of the Adam-fused exchange (peer_device.h): the final metric tails, the early lag

@@ -97,8 +97,8 @@ def _sampling_worker(rank, world, port, q):
         local = e.local_flat()
         e.step_eval()
         e.step_aggregate()
-        out.append((list(e.participants(r)), g0, local, e.global_flat()))
-    q.put((rank, len(idx), out))
+        out.append((list(e.participants(r)), g0, local, e.global_flat(), e._loss))
+    q.put((rank, len(idx), out, e.history()))
     comm.close()
 
 
@@ -130,3 +130,10 @@ def test_partial_participation_over_gloo():
             np.testing.assert_array_equal(x[2][r][3], res[0][2][r][3])
     # different rounds draw different sets (seeded per round)
     assert len({tuple(res[0][2][r][0]) for r in range(3)}) > 1
+    # global loss and metrics are the sampled clients' (unsampled ones post no loss and score the
+    # global model they hold, kept in the per-client history)
+    h = res[0][3]
+    for r in range(3):
+        parts = res[0][2][r][0]
+        assert abs(h["loss"][r] - np.mean([res[k][2][r][4] for k in parts])) < 1e-6
+        np.testing.assert_allclose(h["global"][r], h["per_rank"][r][parts].mean(axis=0), atol=1e-12)
