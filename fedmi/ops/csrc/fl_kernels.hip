@@ -428,11 +428,9 @@ __device__ __forceinline__ void pack_store(char* img, int pk, bool is_bias, int 
 __device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& b, float* __restrict__ comm,
                                             const FLState& S, int local_step, int last_local_step, int pack, int j,
                                             int pk, bool is_bias, int wlo_delta, float (*part)[64], int lane, float p,
-                                            float m, float v, float anc) {
-    // this round's FedAvg weight; 0 = the client is not sampled this round: no update, its local
-    // model stays the round's input (global) model and it contributes nothing
-    const float* rt = b.rtab + 4 * (size_t)S.cur_round;
-    const float scale = rt[0];
+                                            float m, float v, float anc, float scale) {
+    // `scale`: this round's FedAvg weight (rtab); 0 = the client is not sampled this round: no
+    // update, its local model stays the round's input (global) model and it contributes nothing
     if (scale != 0.f) {
         float g = 0.f;
 #pragma unroll
@@ -615,12 +613,16 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         return;
     }
     // wave 0's operands of the update, issued before the slab loads so their latency overlaps
-    float p0 = 0.f, m0 = 0.f, v0 = 0.f, a0 = 0.f;
+    float p0 = 0.f, m0 = 0.f, v0 = 0.f, a0 = 0.f, sc0 = 0.f;
     if (wave == 0 && valid) {
         p0 = pin[j];
         m0 = b.m[j];
         v0 = b.v[j];
         a0 = anchor[j];
+        // the round this step belongs to whenever it is live: the folded state's next round, or
+        // the running one
+        const int rg = fold ? st->next_round : st->cur_round;
+        sc0 = b.rtab[4 * (size_t)min(max(rg, 0), c.max_rounds - 1)];
     }
     float g = 0.f;
     bool have_state = false;
@@ -653,7 +655,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             if (last_local_step) comm[j] = (c.rank == 0) ? a0 : 0.f;
         } else {
             adam_update(c, b, comm, S, local_step, last_local_step, pack, j, pk, is_bias, e.wlo_delta, part, lane, p0,
-                        m0, v0, a0);
+                        m0, v0, a0, sc0);
         }
     }
     if (xchg) {

@@ -130,9 +130,9 @@ __device__ __forceinline__ unsigned peer_target(const PeerArgs& a) {
 }
 
 // Lanes 0..world-1: store `target` into every rank's flag slot for this rank.
+__device__ __forceinline__ void peer_flag_store(unsigned* dst, unsigned v);
 __device__ __forceinline__ void peer_publish(unsigned* const* dst, int world, unsigned target) {
-    if (threadIdx.x < (unsigned)world)
-        __hip_atomic_store(dst[threadIdx.x], target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x < (unsigned)world) peer_flag_store(dst[threadIdx.x], target);
 }
 
 // Memory ordering of the protocol (publisher on GPU j, reader on GPU i):
@@ -145,7 +145,26 @@ __device__ __forceinline__ void peer_publish(unsigned* const* dst, int world, un
 //              in addition uses cache-bypassing (sc0 sc1) loads.
 // Release / acquire pair at system scope: correct across GPUs by construction, not only on
 // one device where the tests run.
-__device__ __forceinline__ void peer_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+// PEER_FENCES (build option, A/B-measured in profiles/peer_fences_r2.log): 2 = release publishes +
+// acquire fences (default); 1 = acquire fences, publishes ordered by s_waitcnt vmcnt(0) only (the
+// data live in uncached memory, so their stores are complete when acknowledged); 0 = neither.
+#ifndef PEER_FENCES
+#define PEER_FENCES 2
+#endif
+__device__ __forceinline__ void peer_acquire() {
+#if PEER_FENCES >= 1
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
+}
+// flag publish of a value whose data this wave stored into the uncached send buffer
+__device__ __forceinline__ void peer_flag_store(unsigned* dst, unsigned v) {
+#if PEER_FENCES >= 2
+    __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+}
 
 // Wait until every rank has published `target` in `flags` (one polling lane per rank,
 // bounded by the timeout: on expiry the sticky error word is set and the wait ends).
@@ -290,8 +309,7 @@ __device__ __forceinline__ void peer_eval_done(const PeerArgs& a, unsigned targe
 // (the caller's stores of the chunk are this wave's: the release store waits for all of them)
 __device__ __forceinline__ void peer_chunk_publish(const PeerArgs& a, int chunk, unsigned target) {
     const int lane = threadIdx.x & 63;
-    if (lane < a.world)
-        __hip_atomic_store(a.cflag_dst[lane] + chunk, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane < a.world) peer_flag_store(a.cflag_dst[lane] + chunk, target);
 }
 __device__ __forceinline__ void peer_chunk_wait(const PeerArgs& a, int chunk, unsigned target) {
     const int lane = threadIdx.x & 63;
