@@ -39,6 +39,7 @@ class PeerAllReduce {
     int rank() const { return rank_; }
     int n_chunks() const { return n_chunks_; }
     bool is_open() const { return open_; }
+    bool uncached() const { return uncached_; }         // send buffers in uncached memory
     void close();
 
   private:
@@ -51,6 +52,7 @@ class PeerAllReduce {
     char* peer_base_[PEER_MAX_WORLD] = {};
     long long timeout_ticks_ = 0;      // s_memrealtime ticks (100 MHz)
     bool open_ = false;
+    bool uncached_ = true;
     unsigned* eflags_ = nullptr;       // fused calls: one completion flag per evaluation block
     int n_eval_ = 0;
 };

@@ -52,8 +52,8 @@ static void phip(hipError_t e, const char* what) {
 __global__ void __launch_bounds__(PEER_THREADS) peer_allreduce_kernel(PeerArgs a, PeerPack pk) {
     const unsigned target = peer_target(a);
     if (blockIdx.x == 0) {
-        peer_publish(a.flag_dst, a.world, target);
-        peer_publish(a.tflag_dst, a.world, target);
+        peer_publish(a.flag_dst, a.world, target, a.uc);
+        peer_publish(a.tflag_dst, a.world, target, a.uc);
     }
     peer_wait(a, a.ctl->flags, target);
     peer_reduce4<PEER_MAX_WORLD>(a, pk, 0, a.n >> 2, blockIdx.x, gridDim.x);
@@ -91,9 +91,11 @@ PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, doubl
     // flags and read the send buffers over xGMI, and no L2 -- this GPU's or a peer's -- may
     // hold a stale copy of either.  The send buffers are written once per round (~50 KB),
     // so bypassing the L2 costs nothing measurable.
+    uncached_ = true;
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&base_), total_, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         base_ = nullptr;
+        uncached_ = false;  // cacheable fallback: flag publishes become system-scope releases
         PHIP(hipMalloc(reinterpret_cast<void**>(&base_), total_));
     }
     PHIP(hipMemset(base_, 0, total_));
@@ -204,6 +206,7 @@ PeerArgs PeerAllReduce::args(int parity, float* out, long long n_w) const {
     a.eflags = eflags_;
     a.n_eval = n_eval_;
     a.world = world_;
+    a.uc = uncached_ ? 1 : 0;
     a.n_chunks = n_chunks_;
     if (n_chunks_ > 0) {
         for (int j = 0; j < world_; ++j)
@@ -267,5 +270,6 @@ void register_peer(py::module_& m) {
         .def_property_readonly("world", &PeerAllReduce::world)
         .def_property_readonly("rank", &PeerAllReduce::rank)
         .def_property_readonly("n_floats", &PeerAllReduce::n_floats)
-        .def_property_readonly("is_open", &PeerAllReduce::is_open);
+        .def_property_readonly("is_open", &PeerAllReduce::is_open)
+        .def_property_readonly("uncached", &PeerAllReduce::uncached);
 }

@@ -60,6 +60,7 @@ struct PeerArgs {
     unsigned* eflags;                    // fused calls: per evaluation block, last call it finished
     int n_eval;                          // evaluation blocks of a fused call
     int world;
+    int uc;                              // send buffers are uncached memory (see peer_flag_store)
     // Adam-fused exchange (chunked flags, call index = FLState::calls): chunk k of call t
     // published by rank j  <=>  cflags_j... row of rank j in MY chunk-flag table >= t
     unsigned* cflag_dst[PEER_MAX_WORLD]; // &chunk_flags_j[rank * n_chunks]: my row in rank j's table
@@ -130,9 +131,9 @@ __device__ __forceinline__ unsigned peer_target(const PeerArgs& a) {
 }
 
 // Lanes 0..world-1: store `target` into every rank's flag slot for this rank.
-__device__ __forceinline__ void peer_flag_store(unsigned* dst, unsigned v);
-__device__ __forceinline__ void peer_publish(unsigned* const* dst, int world, unsigned target) {
-    if (threadIdx.x < (unsigned)world) peer_flag_store(dst[threadIdx.x], target);
+__device__ __forceinline__ void peer_flag_store(unsigned* dst, unsigned v, int uc);
+__device__ __forceinline__ void peer_publish(unsigned* const* dst, int world, unsigned target, int uc) {
+    if (threadIdx.x < (unsigned)world) peer_flag_store(dst[threadIdx.x], target, uc);
 }
 
 // Memory ordering of the protocol (publisher on GPU j, reader on GPU i):
@@ -145,25 +146,22 @@ __device__ __forceinline__ void peer_publish(unsigned* const* dst, int world, un
 //              in addition uses cache-bypassing (sc0 sc1) loads.
 // Release / acquire pair at system scope: correct across GPUs by construction, not only on
 // one device where the tests run.
-// PEER_FENCES (build option, A/B-measured in profiles/peer_fences_r2.log): 2 = release publishes +
-// acquire fences (default); 1 = acquire fences, publishes ordered by s_waitcnt vmcnt(0) only (the
-// data live in uncached memory, so their stores are complete when acknowledged); 0 = neither.
-#ifndef PEER_FENCES
-#define PEER_FENCES 2
-#endif
-__device__ __forceinline__ void peer_acquire() {
-#if PEER_FENCES >= 1
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-#endif
-}
-// flag publish of a value whose data this wave stored into the uncached send buffer
-__device__ __forceinline__ void peer_flag_store(unsigned* dst, unsigned v) {
-#if PEER_FENCES >= 2
-    __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
+// Fence strength.  Reader: an acquire fence (system scope) after every wait.  Writer: when the
+// send buffers are UNCACHED memory (the normal case, PeerArgs::uc), a data store is complete once
+// acknowledged, so `s_waitcnt vmcnt(0)` before the flag store is the release; if the uncached
+// allocation was refused and the buffers are ordinary (cacheable) memory, the flag store is a
+// system-scope RELEASE (which also writes this GPU's dirty L2 lines back).  A/B on the emulated
+// multi-client round (profiles/peer_fences_r2.log): release stores on every Adam block cost
+// 1.0-1.6 us per round, the acquire fences 0.6 us.
+__device__ __forceinline__ void peer_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+// flag publish of a value whose data this wave stored into the send buffer
+__device__ __forceinline__ void peer_flag_store(unsigned* dst, unsigned v, int uc) {
+    if (uc) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Wait until every rank has published `target` in `flags` (one polling lane per rank,
@@ -279,12 +277,12 @@ __device__ __forceinline__ void peer_wait_eval(const PeerArgs& a, unsigned targe
 // reduces them.
 __device__ __forceinline__ void peer_fused_reduce(const PeerArgs& a, const PeerPack& pk, unsigned target, int bid,
                                                   int nb) {
-    if (bid == 0) peer_publish(a.flag_dst, a.world, target);
+    if (bid == 0) peer_publish(a.flag_dst, a.world, target, a.uc);
     peer_wait(a, a.ctl->flags, target);
     peer_reduce4<2>(a, pk, 0, a.n_w >> 2, bid, nb);
     if (bid == 0) {
         peer_wait_eval(a, target);
-        peer_publish(a.tflag_dst, a.world, target);
+        peer_publish(a.tflag_dst, a.world, target, a.uc);
         peer_wait(a, a.ctl->tflags, target);
         peer_reduce1(a, a.n_w, a.n);
     }
@@ -309,7 +307,7 @@ __device__ __forceinline__ void peer_eval_done(const PeerArgs& a, unsigned targe
 // (the caller's stores of the chunk are this wave's: the release store waits for all of them)
 __device__ __forceinline__ void peer_chunk_publish(const PeerArgs& a, int chunk, unsigned target) {
     const int lane = threadIdx.x & 63;
-    if (lane < a.world) peer_flag_store(a.cflag_dst[lane] + chunk, target);
+    if (lane < a.world) peer_flag_store(a.cflag_dst[lane] + chunk, target, a.uc);
 }
 __device__ __forceinline__ void peer_chunk_wait(const PeerArgs& a, int chunk, unsigned target) {
     const int lane = threadIdx.x & 63;
