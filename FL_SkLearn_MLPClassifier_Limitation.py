@@ -61,14 +61,28 @@ class FederatedMLPLearning:
         self.global_weights = average_estimator_weights(self.local_model, comm, weighting="uniform")
         self._set_weights(self.global_weights)
 
-    def train_and_evaluate(self, comm, rounds=1):
+    def train_and_evaluate(self, comm, rounds=1, save=None, resume=None):
+        """S:68-153.  ``save``: checkpoint directory written after every round in the reference's
+        exchange layout (coefs_ + intercepts_, float64 [in, out]); ``resume``: continue such a run."""
+        from fedmi.ckpt.checkpoint import load_sklearn_run, save_sklearn_run
         self.local_model = MLPClassifier(activation="relu", hidden_layer_sizes=self.hidden,
                                          learning_rate_init=self.lr, max_iter=self.max_iter, random_state=42,
                                          warm_start=self.warm_start, backend=self.backend)
         classes = np.unique(self.y_local)
         self.local_model.partial_fit(self.X_local, self.y_local, classes=classes)
         history = []
-        for rnd in range(rounds):
+        start = 0
+        if resume:
+            ck = load_sklearn_run(resume, self.rank)
+            m = ck["meta"]
+            if list(m["hidden"]) != list(self.hidden) or int(m["world"]) != self.size:
+                raise ValueError(f"{resume}: saved for hidden {m['hidden']} x {m['world']} clients")
+            start, history = int(m["rounds"]), list(m["history"])
+            self.global_weights = ck["global"]
+            self._set_weights(ck["local"])
+            if self.rank == 0:
+                print(f"Resumed from {resume} after {start} rounds", flush=True)
+        for rnd in range(start, rounds):
             print(f"\n[Rank {self.rank}] Starting Round {rnd + 1}", flush=True)
             if rnd > 0 and self.global_weights is not None:
                 self._set_weights(self.global_weights)
@@ -82,7 +96,7 @@ class FederatedMLPLearning:
                 print(f"[Rank {self.rank}] Computed global weights after Round {rnd + 1}", flush=True)
             cm = allreduce_confusion(confusion_matrix(self.y_local, y_pred, 2), comm)
             g = metrics_from_confusion(cm)
-            history.append({"local": local_metrics, "global": g, "n_iter": self.local_model.n_iter_})
+            history.append({"local": local_metrics, "global": g, "n_iter": int(self.local_model.n_iter_)})
             if self.rank == 0:
                 print(f"\n[Rank {self.rank}] Global Metrics for Round {rnd + 1}:")
                 print(f"  Accuracy: {g['accuracy']:.4f}")
@@ -92,7 +106,12 @@ class FederatedMLPLearning:
                 print("-" * 50, flush=True)
             if comm is not None:
                 comm.Barrier()
-        if self.rank == 0:
+            if save:
+                save_sklearn_run(save, self.rank, rnd + 1, self.global_weights,
+                                 list(self.local_model.coefs_) + list(self.local_model.intercepts_),
+                                 {"hidden": list(self.hidden), "lr": self.lr, "max_iter": self.max_iter,
+                                  "warm_start": self.warm_start, "world": self.size, "history": history}, comm)
+        if self.rank == 0 and self.global_weights is not None:
             print("\nFinal Global Weight Statistics:")
             for idx, w in enumerate(self.global_weights):
                 print(f"Layer {idx + 1} - Shape: {w.shape}")
@@ -111,6 +130,8 @@ def main(argv=None):
     ap.add_argument("--warm-start", action="store_true", help="keep the averaged weights across rounds (fixes Q8)")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--backend", default="auto", help="estimator backend: hip | numpy")
+    ap.add_argument("--save", default=None, help="checkpoint directory (coefs_ + intercepts_ layout), every round")
+    ap.add_argument("--resume", default=None, help="continue a run saved with --save")
     a = ap.parse_args(argv)
     comm = get_world(backend="gloo" if a.device == "cpu" else "auto", device=a.device)
     ds = load_tabular(a.data, label=a.label, with_mean=False)
@@ -119,7 +140,7 @@ def main(argv=None):
         backend = "hip" if comm.device.type == "cuda" else "numpy"
     tr = FederatedMLPLearning(ds.X_train, ds.y_train, comm.rank, comm.size, comm=comm, hidden=tuple(a.hidden),
                               lr=a.lr, max_iter=a.max_iter, warm_start=a.warm_start, backend=backend)
-    hist = tr.train_and_evaluate(comm, rounds=a.rounds)
+    hist = tr.train_and_evaluate(comm, rounds=a.rounds, save=a.save, resume=a.resume)
     comm.close()
     return hist
 

@@ -125,3 +125,72 @@ def resume(path: str, trainer) -> int:
         st["opt_steps"] = int(np.asarray(c["opt_steps"]).reshape(-1)[0])
     eng.load_portable_state(st)
     return st["rounds"]
+
+
+# ---------------------------------------------------------------------------------------
+# sklearn layout ([S] / [H] flows): the exchange list coefs_ + intercepts_ (S:26, S:109, H:30)
+# ---------------------------------------------------------------------------------------
+SK_FORMAT = "fedmi-sklearn-ckpt-1"
+
+
+def save_sklearn_weights(path: str, weights) -> None:
+    """``weights`` = the reference's flat exchange list ``coefs_ + intercepts_``: L coefficient
+    matrices [in, out] then L intercept vectors, float64 (S:26).  Stored as safetensors keys
+    ``coefs_.{i}`` / ``intercepts_.{i}``, float64, same shapes."""
+    save_file, _ = _st()
+    ws = [np.asarray(w, dtype=np.float64) for w in weights]
+    L = len(ws) // 2
+    if len(ws) != 2 * L or any(ws[i].ndim != 2 or ws[L + i].shape != (ws[i].shape[1],) for i in range(L)):
+        raise ValueError("expected coefs_ ([in, out] matrices) followed by intercepts_ ([out] vectors)")
+    t = {f"coefs_.{i}": np.ascontiguousarray(ws[i]) for i in range(L)}
+    t.update({f"intercepts_.{i}": np.ascontiguousarray(ws[L + i]) for i in range(L)})
+    save_file(t, path)
+
+
+def load_sklearn_weights(path: str):
+    """Inverse of :func:`save_sklearn_weights`: the ``coefs_ + intercepts_`` list, float64."""
+    _, load_file = _st()
+    t = dict(load_file(path))
+    L = sum(1 for k in t if k.startswith("coefs_."))
+    if L == 0 or any(f"coefs_.{i}" not in t or f"intercepts_.{i}" not in t for i in range(L)):
+        raise ValueError(f"{path}: not a coefs_/intercepts_ checkpoint")
+    return [t[f"coefs_.{i}"] for i in range(L)] + [t[f"intercepts_.{i}"] for i in range(L)]
+
+
+def sklearn_to_torch_layout(weights):
+    """coefs_ + intercepts_ ([in, out]) -> the [C] ``model.{2i}.weight`` [out, in] / ``.bias`` dict."""
+    L = len(weights) // 2
+    out = {}
+    for i in range(L):
+        out[f"model.{2 * i}.weight"] = np.ascontiguousarray(np.asarray(weights[i]).T, dtype=np.float32)
+        out[f"model.{2 * i}.bias"] = np.asarray(weights[L + i], dtype=np.float32)
+    return out
+
+
+def save_sklearn_run(path: str, rank: int, round_done: int, global_weights, local_weights, meta: dict,
+                     comm=None) -> None:
+    """[S] round checkpoint (collective): rank 0 writes ``global.safetensors`` + ``meta.json``
+    (rounds done, history, run settings), every rank its local model ``client{r}.safetensors``."""
+    os.makedirs(path, exist_ok=True)
+    save_sklearn_weights(os.path.join(path, f"client{rank}.safetensors"), local_weights)
+    if rank == 0:
+        if global_weights is not None:
+            save_sklearn_weights(os.path.join(path, "global.safetensors"), global_weights)
+        m = dict(meta, format=SK_FORMAT, rounds=int(round_done))
+        tmp = os.path.join(path, "meta.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(m, f)
+        os.replace(tmp, os.path.join(path, "meta.json"))
+    if comm is not None and getattr(comm, "size", 1) > 1:
+        comm.Barrier()
+
+
+def load_sklearn_run(path: str, rank: int) -> dict:
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    if meta.get("format") != SK_FORMAT:
+        raise ValueError(f"{path}: unsupported checkpoint format {meta.get('format')!r}")
+    out = {"meta": meta, "local": load_sklearn_weights(os.path.join(path, f"client{rank}.safetensors"))}
+    gp = os.path.join(path, "global.safetensors")
+    out["global"] = load_sklearn_weights(gp) if os.path.isfile(gp) else None
+    return out

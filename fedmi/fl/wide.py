@@ -400,3 +400,56 @@ def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int
     return {"loss": losses, "accuracy": accs, "round_s": times, "median_round_s": dt,
             "tflops_per_client": c.flops_per_round / dt / 1e12,
             "samples_per_s_per_client": rows_per_client / dt}
+
+
+def save_wide(path: str, client: WideClient) -> None:
+    """Wide-client checkpoint (rank 0 writes the global weights, every rank its Adam state):
+    ``weights.safetensors`` under the reference's ``model.{2i}.weight`` [out, in] / ``.bias`` keys
+    (C:93-94), ``client{r}.safetensors`` with the flat fp32 Adam moments, ``wide_meta.json`` with the
+    dims and the round (= StepLR epoch and Adam step; every wide client trains every round)."""
+    import json
+    import os
+    from ..ckpt.checkpoint import save_weights
+    from ..models.mlp import flat_to_dict
+    from safetensors.numpy import save_file
+    client.sync()
+    client.stream.synchronize()
+    rank = client.comm.rank if client.comm is not None else 0
+    os.makedirs(path, exist_ok=True)
+    save_file({"exp_avg": client.m_.cpu().numpy(), "exp_avg_sq": client.v_.cpu().numpy()},
+              os.path.join(path, f"client{rank}.safetensors"))
+    if rank == 0:
+        save_weights(os.path.join(path, "weights.safetensors"), flat_to_dict(client.params.cpu().numpy(), client.dims))
+        with open(os.path.join(path, "wide_meta.json"), "w") as f:
+            json.dump({"format": "fedmi-wide-ckpt-1", "dims": client.dims, "round": int(client.round),
+                       "world": client.world, "lr": client.lr, "step_size": client.step_size,
+                       "gamma": client.gamma}, f)
+    if client.comm is not None and client.world > 1:
+        client.comm.Barrier()
+
+
+def load_wide(path: str, client: WideClient) -> int:
+    """Restore :func:`save_wide` into a client of the same dims / client count; returns the round."""
+    import json
+    import os
+    from ..ckpt.checkpoint import load_weights
+    from ..models.mlp import dict_to_flat
+    from safetensors.numpy import load_file
+    with open(os.path.join(path, "wide_meta.json")) as f:
+        meta = json.load(f)
+    if meta.get("format") != "fedmi-wide-ckpt-1" or list(meta["dims"]) != client.dims:
+        raise ValueError(f"{path}: not a wide checkpoint for dims {client.dims}")
+    if int(meta["world"]) != client.world:
+        raise ValueError(f"{path}: saved with {meta['world']} clients, this run has {client.world}")
+    rank = client.comm.rank if client.comm is not None else 0
+    flat = dict_to_flat(load_weights(os.path.join(path, "weights.safetensors")), client.dims)
+    st = load_file(os.path.join(path, f"client{rank}.safetensors"))
+    client.sync()
+    with torch.cuda.stream(client.stream):
+        client.params.copy_(torch.as_tensor(flat, device=client.dev))
+        client.m_.copy_(torch.as_tensor(st["exp_avg"], device=client.dev))
+        client.v_.copy_(torch.as_tensor(st["exp_avg_sq"], device=client.dev))
+    client._quantize()
+    client.stream.synchronize()
+    client.round = int(meta["round"])
+    return client.round

@@ -40,11 +40,25 @@ class TrialResult:
 
 def run_sweep(X_local, y_local, comm, hidden_grid: Sequence = HIDDEN_GRID, lr_grid: Sequence = LR_GRID,
               max_iter: int = 400, random_state: int = 42, backend: str = "auto", packed: bool = True,
-              on_trial=None) -> Tuple[Optional[TrialResult], List[TrialResult]]:
-    results: List[TrialResult] = []
-    best: Optional[TrialResult] = None
+              on_trial=None, done: Sequence[TrialResult] = ()) -> Tuple[Optional[TrialResult], List[TrialResult]]:
+    """``done``: results of an earlier (checkpointed) sweep; their hidden configs are not trained
+    again and the best trial is taken over old and new results in grid order."""
     classes = np.unique(y_local)
     n_cls = max(2, len(classes))
+    have = {(tuple(r.hidden), float(r.lr)): r for r in done}
+    todo = [hl for hl in hidden_grid if any((tuple(hl), float(lr)) not in have for lr in lr_grid)]
+    fresh = _train(X_local, y_local, comm, todo, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial)
+    results = [have.get((tuple(hl), float(lr))) or fresh[(tuple(hl), float(lr))] for hl in hidden_grid
+               for lr in lr_grid]
+    best: Optional[TrialResult] = None
+    for res in results:
+        if best is None or res.global_["accuracy"] > best.global_["accuracy"]:
+            best = res
+    return best, results
+
+
+def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial):
+    out = {}
     groups = [[MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=max_iter,
                              random_state=random_state, backend=backend) for lr in lr_grid] for hl in hidden_grid]
     # Training needs no communication (every trial fits from scratch, Q8): on the GPU the
@@ -80,9 +94,38 @@ def run_sweep(X_local, y_local, comm, hidden_grid: Sequence = HIDDEN_GRID, lr_gr
             cm = allreduce_confusion(confusion_matrix(y_local, y_pred, n_cls), comm)
             res = TrialResult(tuple(hl), float(lr), local, metrics_from_confusion(cm), int(est.n_iter_),
                               [np.copy(w) for w in gw])
-            results.append(res)
+            out[(tuple(hl), float(lr))] = res
             if on_trial is not None:
                 on_trial(res)
-            if best is None or res.global_["accuracy"] > best.global_["accuracy"]:
-                best = res
-    return best, results
+    return out
+
+
+def save_sweep(path: str, results: Sequence[TrialResult], best: Optional[TrialResult], meta: dict) -> None:
+    """[H] checkpoint: every trial's metrics (JSON) + the best trial's averaged weights in the
+    reference's coefs_ + intercepts_ layout (H:119, H:130-132) as ``best.safetensors``."""
+    import json
+    import os
+    from ..ckpt.checkpoint import save_sklearn_weights
+    os.makedirs(path, exist_ok=True)
+    if best is not None:
+        save_sklearn_weights(os.path.join(path, "best.safetensors"), best.weights)
+    rows = [{"hidden": list(r.hidden), "lr": r.lr, "local": r.local, "global": r.global_, "n_iter": r.n_iter}
+            for r in results]
+    with open(os.path.join(path, "sweep.json"), "w") as f:
+        json.dump(dict(meta, trials=rows, best={"hidden": list(best.hidden), "lr": best.lr} if best else None), f)
+    # every trial's averaged weights, so a resumed sweep can still return any of them as the best
+    for i, r in enumerate(results):
+        save_sklearn_weights(os.path.join(path, f"trial{i}.safetensors"), r.weights)
+
+
+def load_sweep(path: str) -> List[TrialResult]:
+    import json
+    import os
+    from ..ckpt.checkpoint import load_sklearn_weights
+    with open(os.path.join(path, "sweep.json")) as f:
+        m = json.load(f)
+    out = []
+    for i, r in enumerate(m["trials"]):
+        w = load_sklearn_weights(os.path.join(path, f"trial{i}.safetensors"))
+        out.append(TrialResult(tuple(r["hidden"]), float(r["lr"]), r["local"], r["global"], int(r["n_iter"]), w))
+    return out

@@ -95,6 +95,10 @@ def main(argv=None):
     ap.add_argument("--no-pack", action="store_true", help="fit trials one by one")
     ap.add_argument("--quiet", action="store_true", help="only print the best result")
     ap.add_argument("--json", default=None, help="write all trial results here (rank 0)")
+    ap.add_argument("--save", default=None,
+                    help="checkpoint directory (rank 0): trial results + every trial's averaged weights and the "
+                         "best one as best.safetensors, coefs_ + intercepts_ layout (float64, [in, out])")
+    ap.add_argument("--resume", default=None, help="reuse the trials of a sweep saved with --save")
     ap.add_argument("--federated", action="store_true",
                     help="round-engine sweep over hidden x lr x local steps (BASELINE config 5)")
     ap.add_argument("--local-steps", type=int, nargs="+", default=None, help="--federated: local steps grid")
@@ -124,14 +128,21 @@ def main(argv=None):
             print(f"\t[Rank {rank}] Global Metrics (Hidden Layers: {res.hidden}, LR: {res.lr}): {res.global_}\n")
             print("-" * 50, flush=True)
 
+    from fedmi.hpo.sweep import load_sweep, save_sweep
+    done = load_sweep(a.resume) if a.resume else []
+    if done and rank == 0:
+        print(f"Resumed {len(done)} trials from {a.resume}", flush=True)
     t0 = time.time()
     best, results = None, []
     for rnd in range(a.rounds):
         if rank == 0:
             print(f"Training Round {rnd + 1}...\n{'-' * 50}")
         best, results = run_sweep(X_local, y_local, comm, hidden, lrs, max_iter=a.max_iter, backend=backend,
-                                  packed=not a.no_pack, on_trial=report)
+                                  packed=not a.no_pack, on_trial=report, done=done)
     wall = time.time() - t0
+    if a.save and rank == 0:
+        save_sweep(a.save, results, best, {"world": comm.Get_size(), "max_iter": a.max_iter})
+    comm.Barrier()
     if rank == 0:
         print("\n\nBest MEASURED RESULTS")
         print("\nBest Global Hyperparameters:", {"hidden_layer_sizes": best.hidden, "learning_rate": best.lr})

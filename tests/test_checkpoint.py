@@ -64,3 +64,80 @@ def test_resume_rejects_mismatched_dims(tmp_path):
     save_checkpoint(str(tmp_path), e)
     with pytest.raises(ValueError):
         resume(str(tmp_path), _engine(X, y, [14, 9, 2]))
+
+
+def test_sklearn_layout_roundtrip(tmp_path):
+    """[S]/[H] exchange layout (S:26): coefs_ [in, out] then intercepts_, float64."""
+    from fedmi.ckpt.checkpoint import load_sklearn_weights, save_sklearn_weights, sklearn_to_torch_layout
+    rs = np.random.RandomState(0)
+    dims = [14, 50, 400, 1]
+    coefs = [rs.randn(a, b) for a, b in zip(dims[:-1], dims[1:])]
+    inter = [rs.randn(b) for b in dims[1:]]
+    save_sklearn_weights(str(tmp_path / "w.safetensors"), coefs + inter)
+    back = load_sklearn_weights(str(tmp_path / "w.safetensors"))
+    assert len(back) == 6 and all(b.dtype == np.float64 for b in back)
+    for a, b in zip(coefs + inter, back):
+        np.testing.assert_array_equal(a, b)
+    t = sklearn_to_torch_layout(back)
+    assert t["model.2.weight"].shape == (400, 50) and t["model.4.bias"].shape == (1,)
+    with pytest.raises(ValueError):
+        save_sklearn_weights(str(tmp_path / "bad.safetensors"), coefs)   # intercepts missing
+
+
+def test_sklearn_flow_save_resume_exact(tmp_path):
+    """[S] rounds with --save, interrupted after round 2 and resumed: same global weights and
+    history as the uninterrupted run (warm start, numpy float64 backend)."""
+    import importlib
+    S = importlib.import_module("FL_SkLearn_MLPClassifier_Limitation")
+    from fedmi.data.tabular import load_tabular
+    ds = load_tabular(with_mean=False)
+    X, y = ds.X_train[:600], ds.y_train[:600]
+    mk = lambda: S.FederatedMLPLearning(X, y, 0, 1, hidden=(8, 6), max_iter=15, warm_start=True, backend="numpy")
+    full = mk()
+    h_full = full.train_and_evaluate(None, rounds=4)
+    a = mk()
+    a.train_and_evaluate(None, rounds=2, save=str(tmp_path))
+    b = mk()
+    h_b = b.train_and_evaluate(None, rounds=4, resume=str(tmp_path))
+    assert [r["global"] for r in h_b] == [r["global"] for r in h_full]
+    for u, v in zip(full.global_weights, b.global_weights):
+        np.testing.assert_array_equal(u, v)
+
+
+def test_hpo_sweep_save_resume_reuses_trials(tmp_path):
+    from fedmi.data.tabular import load_tabular
+    from fedmi.hpo.sweep import load_sweep, run_sweep, save_sweep
+    ds = load_tabular(with_mean=False)
+    X, y = ds.X_train[:400], ds.y_train[:400]
+    best, res = run_sweep(X, y, None, [(5,)], [0.01, 0.02], max_iter=5, backend="numpy")
+    save_sweep(str(tmp_path), res, best, {"world": 1})
+    done = load_sweep(str(tmp_path))
+    calls = []
+    best2, res2 = run_sweep(X, y, None, [(5,), (6,)], [0.01, 0.02], max_iter=5, backend="numpy", done=done,
+                            on_trial=lambda r: calls.append(r.hidden))
+    assert calls == [(6,), (6,)]                 # only the new hidden config trained
+    assert [r.global_ for r in res2[:2]] == [r.global_ for r in res]
+    for u, v in zip(res2[0].weights, res[0].weights):
+        np.testing.assert_array_equal(u, v)
+    assert os.path.isfile(tmp_path / "best.safetensors")
+
+
+@pytest.mark.gpu
+def test_wide_client_checkpoint_exact(tmp_path):
+    from fedmi.data.synthetic import make_income_like
+    from fedmi.fl.wide import WideClient, load_wide, save_wide
+    dev = torch.device("cuda", 0)
+    Xn, yn = make_income_like(1024, seed=8)
+    X, y = torch.as_tensor(Xn, device=dev), torch.as_tensor(yn, device=dev)
+    mk = lambda: WideClient(X, y, [14, 256, 128, 2], micro_batch=512, dtype="bf16", seed=3)
+    a = mk()
+    for _ in range(2):
+        a.run_round()
+    save_wide(str(tmp_path), a)
+    b = mk()
+    assert load_wide(str(tmp_path), b) == 2
+    a.run_round()
+    b.run_round()
+    a.sync(); b.sync()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
