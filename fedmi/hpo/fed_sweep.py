@@ -10,7 +10,8 @@ with its own hidden sizes, learning rate and local steps per round, and a
 :class:`FedTrialGroup` runs K trials concurrently on every GPU:
 
 * each trial is a fused :class:`~fedmi.fl.engine.HipRoundEngine` on its own HIP stream, so
-  the small per-trial kernels of different trials overlap on the CUs;
+  the small per-trial kernels of different trials overlap on the CUs, and a whole group
+  round (all trials, fork/join, shared all-reduce) is one captured HIP graph;
 * all trials' FedAvg buffers are slices of ONE device allocation, so a round of all K
   trials costs one all-reduce (the per-trial weights, metric tails and early-stop inputs
   ride together), instead of K latency-bound collectives;
@@ -64,10 +65,17 @@ def grid(hidden: Sequence[Sequence[int]] = DEFAULT_HIDDEN, lrs: Sequence[float] 
 
 
 class FedTrialGroup:
-    """K federated trials on this client's shard, advanced in lock-step rounds."""
+    """K federated trials on this client's shard, advanced in lock-step rounds.
+
+    HIP: a round of the whole group -- every trial's kernels forked onto its own stream, joined,
+    then (several clients) one all-reduce over all trials' FedAvg buffers -- is captured ONCE
+    into a HIP graph of ``group_graph_rounds`` rounds and replayed, so a group round costs one
+    graph launch for all K trials instead of K x (2-3) kernel launches + stream fork/join from
+    Python.  One client: the trials are ordinary fused engines (evaluation inside the next
+    round's train kernel, no all-reduce); several: classic rounds sharing one collective."""
 
     def __init__(self, X, y, n_classes: int, trials: Sequence[FedTrial], comm, base: EngineConfig,
-                 n_total: Optional[int] = None, backend: str = "auto", seed: int = 0):
+                 n_total: Optional[int] = None, backend: str = "auto", seed: int = 0, group_graph_rounds: int = 16):
         self.trials = list(trials)
         self.comm = comm
         self.world = comm.size if comm is not None else 1
@@ -78,18 +86,26 @@ class FedTrialGroup:
         F = int(X.shape[1])
         self.engines = []
         self.buffers = None
+        self.graph = None
+        self.graph_rounds = int(group_graph_rounds)
         cfgs = [replace(base, hidden=t.hidden, lr=t.lr, local_steps=t.local_steps) for t in self.trials]
         flats = [init_flat([F, *t.hidden, n_classes], seed * 1000003 + rank) for t in self.trials]
         if backend == "hip":
             dev = comm.device if comm is not None else torch.device("cuda", torch.cuda.current_device())
-            lens = [comm_len([F, *t.hidden, n_classes], self.world) for t in self.trials]
-            offs = np.concatenate([[0], np.cumsum([(n + 63) & ~63 for n in lens])]).astype(np.int64)
-            self.buffers = [torch.zeros(int(offs[-1]), dtype=torch.float32, device=dev) for _ in range(2)]
-            for i, (cfg, flat) in enumerate(zip(cfgs, flats)):
-                views = (self.buffers[0][offs[i]:offs[i] + lens[i]], self.buffers[1][offs[i]:offs[i] + lens[i]])
-                self.engines.append(HipRoundEngine(X, y, n_classes, cfg, comm, flat, n_total=n_total, device=dev,
-                                                   comm_buffers=views))
+            if self.world == 1:
+                # no collective: every trial is a plain fused engine
+                for cfg, flat in zip(cfgs, flats):
+                    self.engines.append(HipRoundEngine(X, y, n_classes, cfg, None, flat, device=dev))
+            else:
+                lens = [comm_len([F, *t.hidden, n_classes], self.world) for t in self.trials]
+                offs = np.concatenate([[0], np.cumsum([(n + 63) & ~63 for n in lens])]).astype(np.int64)
+                self.buffers = [torch.zeros(int(offs[-1]), dtype=torch.float32, device=dev) for _ in range(2)]
+                for i, (cfg, flat) in enumerate(zip(cfgs, flats)):
+                    views = (self.buffers[0][offs[i]:offs[i] + lens[i]], self.buffers[1][offs[i]:offs[i] + lens[i]])
+                    self.engines.append(HipRoundEngine(X, y, n_classes, cfg, comm, flat, n_total=n_total, device=dev,
+                                                       comm_buffers=views))
             self.stream = torch.cuda.Stream(device=dev)
+            self.stream.wait_stream(torch.cuda.current_stream(dev))
             self._native = comm.native if (comm is not None and self.world > 1) else None
         elif backend == "torch":
             for cfg, flat in zip(cfgs, flats):
@@ -98,12 +114,15 @@ class FedTrialGroup:
             raise ValueError(f"unknown backend {backend!r}")
         self.rounds_issued = 0
 
-    def _round_hip(self, r: int) -> None:
-        # fork: every trial's train/adam/eval on its own stream
+    # ---- HIP rounds ----
+    def _issue_group_round(self, r: int) -> None:
+        """Round r of every trial on the group stream (fork/join), plus the shared all-reduce."""
         for e in self.engines:
             e.stream.wait_stream(self.stream)
-            e.engine.run_local(r, e._stream())
-        # join + one all-reduce over all trials' buffers
+            if self.world == 1:
+                e.engine.run(r, 1, e._stream(), None, close=False)   # fused evaluation round
+            else:
+                e.engine.run_local(r, e._stream())                   # classic round, no collective
         for e in self.engines:
             self.stream.wait_stream(e.stream)
         if self.world > 1:
@@ -113,19 +132,45 @@ class FedTrialGroup:
                     self._native.allreduce_f32(buf.data_ptr(), buf.numel(), self.stream.cuda_stream)
                 else:
                     self.comm.allreduce_(buf)
+
+    def _capturable(self) -> bool:
+        return self.graph_rounds >= 2 and (self.world == 1 or self._native is not None)
+
+    def _steady(self) -> bool:
+        return not any(e.engine.needs_eager_round() for e in self.engines)
+
+    def _capture(self) -> None:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self.stream):
+            for r in range(self.graph_rounds):   # parities 0, 1, ...: replayed from even rounds
+                self._issue_group_round(r)
+        self.graph = g
+
+    def _run_hip(self, n_rounds: int) -> None:
+        r, end = self.rounds_issued, self.rounds_issued + n_rounds
+        G = self.graph_rounds
+        while r < end:
+            if self._capturable() and r % 2 == 0 and end - r >= G and self._steady():
+                if self.graph is None:
+                    self._capture()
+                with torch.cuda.stream(self.stream):
+                    self.graph.replay()
+                r += G
+            else:
+                self._issue_group_round(r)
+                r += 1
+            for e in self.engines:
+                e.rounds_issued = r
+        self.stream.synchronize()
         for e in self.engines:
-            e.rounds_issued = r + 1
+            e.stream.wait_stream(self.stream)
+            e.sync_history()
 
     def run(self, n_rounds: int) -> None:
         """Run ``n_rounds`` rounds of every trial (trials that stopped early idle)."""
         n_rounds = min(n_rounds, min(e.cfg.max_rounds for e in self.engines) - self.rounds_issued)
         if self.backend == "hip":
-            for r in range(self.rounds_issued, self.rounds_issued + n_rounds):
-                self._round_hip(r)
-            self.stream.synchronize()
-            for e in self.engines:
-                e.stream.wait_stream(self.stream)
-                e.sync_history()
+            self._run_hip(n_rounds)
         else:
             for e in self.engines:
                 e.run(n_rounds)
@@ -140,14 +185,15 @@ class FedTrialGroup:
 
 def run_fed_sweep(X_local, y_local, n_classes: int, comm, trials: Sequence[FedTrial], rounds: int = 50,
                   trials_per_gpu: int = 6, base: Optional[EngineConfig] = None, n_total: Optional[int] = None,
-                  backend: str = "auto", seed: int = 0, on_group=None) -> Tuple[FedTrial, List[FedTrial]]:
+                  backend: str = "auto", seed: int = 0, on_group=None,
+                  group_graph_rounds: int = 16) -> Tuple[FedTrial, List[FedTrial]]:
     """Run ``trials`` in groups of ``trials_per_gpu`` concurrent trials; returns (best, all)."""
     base = base or EngineConfig()
     base = replace(base, max_rounds=max(base.max_rounds, rounds))
     done: List[FedTrial] = []
     for g0 in range(0, len(trials), trials_per_gpu):
         group = FedTrialGroup(X_local, y_local, n_classes, trials[g0:g0 + trials_per_gpu], comm, base,
-                              n_total=n_total, backend=backend, seed=seed)
+                              n_total=n_total, backend=backend, seed=seed, group_graph_rounds=group_graph_rounds)
         group.run(rounds)
         done.extend(group.trials)
         if on_group is not None:

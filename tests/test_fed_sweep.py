@@ -2,6 +2,7 @@
 import os
 import subprocess
 import sys
+from dataclasses import replace
 
 import numpy as np
 import pytest
@@ -83,3 +84,27 @@ def test_reference_h_client_api_runs_grid_and_returns_best():
     assert [w.shape for w in weights] == [w.shape for w in best.weights]
     # single client: the uniform FedAvg is the identity and the confusion matrix is local
     assert c._compute_metrics(y[:10], y[:10])["accuracy"] == 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_group_graph_equals_standalone_engines(dtype):
+    """One client: the packed group (K trials' rounds captured into one graph, fused
+    evaluation) gives every trial bit-identical weights and history to its own engine run
+    alone; early stopping inside the group is per trial."""
+    X, y = make_income_like(1500, seed=6)
+    trials = grid([(16,), (24, 8)], [0.004, 0.02], [1, 2])
+    base = EngineConfig(max_rounds=60, patience=3, tolerance=3e-3, dtype=dtype, graph_rounds=8)
+    from fedmi.hpo.fed_sweep import FedTrialGroup
+    g = FedTrialGroup(X, y, 2, trials, None, base, group_graph_rounds=8)
+    g.run(3)     # eager rounds first, then graph replays from an odd start
+    g.run(41)
+    assert g.graph is not None
+    for t, e in zip(g.trials, g.engines):
+        cfg = replace(base, hidden=t.hidden, lr=t.lr, local_steps=t.local_steps)
+        ref = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *t.hidden, 2], 0))
+        ref.run(44)
+        np.testing.assert_array_equal(ref.global_flat(), e.global_flat())
+        h = ref.history()
+        assert h["rounds_run"] == t.rounds_run and h["stop_round"] == t.history["stop_round"]
+        np.testing.assert_array_equal(h["global"], t.history["global"])
