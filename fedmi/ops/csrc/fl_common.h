@@ -76,6 +76,8 @@ struct MLPDescB {
     int alo_off[FL_MAX_LAYERS + 1];   // act_l lo parts bf16 [R][lda[l]] (l < L; forward pass only)
     int dlt_off[FL_MAX_LAYERS + 1];   // D_l  bf16 [R][lda[l]]    (1 <= l <= L): dLoss/dz_l
     int logit_off;                    // fp32 [R][16] classifier logits
+    int head_split;                   // logits layer: K split over this many waves (1 = one wave)
+    int part_off;                     // ... their fp32 partial logits [head_split][R][C]
     int cm_off;                       // int [16][16] confusion counters (fused evaluation)
     int item_base[FL_MAX_LAYERS + 1]; // packing: prefix sums of the 8-element items of each W_l
     int param_off;                    // start of the parameter region (all W_l hi, all b_l, all W_l lo):

@@ -558,6 +558,23 @@ class FLEngine {
             ev_.bias_off[l] = e_.bias_off[l] - e_.param_off + ev_.param_off;
         }
         ev_.lds_bytes = ev_.param_off + e_.param_bytes;
+        // Logits layer (one 16-column tile): its K loop is split over up to FL_WAVES waves
+        // (fixed-order sum of the partial logits) instead of one wave's chain of kp/32 steps,
+        // as far as LDS room allows; the same split in both layouts, so training, fused and
+        // classic evaluation see bit-identical logits.
+        const int C = d_.dim[L];
+        const int part1 = R * C * 4;
+        const int ksteps = e_.kp[L - 1] >> 5;
+        const int room = (int)FL_LDS_DYNAMIC_MAX - std::max(e_.lds_bytes, ev_.lds_bytes) - 16;
+        int G = std::min({ksteps, 16, std::max(1, room / part1)});
+        if (G < 2) G = 1;
+        e_.head_split = ev_.head_split = G;
+        if (G > 1) {
+            e_.part_off = e_.lds_bytes;
+            e_.lds_bytes += (G * part1 + 15) & ~15;
+            ev_.part_off = ev_.lds_bytes;
+            ev_.lds_bytes += (G * part1 + 15) & ~15;
+        }
     }
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
                       int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr, int fold_mask = FL_FOLD_B) {

@@ -358,11 +358,70 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
     }
 }
 
+// Logits layer with its K loop split over e.head_split waves: wave w < G computes the split-bf16
+// product over k-steps [w*kper, (w+1)*kper) of the single 16-column tile and drops its C useful
+// columns into part[w][row][c]; after a barrier, thread (row, c) sums the G partials in order
+// and adds the bias.  (One wave's chain of kp/32 dependent steps was the longest forward phase.)
+template <int RT>
+__device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPDescB& e, char* lds) {
+    const int l = d.L - 1, C = d.dim[d.L], G = e.head_split;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lr = lane & 15, lg = lane >> 4;
+    const int ksteps = e.kp[l] >> 5, kper = (ksteps + G - 1) / G;
+    const int lda = e.lda[l];
+    float* part = reinterpret_cast<float*>(lds + e.part_off);
+    if (wave < G) {
+        const char* wrow = lds + e.w_off[l] + (lr * lda + 8 * lg) * 2;
+        const char* act = lds + e.act_off[l];
+        const char* alo = lds + e.alo_off[l];
+        const int aoff = (lr * lda + 8 * lg) * 2;
+        f32x4 acc[RT], acl[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            acl[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+        const int k0 = wave * kper, k1 = min(ksteps, k0 + kper);
+        for (int ks = k0; ks < k1; ++ks) {
+            const bf16x8 bv = ld128(wrow + ks * 64);
+            const bf16x8 bl = ld128(wrow + e.wlo_delta + ks * 64);
+            bf16x8 av[RT], al[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                av[rt] = ld128(act + aoff + rt * 16 * lda * 2 + ks * 64);
+                al[rt] = ld128(alo + aoff + rt * 16 * lda * 2 + ks * 64);
+            }
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                acc[rt] = mfma32(av[rt], bv, acc[rt]);
+                acl[rt] = mfma32(al[rt], bv, acl[rt]);
+                acl[rt] = mfma32(av[rt], bl, acl[rt]);
+            }
+        }
+        if (lr < C) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) part[(wave * RT * 16 + rt * 16 + 4 * lg + j) * C + lr] = acc[rt][j] + acl[rt][j];
+        }
+    }
+    lds_barrier();
+    const float* bias = reinterpret_cast<const float*>(lds + e.bias_off[l]);
+    float* z = reinterpret_cast<float*>(lds + e.logit_off);
+    for (int i = threadIdx.x; i < RT * 16 * C; i += FL_THREADS) {
+        const int row = i / C, c = i - row * C;
+        float s = part[row * C + c];
+        for (int w = 1; w < G; ++w) s += part[(w * RT * 16 + row) * C + c];
+        z[row * 16 + c] = s + bias[c];
+    }
+}
+
 template <int RT>
 __device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg) {
     for (int l = 0; l < d.L; ++l) {
         if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
-        fwd_layer_bf16<RT>(d, e, l, lds);
+        if (l + 1 == d.L && e.head_split > 1) fwd_head_split_bf16<RT>(d, e, lds);
+        else fwd_layer_bf16<RT>(d, e, l, lds);
         lds_barrier();
     }
 }
