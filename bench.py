@@ -143,7 +143,9 @@ def main(argv=None):
                     help="c: the reference [C] workload (default, the headline metric) | wide: BASELINE config 3, "
                          "MLP 14-4096-4096-4096-2 on --wide-rows synthetic rows per client, bf16 NT GEMMs, "
                          "per-layer FedAvg buckets over RCCL")
-    ap.add_argument("--wide-rows", type=int, default=131072)
+    ap.add_argument("--wide-rows", type=int, default=131072,
+                    help="rows per client (BASELINE config 3 names 1e8-row shards: 12500000 per client at k = 8)")
+    ap.add_argument("--micro-batch", type=int, default=131072, help="--config wide: rows per micro-batch")
     a = ap.parse_args(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _self_launch(a, argv)
@@ -259,21 +261,24 @@ def main_wide(a) -> None:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
     dims = [14, 4096, 4096, 4096, 2]
     X, y = synth_shard(a.wide_rows, comm.rank, comm.device)
-    c = WideClient(X, y, dims, comm=comm if N > 1 else None, n_total=a.wide_rows * N, dtype="bf16", seed=0)
+    c = WideClient(X, y, dims, comm=comm if N > 1 else None, n_total=a.wide_rows * N, dtype="bf16", seed=0,
+                   micro_batch=a.micro_batch)
 
     def barrier():
         if N > 1:
             dist.barrier()
 
+    # every round as the reference runs it: local step, local evaluation of the post-step model
+    # on the whole shard (device-side confusion counts), FedAvg
     for _ in range(a.warmup):
-        c.run_round()
+        c.run_round(evaluate=True)
     c.sync()
     torch.cuda.synchronize(comm.device)
     barrier()
     torch.cuda.synchronize(comm.device)
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        c.run_round()
+        c.run_round(evaluate=True)
     c.sync()
     torch.cuda.synchronize(comm.device)
     barrier()
@@ -286,13 +291,16 @@ def main_wide(a) -> None:
     if comm.rank == 0:
         print(json.dumps({
             "metric": "train samples/s, wide-MLP FedAvg (BASELINE config 3)", "value": value,
-            "unit": "train samples/s (sum over clients; step = 1 federated round: full-batch Adam step + FedAvg)",
+            "unit": "train samples/s (sum over clients; step = 1 federated round: full-batch Adam step + local "
+                    "evaluation of the shard + FedAvg)",
             "n_gpus": N, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": f"synthetic income-shaped (device Philox), {a.wide_rows} rows/client; random-init weights",
             "config": {"model": "MLP " + "-".join(map(str, dims)), "global_batch": a.wide_rows * N, "seq_len": 1,
                        "parallelism": f"fedavg{N} (1 client/GPU, per-layer RCCL buckets)"},
             "tflops_per_client": c.flops_per_round / (dt / a.steps) / 1e12,
+            "local_train_acc_synthetic": c.metrics()["accuracy"],
+            "micro_batch": c.mb,
         }), flush=True)
     comm.close()
 

@@ -87,6 +87,8 @@ class WideClient:
                         if self._skinny else None)
         self.dz_out = torch.empty(mb, dims[-1], **f32)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.cm = torch.zeros(dims[-1] * dims[-1], dtype=torch.float32, device=dev)  # local confusion counts
+        self.evaluated = False
         self.round = 0
         self.stream = torch.cuda.Stream(device=dev)
         self.comm_stream = torch.cuda.Stream(device=dev)
@@ -338,21 +340,39 @@ class WideClient:
         for l in range(self.L):
             self._wait_bucket(l)
 
-    def evaluate(self) -> float:
-        rows = min(self.eval_rows or self.mb, self.n, self.mb)
+    def evaluate_shard(self) -> None:
+        """Local evaluation of the post-step local model on the WHOLE shard (C:148, C:75-91):
+        micro-batched forward passes, argmax + confusion counts on the device into
+        ``self.cm`` (no host synchronisation; :meth:`metrics` reads them)."""
+        C = self.dims[-1]
         with torch.cuda.stream(self.stream):
-            self._forward(0, rows, keep_t=False)
-            pred = self.logits[:rows].argmax(dim=1)
-            acc = (pred == self.y[:rows].long()).float().mean()
-        self.stream.synchronize()
-        return float(acc)
+            self.cm.zero_()
+            for r0 in range(0, self.n, self.mb):
+                rows = min(self.mb, self.n - r0)
+                self._forward(r0, rows, keep_t=False)
+                self.m.logits_confusion(self.logits.data_ptr(), self.logits.stride(0), self.y[r0:].data_ptr(), rows,
+                                        C, self.cm.data_ptr(), self._s())
+        self.evaluated = True
 
-    def run_round(self, evaluate: bool = False) -> Optional[float]:
+    def metrics(self) -> dict:
+        """Accuracy / weighted precision, recall, F1 of the last :meth:`evaluate_shard`."""
+        from .metrics import metrics_from_confusion
+        self.stream.synchronize()
+        C = self.dims[-1]
+        return metrics_from_confusion(self.cm.cpu().numpy().reshape(C, C).astype(np.int64))
+
+    def evaluate(self) -> float:
+        self.evaluate_shard()
+        return float(self.metrics()["accuracy"])
+
+    def run_round(self, evaluate: bool = True) -> None:
+        """One federated round as the reference runs it (C:145-198): local step, local evaluation
+        of the post-step model on the shard (device-side, no host sync), FedAvg buckets."""
         self.local_step()
-        acc = self.evaluate() if evaluate else None
+        if evaluate:
+            self.evaluate_shard()
         self.aggregate()
         self.round += 1
-        return acc
 
     def loss(self) -> float:
         self.sync()
@@ -361,8 +381,9 @@ class WideClient:
 
     @property
     def flops_per_round(self) -> float:
+        """Training (forward + backward, 6 n MACs) plus the local evaluation forward (2 n MACs)."""
         macs = sum(a * b for a, b in zip(self.dims[:-1], self.dims[1:]))
-        return 6.0 * self.n * macs
+        return (6.0 + (2.0 if self.evaluated else 0.0)) * self.n * macs
 
 
 def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int, micro_batch: int = 131072,
@@ -384,8 +405,10 @@ def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int
     losses, accs, times = [], [], []
     for r in range(rounds):
         t0 = time.perf_counter()
-        acc = c.run_round(evaluate=bool(eval_every) and (r + 1) % eval_every == 0)
+        ev = bool(eval_every) and (r + 1) % eval_every == 0
+        c.run_round(evaluate=ev)
         loss = c.loss()          # joins the round (and its FedAvg buckets)
+        acc = c.metrics()["accuracy"] if ev else None
         times.append(time.perf_counter() - t0)
         losses.append(loss)
         if acc is not None:

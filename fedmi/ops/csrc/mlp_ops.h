@@ -64,5 +64,6 @@ hipError_t xent_launch(const XentArgs& a, int T, hipStream_t s);
 hipError_t adam_launch(const AdamArgs& a, int T, hipStream_t s);
 hipError_t step_count_launch(long long* step, const int* active, int T, hipStream_t s);
 hipError_t epoch_end_launch(const EpochArgs& a, hipStream_t s);
+hipError_t logits_confusion_launch(const float* z, int ldz, const int* y, int M, int C, float* cm, hipStream_t s);
 hipError_t confusion_launch(const int* pred, const int* y, const int* idx, int M, int C, int T, float* cm,
                             hipStream_t s);

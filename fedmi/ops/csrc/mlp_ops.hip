@@ -9,6 +9,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "mlp_ops.h"
 
 // ---------------------------------------------------------------------------------------
@@ -178,7 +180,37 @@ __global__ void confusion_kernel(const int* __restrict__ pred, const int* __rest
     atomicAdd(&cm[(size_t)t * C * C + yy * C + pred[(size_t)t * M + i]], 1.f);
 }
 
+// Argmax of fp32 logits rows + confusion counts (local evaluation of the wide client, C:75-91):
+// cm[y][argmax] += 1 over M rows, counts accumulated per block in LDS then added to the float
+// counters (exact below 2^24 per cell per call).
+__global__ void __launch_bounds__(256)
+logits_confusion_kernel(const float* __restrict__ z, int ldz, const int* __restrict__ y, int M, int C,
+                        float* __restrict__ cm) {
+    __shared__ int cnt[16 * 16];
+    for (int i = threadIdx.x; i < C * C; i += blockDim.x) cnt[i] = 0;
+    __syncthreads();
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+        const float* zr = z + (size_t)i * ldz;
+        int best = 0;
+        float bv = zr[0];
+        for (int k = 1; k < C; ++k)
+            if (zr[k] > bv) { bv = zr[k]; best = k; }   // torch.max(dim=1): first maximum
+        atomicAdd(&cnt[y[i] * C + best], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * C; i += blockDim.x)
+        if (cnt[i]) atomicAdd(&cm[i], (float)cnt[i]);
+}
+
 // ---------------------------------------------------------------------------------------
+hipError_t logits_confusion_launch(const float* z, int ldz, const int* y, int M, int C, float* cm, hipStream_t s) {
+    if (C < 1 || C > 16 || M < 0) return hipErrorInvalidValue;
+    if (M == 0) return hipSuccess;
+    const int blocks = (int)std::min<long long>(1024, ((long long)M + 255) / 256);
+    hipLaunchKernelGGL(logits_confusion_kernel, dim3(blocks), dim3(256), 0, s, z, ldz, y, M, C, cm);
+    return hipGetLastError();
+}
+
 hipError_t gather_rows_launch(const GatherArgs& a, hipStream_t s) {
     const int n = a.M * a.ldo;
     hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a);

@@ -349,7 +349,13 @@ static void colsum_split_py(uintptr_t X, int M, int N, int splits, uintptr_t sla
                                  reinterpret_cast<float*>(out), beta, reinterpret_cast<hipStream_t>(stream)));
 }
 
+static void logits_confusion_py(uintptr_t z, int ldz, uintptr_t y, int M, int C, uintptr_t cm, uintptr_t stream) {
+    TR_CHECK(logits_confusion_launch(reinterpret_cast<const float*>(z), ldz, reinterpret_cast<const int*>(y), M, C,
+                                     reinterpret_cast<float*>(cm), reinterpret_cast<hipStream_t>(stream)));
+}
+
 void register_trainer(py::module_& m) {
+    m.def("logits_confusion", &logits_confusion_py);
     m.def("colsum_split", &colsum_split_py);
     m.def("skinny_wgrad", &skinny_wgrad_py);
     m.def("gemm_nt", &gemm_nt_py);

@@ -88,3 +88,27 @@ def test_wide_fedavg_buckets_match_simulation():
     ref = cl[0].params.cpu().numpy()
     err = np.max(np.abs(out[0][1] - ref)) / np.max(np.abs(ref))
     assert err < 1e-6, err
+
+
+def test_wide_local_evaluation_whole_shard():
+    """evaluate_shard: micro-batched forward + device argmax / confusion over EVERY row of the
+    shard (the reference's per-round local evaluation, C:148); vs an fp32 torch forward."""
+    import torch
+    from fedmi.fl.wide import WideClient
+    from fedmi.models.mlp import flat_to_dict
+    dev = torch.device("cuda", 0)
+    X, y = _data(0, dev)
+    c = WideClient(X, y, DIMS, micro_batch=512, dtype="bf16")
+    c.run_round(evaluate=True)
+    m = c.metrics()
+    cm = c.cm.cpu().numpy()
+    assert cm.sum() == ROWS[0]
+    # the evaluated model is the post-step local model (before aggregate: one client -> same)
+    d = flat_to_dict(c.params.cpu().numpy(), DIMS)
+    a = X.float()
+    for l in range(len(DIMS) - 1):
+        a = a @ torch.as_tensor(d[f"model.{2 * l}.weight"], device=dev).T + torch.as_tensor(d[f"model.{2 * l}.bias"], device=dev)
+        if l < len(DIMS) - 2:
+            a = torch.relu(a)
+    acc = float((a.argmax(1) == y.long()).float().mean())
+    assert abs(m["accuracy"] - acc) < 0.01, (m["accuracy"], acc)
