@@ -299,6 +299,7 @@ class WideClient:
 
     def local_step(self):
         """One full-batch Adam step over the whole shard (micro-batched accumulation)."""
+        self._local_quantized = False
         C = self.dims[-1]
         s = self._s()
         with torch.cuda.stream(self.stream):
@@ -322,7 +323,10 @@ class WideClient:
         comm stream: scale by n_i/N, all-reduce, re-quantise, record the bucket's event.  The
         compute stream does not wait here: its next use of layer l waits on event l."""
         if self.world == 1:
-            self._quantize()
+            # FedAvg of one client is the identity: its operand copies are the local model's
+            if not getattr(self, "_local_quantized", False):
+                self._quantize()
+            self._local_quantized = False
             return
         self.comm_stream.wait_stream(self.stream)  # the Adam step (and evaluation) are done
         for l, ((name, shape, off), (bn, bs, boff)) in enumerate(zip(self.layout[0::2], self.layout[1::2])):
@@ -345,6 +349,8 @@ class WideClient:
         micro-batched forward passes, argmax + confusion counts on the device into
         ``self.cm`` (no host synchronisation; :meth:`metrics` reads them)."""
         C = self.dims[-1]
+        self._quantize()   # the GEMM operand copies of the post-step local weights
+        self._local_quantized = True
         with torch.cuda.stream(self.stream):
             self.cm.zero_()
             for r0 in range(0, self.n, self.mb):
