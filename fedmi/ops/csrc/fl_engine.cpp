@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "fl_common.h"
+#include "fl_layout.h"
 #include "peer_allreduce.h"
 
 namespace py = pybind11;
@@ -110,10 +111,6 @@ class RcclComm {
 // ---------------------------------------------------------------------------------------
 // Engine
 // ---------------------------------------------------------------------------------------
-// Activation row stride: roundup16(dim) + 4 floats (16-byte aligned rows, 4 mod 8 so the
-// b128 / b32 MFMA operand patterns of fl_kernels.hip are bank-conflict free).
-static int pick_ld(int dim) { return ((dim + 15) & ~15) + 4; }
-
 class FLEngine {
   public:
     FLEngine(std::vector<int> dims, py::dict cfg, py::dict bufs) {
@@ -122,49 +119,13 @@ class FLEngine {
         std::memset(&d_, 0, sizeof(d_));
         std::memset(&c_, 0, sizeof(c_));
         std::memset(&b_, 0, sizeof(b_));
-        d_.L = L;
-        int off = 0;
-        for (int l = 0; l <= L; ++l) d_.dim[l] = dims[l];
-        for (int l = 0; l < L; ++l) {
-            d_.w_off[l] = off;
-            off += dims[l] * dims[l + 1];
-            d_.b_off[l] = off;
-            off += dims[l + 1];
-        }
-        d_.P = off;
+        c_.R = cfg["R"].cast<int>();
+        if (c_.R != 16 && c_.R != 32 && c_.R != 64) throw std::runtime_error("FLEngine: R must be 16, 32 or 64");
         const int C = dims[L];
         if (C > FL_MAX_CLASSES) throw std::runtime_error("FLEngine: at most 16 classes");
         if (dims[0] > 4096) throw std::runtime_error("FLEngine: too many features");
-
-        // parameter image (fl_common.h): per layer [wrows(N)][ldw(K)] then bias[roundup16(N)]
-        int io = 0;
-        for (int l = 0; l < L; ++l) {
-            d_.iw_off[l] = io;
-            io += fl_wrows(dims[l + 1]) * fl_ldw(dims[l]);
-            d_.ib_off[l] = io;
-            io += (dims[l + 1] + 15) & ~15;
-        }
-        d_.Pimg = (io + 3) & ~3;
-
-        c_.R = cfg["R"].cast<int>();
-        if (c_.R != 16 && c_.R != 32 && c_.R != 64) throw std::runtime_error("FLEngine: R must be 16, 32 or 64");
-        int lds = 0;
-        for (int l = 0; l <= L; ++l) {
-            d_.ld[l] = pick_ld(dims[l]);
-            d_.act_off[l] = lds;
-            lds += c_.R * d_.ld[l];
-            lds = (lds + 3) & ~3;
-        }
-        for (int l = 1; l < L; ++l) {  // backward deltas of the hidden layers
-            d_.dlt_off[l] = lds;
-            lds += c_.R * d_.ld[l];
-            lds = (lds + 3) & ~3;
-        }
-        d_.cm_off = lds;  // fused evaluation's confusion counters (FL_CM_INTS ints)
-        lds += FL_CM_INTS;
-        d_.img_lds = lds;
-        lds += d_.Pimg;
-        d_.lds_floats = lds;
+        fl_build_fp32_layout(dims.data(), L, c_.R, &d_);   // fl_layout.h (host-tested with sanitizers)
+        const int lds = d_.lds_floats;
         dtype_ = cfg.contains("dtype") ? cfg["dtype"].cast<int>() : 0;
         if (dtype_ == 0) {
             if (c_.R == 64) throw std::runtime_error("FLEngine: R = 64 needs the bf16 kernels");
@@ -172,7 +133,7 @@ class FLEngine {
                 throw std::runtime_error("FLEngine: activations exceed LDS; use a smaller R or the layered path");
             HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));
         } else {
-            build_bf16_layout();
+            fl_build_bf16_layout(d_, c_.R, &e_, &ev_);
             const size_t need = (size_t)std::max(e_.lds_bytes, ev_.lds_bytes);
             if (need > FL_LDS_DYNAMIC_MAX)
                 throw std::runtime_error("FLEngine(bf16): model exceeds LDS; use a smaller R or the layered path");
@@ -514,68 +475,6 @@ class FLEngine {
     }
 
   private:
-    // bf16 LDS layout (fl_common.h MLPDescB), byte offsets, 16-byte aligned pieces
-    void build_bf16_layout() {
-        std::memset(&e_, 0, sizeof(e_));
-        const int L = d_.L, R = c_.R;
-        for (int l = 0; l <= L; ++l) {
-            e_.kp[l] = (d_.dim[l] + 31) & ~31;
-            e_.lda[l] = e_.kp[l] + 8;
-        }
-        int off = 0;
-        auto take = [&](int bytes) { const int o = off; off += (bytes + 15) & ~15; return o; };
-        for (int l = 0; l < L; ++l) e_.act_off[l] = take(R * e_.lda[l] * 2);
-        for (int l = 1; l <= L; ++l) e_.dlt_off[l] = take(R * e_.lda[l] * 2);
-        e_.logit_off = take(R * 16 * 4);
-        e_.cm_off = take(FL_CM_INTS * 4);
-        // split-bf16 forward: lo parts of the layer inputs -- X in its own buffer, the hidden
-        // activations in the delta buffers (same [R][lda] shape, free until the backward pass)
-        e_.alo_off[0] = take(R * e_.lda[0] * 2);
-        for (int l = 1; l < L; ++l) e_.alo_off[l] = e_.dlt_off[l];
-        // parameter region: W hi images, biases, W lo images (each W size is a multiple of 16
-        // bytes, so the lo images sit at one constant offset from their hi images)
-        e_.param_off = off;
-        for (int l = 0; l < L; ++l) e_.w_off[l] = take(e_.kp[l + 1] * e_.lda[l] * 2);
-        for (int l = 0; l < L; ++l) e_.bias_off[l] = take(e_.kp[l + 1] * 4);
-        e_.wlo_delta = off - e_.w_off[0];
-        for (int l = 0; l < L; ++l) take(e_.kp[l + 1] * e_.lda[l] * 2);
-        e_.param_bytes = off - e_.param_off;
-        e_.lds_bytes = off;
-        e_.item_base[0] = 0;
-        for (int l = 0; l < L; ++l) e_.item_base[l + 1] = e_.item_base[l] + e_.kp[l + 1] * (e_.kp[l] >> 3);
-        // Evaluation kernels run the forward pass only: their layout has no delta buffers, so the
-        // lo parts of the hidden activations get buffers of their own.
-        ev_ = e_;
-        off = 0;
-        for (int l = 0; l < L; ++l) ev_.act_off[l] = take(R * e_.lda[l] * 2);
-        for (int l = 1; l <= L; ++l) ev_.dlt_off[l] = -1;
-        ev_.logit_off = take(R * 16 * 4);
-        ev_.cm_off = take(FL_CM_INTS * 4);
-        for (int l = 0; l < L; ++l) ev_.alo_off[l] = take(R * e_.lda[l] * 2);
-        ev_.param_off = off;
-        for (int l = 0; l < L; ++l) {
-            ev_.w_off[l] = e_.w_off[l] - e_.param_off + ev_.param_off;
-            ev_.bias_off[l] = e_.bias_off[l] - e_.param_off + ev_.param_off;
-        }
-        ev_.lds_bytes = ev_.param_off + e_.param_bytes;
-        // Logits layer (one 16-column tile): its K loop is split over up to FL_WAVES waves
-        // (fixed-order sum of the partial logits) instead of one wave's chain of kp/32 steps,
-        // as far as LDS room allows; the same split in both layouts, so training, fused and
-        // classic evaluation see bit-identical logits.
-        const int C = d_.dim[L];
-        const int part1 = R * C * 4;
-        const int ksteps = e_.kp[L - 1] >> 5;
-        const int room = (int)FL_LDS_DYNAMIC_MAX - std::max(e_.lds_bytes, ev_.lds_bytes) - 16;
-        int G = std::min({ksteps, 16, std::max(1, room / part1)});
-        if (G < 2) G = 1;
-        e_.head_split = ev_.head_split = G;
-        if (G > 1) {
-            e_.part_off = e_.lds_bytes;
-            e_.lds_bytes += (G * part1 + 15) & ~15;
-            ev_.part_off = ev_.lds_bytes;
-            ev_.lds_bytes += (G * part1 + 15) & ~15;
-        }
-    }
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
                       int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr, int fold_mask = FL_FOLD_B) {
         if (dtype_ == 0) {

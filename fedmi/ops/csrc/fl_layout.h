@@ -1,0 +1,123 @@
+// Host-side layout arithmetic of the fused round kernels: the fp32 parameter image and LDS
+// layout (MLPDesc) and the bf16 LDS layouts of the train / evaluation kernels (MLPDescB).
+// Header-only and free of HIP runtime calls, so the same code the engine uses is compiled into
+// a host test binary with AddressSanitizer + UBSan (tests/native/test_layout.cpp) that sweeps
+// model shapes and checks every region the kernels index for bounds, overlap and alignment.
+#pragma once
+#include <algorithm>
+#include <cstring>
+
+#include "fl_common.h"
+
+// Activation row stride: roundup16(dim) + 4 floats (16-byte aligned rows, 4 mod 8 so the
+// b128 / b32 MFMA operand patterns of fl_kernels.hip are bank-conflict free).
+inline int fl_pick_ld(int dim) { return ((dim + 15) & ~15) + 4; }
+
+// dims[0..L]: features, hidden sizes, classes.  Fills the dense / image offsets and the fp32
+// kernels' LDS layout (floats) for R rows per workgroup.
+inline void fl_build_fp32_layout(const int* dims, int L, int R, MLPDesc* d) {
+    std::memset(d, 0, sizeof(*d));
+    d->L = L;
+    int off = 0;
+    for (int l = 0; l <= L; ++l) d->dim[l] = dims[l];
+    for (int l = 0; l < L; ++l) {
+        d->w_off[l] = off;
+        off += dims[l] * dims[l + 1];
+        d->b_off[l] = off;
+        off += dims[l + 1];
+    }
+    d->P = off;
+    // parameter image (fl_common.h): per layer [wrows(N)][ldw(K)] then bias[roundup16(N)]
+    int io = 0;
+    for (int l = 0; l < L; ++l) {
+        d->iw_off[l] = io;
+        io += fl_wrows(dims[l + 1]) * fl_ldw(dims[l]);
+        d->ib_off[l] = io;
+        io += (dims[l + 1] + 15) & ~15;
+    }
+    d->Pimg = (io + 3) & ~3;
+    int lds = 0;
+    for (int l = 0; l <= L; ++l) {
+        d->ld[l] = fl_pick_ld(dims[l]);
+        d->act_off[l] = lds;
+        lds += R * d->ld[l];
+        lds = (lds + 3) & ~3;
+    }
+    for (int l = 1; l < L; ++l) {  // backward deltas of the hidden layers
+        d->dlt_off[l] = lds;
+        lds += R * d->ld[l];
+        lds = (lds + 3) & ~3;
+    }
+    d->cm_off = lds;  // fused evaluation's confusion counters (FL_CM_INTS ints)
+    lds += FL_CM_INTS;
+    d->img_lds = lds;
+    lds += d->Pimg;
+    d->lds_floats = lds;
+}
+
+// bf16 LDS layouts (fl_common.h MLPDescB), byte offsets, 16-byte aligned pieces: `e` for the
+// train kernel, `ev` for the evaluation kernels (forward pass only).
+inline void fl_build_bf16_layout(const MLPDesc& d, int R, MLPDescB* e_out, MLPDescB* ev_out) {
+    MLPDescB e, ev;
+    std::memset(&e, 0, sizeof(e));
+    const int L = d.L;
+    for (int l = 0; l <= L; ++l) {
+        e.kp[l] = (d.dim[l] + 31) & ~31;
+        e.lda[l] = e.kp[l] + 8;
+    }
+    int off = 0;
+    auto take = [&](int bytes) { const int o = off; off += (bytes + 15) & ~15; return o; };
+    for (int l = 0; l < L; ++l) e.act_off[l] = take(R * e.lda[l] * 2);
+    for (int l = 1; l <= L; ++l) e.dlt_off[l] = take(R * e.lda[l] * 2);
+    e.logit_off = take(R * 16 * 4);
+    e.cm_off = take(FL_CM_INTS * 4);
+    // split-bf16 forward: lo parts of the layer inputs -- X in its own buffer, the hidden
+    // activations in the delta buffers (same [R][lda] shape, free until the backward pass)
+    e.alo_off[0] = take(R * e.lda[0] * 2);
+    for (int l = 1; l < L; ++l) e.alo_off[l] = e.dlt_off[l];
+    // parameter region: W hi images, biases, W lo images (each W size is a multiple of 16
+    // bytes, so the lo images sit at one constant offset from their hi images)
+    e.param_off = off;
+    for (int l = 0; l < L; ++l) e.w_off[l] = take(e.kp[l + 1] * e.lda[l] * 2);
+    for (int l = 0; l < L; ++l) e.bias_off[l] = take(e.kp[l + 1] * 4);
+    e.wlo_delta = off - e.w_off[0];
+    for (int l = 0; l < L; ++l) take(e.kp[l + 1] * e.lda[l] * 2);
+    e.param_bytes = off - e.param_off;
+    e.lds_bytes = off;
+    e.item_base[0] = 0;
+    for (int l = 0; l < L; ++l) e.item_base[l + 1] = e.item_base[l] + e.kp[l + 1] * (e.kp[l] >> 3);
+    // Evaluation kernels run the forward pass only: their layout has no delta buffers, so the
+    // lo parts of the hidden activations get buffers of their own.
+    ev = e;
+    off = 0;
+    for (int l = 0; l < L; ++l) ev.act_off[l] = take(R * e.lda[l] * 2);
+    for (int l = 1; l <= L; ++l) ev.dlt_off[l] = -1;
+    ev.logit_off = take(R * 16 * 4);
+    ev.cm_off = take(FL_CM_INTS * 4);
+    for (int l = 0; l < L; ++l) ev.alo_off[l] = take(R * e.lda[l] * 2);
+    ev.param_off = off;
+    for (int l = 0; l < L; ++l) {
+        ev.w_off[l] = e.w_off[l] - e.param_off + ev.param_off;
+        ev.bias_off[l] = e.bias_off[l] - e.param_off + ev.param_off;
+    }
+    ev.lds_bytes = ev.param_off + e.param_bytes;
+    // Logits layer (one 16-column tile): its K loop is split over up to 16 waves (fixed-order
+    // sum of the partial logits) instead of one wave's chain of kp/32 steps, as far as LDS room
+    // allows; the same split in both layouts, so training, fused and classic evaluation see
+    // bit-identical logits.
+    const int C = d.dim[L];
+    const int part1 = R * C * 4;
+    const int ksteps = e.kp[L - 1] >> 5;
+    const int room = (int)FL_LDS_DYNAMIC_MAX - std::max(e.lds_bytes, ev.lds_bytes) - 16;
+    int G = std::min(std::min(ksteps, 16), std::max(1, room / part1));
+    if (G < 2) G = 1;
+    e.head_split = ev.head_split = G;
+    if (G > 1) {
+        e.part_off = e.lds_bytes;
+        e.lds_bytes += (G * part1 + 15) & ~15;
+        ev.part_off = ev.lds_bytes;
+        ev.lds_bytes += (G * part1 + 15) & ~15;
+    }
+    *e_out = e;
+    *ev_out = ev;
+}
