@@ -36,7 +36,7 @@ class FederatedMLPLearning:
     """Reference [S] client API (S:10-66) over fedmi components."""
 
     def __init__(self, X, y, rank, size, comm=None, hidden=(50, 400), lr=0.004, max_iter=300, warm_start=False,
-                 backend="auto"):
+                 backend="auto", dtype="float64"):
         self.rank = rank
         self.size = size
         self.comm = comm
@@ -44,7 +44,7 @@ class FederatedMLPLearning:
         self.local_model = None
         self.global_weights = None
         self.hidden, self.lr, self.max_iter = hidden, lr, max_iter
-        self.warm_start, self.backend = warm_start, backend
+        self.warm_start, self.backend, self.dtype = warm_start, backend, dtype
 
     def _split_data(self, X, y, rank, size):
         return split_data(X, y, rank, size, mode="contiguous")
@@ -67,7 +67,7 @@ class FederatedMLPLearning:
         from fedmi.ckpt.checkpoint import load_sklearn_run, save_sklearn_run
         self.local_model = MLPClassifier(activation="relu", hidden_layer_sizes=self.hidden,
                                          learning_rate_init=self.lr, max_iter=self.max_iter, random_state=42,
-                                         warm_start=self.warm_start, backend=self.backend)
+                                         warm_start=self.warm_start, backend=self.backend, dtype=self.dtype)
         classes = np.unique(self.y_local)
         self.local_model.partial_fit(self.X_local, self.y_local, classes=classes)
         history = []
@@ -130,6 +130,8 @@ def main(argv=None):
     ap.add_argument("--warm-start", action="store_true", help="keep the averaged weights across rounds (fixes Q8)")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--backend", default="auto", help="estimator backend: hip | numpy")
+    ap.add_argument("--dtype", default="float64", choices=["float64", "float32"],
+                    help="HIP backend precision (float64 = sklearn's numerics, f64 MFMA)")
     ap.add_argument("--save", default=None, help="checkpoint directory (coefs_ + intercepts_ layout), every round")
     ap.add_argument("--resume", default=None, help="continue a run saved with --save")
     a = ap.parse_args(argv)
@@ -139,7 +141,8 @@ def main(argv=None):
     if backend == "auto":
         backend = "hip" if comm.device.type == "cuda" else "numpy"
     tr = FederatedMLPLearning(ds.X_train, ds.y_train, comm.rank, comm.size, comm=comm, hidden=tuple(a.hidden),
-                              lr=a.lr, max_iter=a.max_iter, warm_start=a.warm_start, backend=backend)
+                              lr=a.lr, max_iter=a.max_iter, warm_start=a.warm_start, backend=backend,
+                              dtype=a.dtype)
     hist = tr.train_and_evaluate(comm, rounds=a.rounds, save=a.save, resume=a.resume)
     comm.close()
     return hist

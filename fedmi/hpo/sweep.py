@@ -40,14 +40,16 @@ class TrialResult:
 
 def run_sweep(X_local, y_local, comm, hidden_grid: Sequence = HIDDEN_GRID, lr_grid: Sequence = LR_GRID,
               max_iter: int = 400, random_state: int = 42, backend: str = "auto", packed: bool = True,
-              on_trial=None, done: Sequence[TrialResult] = ()) -> Tuple[Optional[TrialResult], List[TrialResult]]:
+              on_trial=None, done: Sequence[TrialResult] = (),
+              dtype: str = "float64") -> Tuple[Optional[TrialResult], List[TrialResult]]:
     """``done``: results of an earlier (checkpointed) sweep; their hidden configs are not trained
     again and the best trial is taken over old and new results in grid order."""
     classes = np.unique(y_local)
     n_cls = max(2, len(classes))
     have = {(tuple(r.hidden), float(r.lr)): r for r in done}
     todo = [hl for hl in hidden_grid if any((tuple(hl), float(lr)) not in have for lr in lr_grid)]
-    fresh = _train(X_local, y_local, comm, todo, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial)
+    fresh = _train(X_local, y_local, comm, todo, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial,
+                   dtype)
     results = [have.get((tuple(hl), float(lr))) or fresh[(tuple(hl), float(lr))] for hl in hidden_grid
                for lr in lr_grid]
     best: Optional[TrialResult] = None
@@ -57,10 +59,12 @@ def run_sweep(X_local, y_local, comm, hidden_grid: Sequence = HIDDEN_GRID, lr_gr
     return best, results
 
 
-def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial):
+def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial,
+           dtype="float64"):
     out = {}
     groups = [[MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=max_iter,
-                             random_state=random_state, backend=backend) for lr in lr_grid] for hl in hidden_grid]
+                             random_state=random_state, backend=backend, dtype=dtype) for lr in lr_grid]
+              for hl in hidden_grid]
     # Training needs no communication (every trial fits from scratch, Q8): on the GPU the
     # packed jobs of all hidden configs run concurrently, one host thread + stream each (the
     # native epoch loop releases the GIL; each job's kernels are far too small to fill the

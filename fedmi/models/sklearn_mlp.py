@@ -16,9 +16,11 @@ This estimator keeps that API -- ``fit``, ``partial_fit``, ``predict``, ``predic
 * minibatches of ``min(200, n)`` rows, reshuffled every epoch from the same RandomState;
 * stop after ``n_iter_no_change`` epochs without a ``tol`` improvement of the training loss.
 
-Backends: ``"hip"`` trains in fp32 on the device with the native packed-trial trainer
-(``MLPTrainer`` in ``fedmi/ops/csrc/mlp_trainer.cpp``: fused-epilogue MFMA GEMMs, device-side
-loss / Adam / stop rule, one HIP-graph launch per epoch); ``"numpy"`` is a float64 host
+Backends: ``"hip"`` trains on the device with the native packed-trial trainer
+(``MLPTrainer`` / ``MLPTrainer64`` in ``fedmi/ops/csrc/mlp_trainer.cpp``: fused-epilogue MFMA
+GEMMs, device-side loss / Adam / stop rule, one HIP-graph launch per epoch) in
+``dtype="float64"`` (the default, sklearn's own precision: ``v_mfma_f64_16x16x4_f64`` GEMMs of
+``mlp_f64.hip``) or ``dtype="float32"`` (exact-fp32 MFMA); ``"numpy"`` is a float64 host
 implementation of the same algorithm (the CPU path and the parity oracle -- it tracks
 sklearn to ~1e-12).  ``warm_start=True`` fixes the reference's limitation: a ``fit`` after
 ``_set_weights`` continues from the averaged weights.
@@ -72,7 +74,7 @@ class MLPClassifier:
     def __init__(self, hidden_layer_sizes=(100,), activation="relu", solver="adam", alpha=1e-4,
                  batch_size="auto", learning_rate_init=1e-3, max_iter=200, shuffle=True, random_state=None,
                  tol=1e-4, verbose=False, warm_start=False, beta_1=0.9, beta_2=0.999, epsilon=1e-8,
-                 n_iter_no_change=10, backend="auto", device=None):
+                 n_iter_no_change=10, backend="auto", device=None, dtype="float64"):
         if activation != "relu" or solver != "adam":
             raise NotImplementedError("fedmi MLPClassifier supports activation='relu', solver='adam'")
         self.hidden_layer_sizes = hidden_layer_sizes
@@ -93,6 +95,10 @@ class MLPClassifier:
         self.n_iter_no_change = n_iter_no_change
         self.backend = backend
         self.device = device
+        dtype = {"fp64": "float64", "fp32": "float32"}.get(dtype, dtype)
+        if dtype not in ("float64", "float32"):
+            raise ValueError("dtype must be 'float64' (fp64) or 'float32' (fp32)")
+        self.dtype = dtype
 
     # ------------------------------------------------------------------ helpers
     def _resolve_backend(self) -> str:
@@ -197,7 +203,7 @@ class MLPClassifier:
     def get_params(self, deep=True):
         keys = ["hidden_layer_sizes", "activation", "solver", "alpha", "batch_size", "learning_rate_init",
                 "max_iter", "shuffle", "random_state", "tol", "verbose", "warm_start", "beta_1", "beta_2",
-                "epsilon", "n_iter_no_change", "backend", "device"]
+                "epsilon", "n_iter_no_change", "backend", "device", "dtype"]
         return {k: getattr(self, k) for k in keys}
 
 
@@ -271,12 +277,12 @@ def _fit_numpy(est: MLPClassifier, X, codes, perms, incremental):
             break
 
 
-# ---------------------------------------------------------------------- HIP (fp32, packed)
-def _pack(coefs, inters) -> np.ndarray:
+# ---------------------------------------------------------------------- HIP (packed)
+def _pack(coefs, inters, dtype=np.float32) -> np.ndarray:
     parts = []
     for W, b in zip(coefs, inters):
-        parts.append(np.asarray(W, dtype=np.float32).T.reshape(-1))
-        parts.append(np.asarray(b, dtype=np.float32).reshape(-1))
+        parts.append(np.asarray(W, dtype=dtype).T.reshape(-1))
+        parts.append(np.asarray(b, dtype=dtype).reshape(-1))
     return np.concatenate(parts)
 
 
@@ -303,10 +309,12 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
     P = sum(a * b + b for a, b in zip(dims[:-1], dims[1:]))
     maxw = max(dims[1:])
     L = len(dims) - 1
-    f32 = dict(dtype=torch.float32, device=dev)
-    st = getattr(e0, "_hip_state", None)
-    params = torch.as_tensor(np.stack([_pack(e.coefs_, e.intercepts_) for e in ests]), device=dev).contiguous()
-    if e0._adam is None or not isinstance(e0._adam, dict) or T > 1:
+    f64 = getattr(e0, "dtype", "float64") == "float64"
+    npdt, tdt = (np.float64, torch.float64) if f64 else (np.float32, torch.float32)
+    f32 = dict(dtype=tdt, device=dev)     # element type of every float buffer of the trainer
+    params = torch.as_tensor(np.stack([_pack(e.coefs_, e.intercepts_, npdt) for e in ests]),
+                             device=dev).contiguous()
+    if e0._adam is None or not isinstance(e0._adam, dict) or T > 1 or e0._adam["m"].dtype != tdt:
         mom = torch.zeros(T, P, **f32)
         vel = torch.zeros(T, P, **f32)
         step = torch.zeros(T, dtype=torch.int64, device=dev)
@@ -319,7 +327,7 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
         off += N * K + N
     max_iter = perms.shape[0]
     bufs_t = {
-        "X": torch.as_tensor(np.ascontiguousarray(X, np.float32), device=dev),
+        "X": torch.as_tensor(np.ascontiguousarray(X, npdt), device=dev),
         "y": torch.as_tensor(codes.astype(np.int32), device=dev),
         "perms": torch.as_tensor(np.ascontiguousarray(perms, np.int32), device=dev),
         "epoch_ctr": torch.zeros(1, dtype=torch.int32, device=dev),
@@ -341,7 +349,8 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
            "alpha": float(e0.alpha), "weight_decay": 0.0, "mu": 0.0, "tol": float(e0.tol),
            "n_iter_no_change": int(e0.n_iter_no_change), "max_iter": max_iter,
            "tol_stop": 0 if incremental else 1, "maxw": maxw}
-    tr = m.MLPTrainer(list(dims), T, cfg, {k: v.data_ptr() for k, v in bufs_t.items()})
+    trainer = m.MLPTrainer64 if f64 else m.MLPTrainer
+    tr = trainer(list(dims), T, cfg, {k: v.data_ptr() for k, v in bufs_t.items()})
     stream = torch.cuda.Stream(device=dev)
     stream.wait_stream(torch.cuda.current_stream(dev))
     tr.run(max_iter, stream.cuda_stream, 8, True)
@@ -370,7 +379,7 @@ def fit_packed(ests: List[MLPClassifier], X, y):
     X = np.asarray(X, dtype=np.float64)
     e0 = ests[0]
     sig = lambda e: (tuple(np.atleast_1d(e.hidden_layer_sizes)), e.random_state, e.batch_size, e.alpha,
-                     e.max_iter, e.tol, e.n_iter_no_change, e.shuffle)
+                     e.max_iter, e.tol, e.n_iter_no_change, e.shuffle, getattr(e, "dtype", "float64"))
     if any(sig(e) != sig(e0) for e in ests):
         raise ValueError("fit_packed: estimators must share everything but learning_rate_init")
     if e0._resolve_backend() != "hip":

@@ -1,4 +1,5 @@
-// Native minibatch trainer for T packed MLPs of one architecture (layered path).
+// Native minibatch trainer for T packed MLPs of one architecture (layered path), in fp32
+// (exact-fp32 MFMA) or float64 (f64 MFMA: sklearn's precision, mlp_f64.hip).
 //
 // Serves the scikit-learn-compatible estimator (FL_SkLearn_MLPClassifier_Limitation.py:77-101,
 // hyperparameters_tuning.py:90-91) and the hyperparameter sweep with trial packing: the 9
@@ -19,6 +20,7 @@
 
 #include "gemm_mfma.h"
 #include "gemm_nt_bf16.h"
+#include "mlp_f64.h"
 #include "mlp_ops.h"
 
 namespace py = pybind11;
@@ -36,9 +38,96 @@ static inline T* ptr_of(py::dict& d, const char* k) {
     return reinterpret_cast<T*>(d[k].cast<uintptr_t>());
 }
 
-class MLPTrainer {
+// Kernel dispatch of the trainer by element type: fp32 (gemm_mfma.hip / mlp_ops.hip: exact-fp32
+// MFMA) or float64 (mlp_f64.hip: v_mfma_f64_16x16x4_f64, sklearn's own precision).
+template <typename T> struct TrainerOps;
+
+template <> struct TrainerOps<float> {
+    static void gather(const float* X, int ld, const int* y, const int* perms, int* epoch_ctr, long long n_perm,
+                       int off, int M, int F, float* out, int ldo, int* yb, hipStream_t s) {
+        GatherArgs ga{X, ld, y, perms, epoch_ctr, n_perm, off, M, F, out, ldo, nullptr, yb};
+        TR_CHECK(gather_rows_launch(ga, s));
+    }
+    static void gemm(int M, int N, int K, const float* A, int lda, long long sA, int akc, const float* B, int ldb,
+                     long long sB, int bkc, float* C, int ldc, long long sC, const float* bias, long long sBias,
+                     const float* mask, int ldmask, long long sMask, int epi, const int* active, int T, hipStream_t s) {
+        GemmArgs g{};
+        g.M = M; g.N = N; g.K = K;
+        g.A = A; g.lda = lda; g.sA = sA;
+        g.B = B; g.ldb = ldb; g.sB = sB;
+        g.C = C; g.ldc = ldc; g.sC = sC;
+        g.bias = bias; g.sBias = sBias;
+        g.mask = mask; g.ldmask = ldmask; g.sMask = sMask;
+        g.alpha = 1.f; g.beta = 0.f; g.active = active;
+        TR_CHECK(gemm_launch(g, 0, akc, bkc, epi, 1, T, s));
+    }
+    static void xent(const float* z, int ldz, long long sZ, const int* y, int M, int C, int mode, double scale,
+                     float* dz, int lddz, long long sDz, double* loss_acc, const int* active, int T, hipStream_t s) {
+        XentArgs xa{};
+        xa.z = z; xa.ldz = ldz; xa.sZ = sZ; xa.y = y; xa.idx = nullptr; xa.M = M; xa.C = C; xa.mode = mode;
+        xa.scale = (float)scale; xa.dz = dz; xa.lddz = lddz; xa.sDz = sDz; xa.loss_acc = loss_acc; xa.pred = nullptr;
+        xa.active = active;
+        TR_CHECK(xent_launch(xa, T, s));
+    }
+    static void colsum(const float* X, int M, int N, int ld, float* out, int T, long long sX, long long sOut,
+                       const int* active, hipStream_t s) {
+        TR_CHECK(colsum_launch(X, M, N, ld, out, 0.f, T, sX, sOut, active, s));
+    }
+    static void adam(float* p, float* m, float* v, const float* g, const float* anchor, const unsigned char* wd_mask,
+                     size_t n, int style, const double* lr, double b1, double b2, double eps, double wd, double mu,
+                     const long long* step, double* loss_acc, double l2, const int* active, int T, hipStream_t s) {
+        AdamArgs aa{};
+        aa.p = p; aa.m = m; aa.v = v; aa.g = g; aa.anchor = anchor; aa.wd_mask = wd_mask; aa.n = n; aa.style = style;
+        aa.lr = lr; aa.beta1 = b1; aa.beta2 = b2; aa.eps = eps; aa.wd = wd; aa.mu = mu; aa.step = step;
+        aa.loss_acc = loss_acc; aa.l2_coef = l2; aa.active = active; aa.p_bf16 = nullptr;
+        TR_CHECK(adam_launch(aa, T, s));
+    }
+};
+
+template <> struct TrainerOps<double> {
+    static void gather(const double* X, int ld, const int* y, const int* perms, int* epoch_ctr, long long n_perm,
+                       int off, int M, int F, double* out, int ldo, int* yb, hipStream_t s) {
+        TR_CHECK(gather_rows_f64_launch(X, ld, y, perms, epoch_ctr, n_perm, off, M, F, out, ldo, yb, s));
+    }
+    static void gemm(int M, int N, int K, const double* A, int lda, long long sA, int akc, const double* B, int ldb,
+                     long long sB, int bkc, double* C, int ldc, long long sC, const double* bias, long long sBias,
+                     const double* mask, int ldmask, long long sMask, int epi, const int* active, int T,
+                     hipStream_t s) {
+        Gemm64Args g{};
+        g.M = M; g.N = N; g.K = K;
+        g.A = A; g.lda = lda; g.sA = sA;
+        g.B = B; g.ldb = ldb; g.sB = sB;
+        g.C = C; g.ldc = ldc; g.sC = sC;
+        g.bias = bias; g.sBias = sBias;
+        g.mask = mask; g.ldmask = ldmask; g.sMask = sMask;
+        g.alpha = 1.0; g.beta = 0.0; g.active = active;
+        TR_CHECK(gemm_f64_launch(g, akc, bkc, epi, T, s));
+    }
+    static void xent(const double* z, int ldz, long long sZ, const int* y, int M, int C, int mode, double scale,
+                     double* dz, int lddz, long long sDz, double* loss_acc, const int* active, int T, hipStream_t s) {
+        TR_CHECK(xent_f64_launch(z, ldz, sZ, y, M, C, mode, scale, dz, lddz, sDz, loss_acc, active, T, s));
+    }
+    static void colsum(const double* X, int M, int N, int ld, double* out, int T, long long sX, long long sOut,
+                       const int* active, hipStream_t s) {
+        TR_CHECK(colsum_f64_launch(X, M, N, ld, out, 0.0, T, sX, sOut, active, s));
+    }
+    static void adam(double* p, double* m, double* v, const double* g, const double* anchor,
+                     const unsigned char* wd_mask, size_t n, int style, const double* lr, double b1, double b2,
+                     double eps, double wd, double mu, const long long* step, double* loss_acc, double l2,
+                     const int* active, int T, hipStream_t s) {
+        Adam64Args a{};
+        a.p = p; a.m = m; a.v = v; a.g = g; a.anchor = anchor; a.wd_mask = wd_mask; a.n = n; a.style = style;
+        a.lr = lr; a.beta1 = b1; a.beta2 = b2; a.eps = eps; a.wd = wd; a.mu = mu; a.step = step;
+        a.loss_acc = loss_acc; a.l2_coef = l2; a.active = active;
+        TR_CHECK(adam_f64_launch(a, T, s));
+    }
+};
+
+template <typename T>
+class MLPTrainerT {
   public:
-    MLPTrainer(std::vector<int> dims, int T, py::dict cfg, py::dict bufs) : dims_(dims), T_(T) {
+    using Ops = TrainerOps<T>;
+    MLPTrainerT(std::vector<int> dims, int Tr, py::dict cfg, py::dict bufs) : dims_(dims), T_(Tr) {
         L_ = (int)dims.size() - 1;
         if (L_ < 1) throw std::runtime_error("MLPTrainer: need >= 1 layer");
         int off = 0;
@@ -63,15 +152,15 @@ class MLPTrainer {
         nic_ = cfg["n_iter_no_change"].cast<int>();
         max_iter_ = cfg["max_iter"].cast<int>();
         tol_stop_ = cfg["tol_stop"].cast<int>();
-        X_ = ptr_of<const float>(bufs, "X");
+        X_ = ptr_of<const T>(bufs, "X");
         y_ = ptr_of<const int>(bufs, "y");
         perms_ = ptr_of<const int>(bufs, "perms");
         epoch_ctr_ = ptr_of<int>(bufs, "epoch_ctr");
-        params_ = ptr_of<float>(bufs, "params");
-        grads_ = ptr_of<float>(bufs, "grads");
-        m_ = ptr_of<float>(bufs, "m");
-        v_ = ptr_of<float>(bufs, "v");
-        anchor_ = ptr_of<const float>(bufs, "anchor");
+        params_ = ptr_of<T>(bufs, "params");
+        grads_ = ptr_of<T>(bufs, "grads");
+        m_ = ptr_of<T>(bufs, "m");
+        v_ = ptr_of<T>(bufs, "v");
+        anchor_ = ptr_of<const T>(bufs, "anchor");
         wd_mask_ = ptr_of<const unsigned char>(bufs, "wd_mask");
         lr_ = ptr_of<const double>(bufs, "lr");
         step_ = ptr_of<long long>(bufs, "step");
@@ -81,69 +170,43 @@ class MLPTrainer {
         n_iter_ = ptr_of<int>(bufs, "n_iter");
         active_ = ptr_of<int>(bufs, "active");
         curve_ = ptr_of<double>(bufs, "curve");
-        xb_ = ptr_of<float>(bufs, "xb");
+        xb_ = ptr_of<T>(bufs, "xb");
         yb_ = ptr_of<int>(bufs, "yb");
-        acts_ = ptr_of<float>(bufs, "acts");    // [L][T][B][maxw]
-        deltas_ = ptr_of<float>(bufs, "deltas");
+        acts_ = ptr_of<T>(bufs, "acts");    // [L][T][B][maxw]
+        deltas_ = ptr_of<T>(bufs, "deltas");
         maxw_ = cfg["maxw"].cast<int>();
     }
-    ~MLPTrainer() { drop_graph(); }
+    ~MLPTrainerT() { drop_graph(); }
 
     int P() const { return P_; }
 
     // One minibatch step on rows perm[epoch][off : off+rows].
     void step(int off, int rows, hipStream_t s) {
-        GatherArgs ga{X_, dims_[0], y_, perms_, epoch_ctr_, (long long)n_, off, rows, dims_[0], xb_, dims_[0],
-                      nullptr, yb_};
-        TR_CHECK(gather_rows_launch(ga, s));
+        Ops::gather(X_, dims_[0], y_, perms_, epoch_ctr_, (long long)n_, off, rows, dims_[0], xb_, dims_[0], yb_, s);
         forward(xb_, rows, s, acts_, /*Bstride*/ B_);
+        const long long sAct = (long long)B_ * maxw_;
         // loss head
-        const int C = dims_[L_];
-        XentArgs xa{};
-        xa.z = act(L_ - 1); xa.ldz = maxw_; xa.sZ = (long long)B_ * maxw_;
-        xa.y = yb_; xa.idx = nullptr; xa.M = rows; xa.C = C; xa.mode = head_;
-        xa.scale = 1.f / (float)rows;
-        xa.dz = delta(L_ - 1); xa.lddz = maxw_; xa.sDz = (long long)B_ * maxw_;
-        xa.loss_acc = loss_acc_; xa.pred = nullptr; xa.active = active_;
-        TR_CHECK(xent_launch(xa, T_, s));
+        Ops::xent(act(L_ - 1), maxw_, sAct, yb_, rows, dims_[L_], head_, 1.0 / (double)rows, delta(L_ - 1), maxw_,
+                  sAct, loss_acc_, active_, T_, s);
         // backward
         for (int l = L_ - 1; l >= 0; --l) {
             const int K = dims_[l], N = dims_[l + 1];
-            const float* in = l == 0 ? xb_ : act(l - 1);
-            const long long s_in = l == 0 ? 0 : (long long)B_ * maxw_;
+            const T* in = l == 0 ? xb_ : act(l - 1);
+            const long long s_in = l == 0 ? 0 : sAct;
             const int ld_in = l == 0 ? dims_[0] : maxw_;
             // wgrad: dW[N][K] = dZ^T (rows x N) . in (rows x K)
-            GemmArgs g{};
-            g.M = N; g.N = K; g.K = rows;
-            g.A = delta(l); g.lda = maxw_; g.sA = (long long)B_ * maxw_;
-            g.B = in; g.ldb = ld_in; g.sB = s_in;
-            g.C = grads_ + w_off_[l]; g.ldc = K; g.sC = P_;
-            g.alpha = 1.f; g.beta = 0.f; g.active = active_;
-            TR_CHECK(gemm_launch(g, 0, 0, 0, GEMM_EPI_NONE, 1, T_, s));
-            TR_CHECK(colsum_launch(delta(l), rows, N, maxw_, grads_ + b_off_[l], 0.f, T_, (long long)B_ * maxw_, P_,
-                                   active_, s));
-            if (l > 0) {
-                // dgrad: dIn[rows][K] = dZ . W[N][K], masked by in > 0 (ReLU)
-                GemmArgs d{};
-                d.M = rows; d.N = K; d.K = N;
-                d.A = delta(l); d.lda = maxw_; d.sA = (long long)B_ * maxw_;
-                d.B = params_ + w_off_[l]; d.ldb = K; d.sB = P_;
-                d.C = delta(l - 1); d.ldc = maxw_; d.sC = (long long)B_ * maxw_;
-                d.mask = act(l - 1); d.ldmask = maxw_; d.sMask = (long long)B_ * maxw_;
-                d.alpha = 1.f; d.beta = 0.f; d.active = active_;
-                TR_CHECK(gemm_launch(d, 0, 1, 0, GEMM_EPI_MASK, 1, T_, s));
-            }
+            Ops::gemm(N, K, rows, delta(l), maxw_, sAct, 0, in, ld_in, s_in, 0, grads_ + w_off_[l], K, P_, nullptr, 0,
+                      nullptr, 0, 0, GEMM_EPI_NONE, active_, T_, s);
+            Ops::colsum(delta(l), rows, N, maxw_, grads_ + b_off_[l], T_, sAct, P_, active_, s);
+            if (l > 0)  // dgrad: dIn[rows][K] = dZ . W[N][K], masked by in > 0 (ReLU)
+                Ops::gemm(rows, K, N, delta(l), maxw_, sAct, 1, params_ + w_off_[l], K, P_, 0, delta(l - 1), maxw_, sAct,
+                          nullptr, 0, act(l - 1), maxw_, sAct, GEMM_EPI_MASK, active_, T_, s);
         }
         TR_CHECK(step_count_launch(step_, active_, T_, s));
-        AdamArgs aa{};
-        aa.p = params_; aa.m = m_; aa.v = v_; aa.g = grads_; aa.anchor = anchor_; aa.wd_mask = wd_mask_;
-        aa.n = (size_t)P_; aa.style = style_; aa.lr = lr_; aa.beta1 = beta1_; aa.beta2 = beta2_; aa.eps = eps_;
         // sklearn: coef grads (dW + alpha*W)/batch; torch: weight_decay * p
-        aa.wd = style_ == 1 ? alpha_ / (double)rows : wd_;
-        aa.mu = mu_; aa.step = step_; aa.loss_acc = loss_acc_;
-        aa.l2_coef = style_ == 1 ? 0.5 * alpha_ : 0.0;
-        aa.active = active_; aa.p_bf16 = nullptr;
-        TR_CHECK(adam_launch(aa, T_, s));
+        Ops::adam(params_, m_, v_, grads_, anchor_, wd_mask_, (size_t)P_, style_, lr_, beta1_, beta2_, eps_,
+                  style_ == 1 ? alpha_ / (double)rows : wd_, mu_, step_, loss_acc_, style_ == 1 ? 0.5 * alpha_ : 0.0,
+                  active_, T_, s);
     }
 
     void epoch(hipStream_t s) {
@@ -183,27 +246,22 @@ class MLPTrainer {
     // logits of the last layer land in out [T][rows][ld = maxw].
     void predict_logits(uintptr_t Xp, int rows, uintptr_t ws, uintptr_t stream) {
         hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-        forward(reinterpret_cast<const float*>(Xp), rows, s, reinterpret_cast<float*>(ws), rows, /*gated*/ false);
+        forward(reinterpret_cast<const T*>(Xp), rows, s, reinterpret_cast<T*>(ws), rows, /*gated*/ false);
     }
 
   private:
-    float* act(int l) const { return acts_ + (size_t)l * T_ * B_ * maxw_; }
-    float* delta(int l) const { return deltas_ + (size_t)l * T_ * B_ * maxw_; }
+    T* act(int l) const { return acts_ + (size_t)l * T_ * B_ * maxw_; }
+    T* delta(int l) const { return deltas_ + (size_t)l * T_ * B_ * maxw_; }
 
     // acts layout [L][T][Bs][maxw]; x shared by all trials (row stride dims[0]).
-    void forward(const float* x, int rows, hipStream_t s, float* acts, int Bs, bool gated = true) {
+    void forward(const T* x, int rows, hipStream_t s, T* acts, int Bs, bool gated = true) {
         for (int l = 0; l < L_; ++l) {
             const int K = dims_[l], N = dims_[l + 1];
-            GemmArgs g{};
-            g.M = rows; g.N = N; g.K = K;
-            g.A = l == 0 ? x : acts + (size_t)(l - 1) * T_ * Bs * maxw_;
-            g.lda = l == 0 ? dims_[0] : maxw_;
-            g.sA = l == 0 ? 0 : (long long)Bs * maxw_;
-            g.B = params_ + w_off_[l]; g.ldb = K; g.sB = P_;
-            g.C = acts + (size_t)l * T_ * Bs * maxw_; g.ldc = maxw_; g.sC = (long long)Bs * maxw_;
-            g.bias = params_ + b_off_[l]; g.sBias = P_;
-            g.alpha = 1.f; g.beta = 0.f; g.active = gated ? active_ : nullptr;
-            TR_CHECK(gemm_launch(g, 0, 1, 1, l + 1 < L_ ? GEMM_EPI_BIAS_RELU : GEMM_EPI_BIAS, 1, T_, s));
+            const T* A = l == 0 ? x : acts + (size_t)(l - 1) * T_ * Bs * maxw_;
+            Ops::gemm(rows, N, K, A, l == 0 ? dims_[0] : maxw_, l == 0 ? 0 : (long long)Bs * maxw_, 1,
+                      params_ + w_off_[l], K, P_, 1, acts + (size_t)l * T_ * Bs * maxw_, maxw_, (long long)Bs * maxw_,
+                      params_ + b_off_[l], P_, nullptr, 0, 0, l + 1 < L_ ? GEMM_EPI_BIAS_RELU : GEMM_EPI_BIAS,
+                      gated ? active_ : nullptr, T_, s);
         }
     }
 
@@ -229,20 +287,20 @@ class MLPTrainer {
     std::vector<int> dims_, w_off_, b_off_;
     int T_, L_, P_, n_, B_, head_, style_, nic_, max_iter_, tol_stop_, maxw_;
     double beta1_, beta2_, eps_, alpha_, wd_, mu_, tol_;
-    const float* X_;
+    const T* X_;
     const int* y_;
     const int* perms_;
     int* epoch_ctr_;
-    float *params_, *grads_, *m_, *v_;
-    const float* anchor_;
+    T *params_, *grads_, *m_, *v_;
+    const T* anchor_;
     const unsigned char* wd_mask_;
     const double* lr_;
     long long* step_;
     double *loss_acc_, *best_, *curve_;
     int *count_, *n_iter_, *active_;
-    float* xb_;
+    T* xb_;
     int* yb_;
-    float *acts_, *deltas_;
+    T *acts_, *deltas_;
     hipGraph_t graph_ = nullptr;
     hipGraphExec_t exec_ = nullptr;
 };
@@ -365,12 +423,18 @@ void register_trainer(py::module_& m) {
     m.def("pad_bf16", &pad_bf16_py);
     m.def("xent", &xent_py);
     m.def("adam_flat", &adam_flat_py);
-    py::class_<MLPTrainer>(m, "MLPTrainer")
+    py::class_<MLPTrainerT<float>>(m, "MLPTrainer")
         .def(py::init<std::vector<int>, int, py::dict, py::dict>())
-        .def("run", &MLPTrainer::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
+        .def("run", &MLPTrainerT<float>::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
              py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
-        .def("predict_logits", &MLPTrainer::predict_logits)
-        .def_property_readonly("P", &MLPTrainer::P);
+        .def("predict_logits", &MLPTrainerT<float>::predict_logits)
+        .def_property_readonly("P", &MLPTrainerT<float>::P);
+    py::class_<MLPTrainerT<double>>(m, "MLPTrainer64")
+        .def(py::init<std::vector<int>, int, py::dict, py::dict>())
+        .def("run", &MLPTrainerT<double>::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
+             py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
+        .def("predict_logits", &MLPTrainerT<double>::predict_logits)
+        .def_property_readonly("P", &MLPTrainerT<double>::P);
     m.def("gemm", &gemm_py);
     m.def("colsum", &colsum_py);
     m.def("to_bf16", &to_bf16_py);

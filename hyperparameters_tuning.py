@@ -103,10 +103,18 @@ def main(argv=None):
                     help="round-engine sweep over hidden x lr x local steps (BASELINE config 5)")
     ap.add_argument("--local-steps", type=int, nargs="+", default=None, help="--federated: local steps grid")
     ap.add_argument("--trials-per-gpu", type=int, default=6, help="--federated: concurrent trials per GPU")
-    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32", help="--federated: engine MFMA dtype")
+    ap.add_argument("--dtype", choices=["fp64", "fp32", "bf16"], default=None,
+                    help="sklearn sweep: estimator precision fp64 (default, sklearn's float64) | fp32; "
+                         "--federated: engine MFMA dtype fp32 (default) | bf16")
     a = ap.parse_args(argv)
     if a.federated:
+        if a.dtype == "fp64":
+            ap.error("--federated engines run fp32 or bf16")
+        a.dtype = a.dtype or "fp32"
         return federated_main(a)
+    if a.dtype == "bf16":
+        ap.error("the sklearn sweep trains in fp64 or fp32")
+    a.dtype = a.dtype or "fp64"
     comm = get_world(backend="gloo" if a.device == "cpu" else "auto", device=a.device)
     rank = comm.Get_rank()
     ds = load_tabular(a.data, label=a.label, with_mean=False)
@@ -138,7 +146,7 @@ def main(argv=None):
         if rank == 0:
             print(f"Training Round {rnd + 1}...\n{'-' * 50}")
         best, results = run_sweep(X_local, y_local, comm, hidden, lrs, max_iter=a.max_iter, backend=backend,
-                                  packed=not a.no_pack, on_trial=report, done=done)
+                                  packed=not a.no_pack, on_trial=report, done=done, dtype=a.dtype)
     wall = time.time() - t0
     if a.save and rank == 0:
         save_sweep(a.save, results, best, {"world": comm.Get_size(), "max_iter": a.max_iter})

@@ -1,5 +1,5 @@
 """fedmi MLPClassifier vs scikit-learn (float64 numpy backend: algorithmic parity), the
-[S] limitation (Q8), warm-start fix, packed sweep semantics, and the HIP fp32 backend."""
+[S] limitation (Q8), warm-start fix, packed sweep semantics, and the HIP backends (float64 f64 MFMA, fp32)."""
 import warnings
 
 import numpy as np
@@ -88,15 +88,33 @@ def test_fit_packed_cpu_equals_individual(data):
 
 
 @pytest.mark.gpu
-def test_hip_backend_tracks_float64(data):
+def test_hip_fp32_backend_tracks_float64(data):
     X, y = data
     a = MLPClassifier(hidden_layer_sizes=(50, 100), learning_rate_init=0.004, max_iter=15, random_state=42,
                       backend="numpy").fit(X, y)
     b = MLPClassifier(hidden_layer_sizes=(50, 100), learning_rate_init=0.004, max_iter=15, random_state=42,
-                      backend="hip").fit(X, y)
+                      backend="hip", dtype="float32").fit(X, y)
     assert b.n_iter_ == a.n_iter_
     np.testing.assert_allclose(b.loss_curve_[:5], a.loss_curve_[:5], rtol=2e-4)
     assert (a.predict(X) == b.predict(X)).mean() > 0.97
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hl,binary", [((50, 100), True), ((50, 400), True), ((24,), False)])
+def test_hip_float64_matches_numpy(data, hl, binary):
+    """dtype=float64 HIP trainer (f64 MFMA GEMMs, mlp_f64.hip) against the float64 host
+    implementation: same loss curve to ~1e-9 relative, same stop epoch, same weights."""
+    X, y = data
+    if not binary:
+        y = (np.arange(len(y)) % 3 + y * 3) % 4     # 4 classes: softmax head
+    kw = dict(hidden_layer_sizes=hl, learning_rate_init=0.004, max_iter=60, random_state=42, tol=1e-3)
+    a = MLPClassifier(backend="numpy", **kw).fit(X, y)
+    b = MLPClassifier(backend="hip", dtype="float64", **kw).fit(X, y)
+    assert b.n_iter_ == a.n_iter_
+    np.testing.assert_allclose(b.loss_curve_, a.loss_curve_, rtol=1e-9)
+    for u, v in zip(a.coefs_ + a.intercepts_, b.coefs_ + b.intercepts_):
+        np.testing.assert_allclose(v, u, rtol=1e-7, atol=1e-9)
+    assert (a.predict(X) == b.predict(X)).all()
 
 
 @pytest.mark.gpu
