@@ -49,11 +49,26 @@ struct MLPDesc {
 
 // bf16 LDS layout of the fused kernels (fl_kernels_bf16.hip).  All offsets are BYTES into
 // the dynamic LDS window.  Every fan-in dimension is padded to kp = roundup32(dim) (one
-// v_mfma_f32_16x16x32_bf16 k-step per 32) and rows are kp + 8 elements apart, i.e. 16-byte
-// aligned and an odd number of 16-byte slots, so the 16 rows of a ds_read_b128 lane group
-// hit 16 distinct bank slots.  W_l has kp[l+1] rows (the dgrad contraction runs over its
-// padded fan-out), activations / deltas have R rows.  Transposed operands (wgrad over rows,
-// dgrad over W's rows) are read with ds_read_b64_tr_b16 from the same images.
+// v_mfma_f32_16x16x32_bf16 k-step per 32).  W_l has kp[l+1] rows (the dgrad contraction
+// runs over its padded fan-out), activations / deltas have R rows.  Transposed operands (wgrad
+// over rows, dgrad over W's rows) are read with ds_read_b64_tr_b16 from the same images.
+//
+// Bank conflicts (64 banks x 4 B; ds_read_b128 serves 16 lanes per LDS cycle,
+// ds_read_b64_tr_b16 32 lanes; tests/native/test_layout.cpp models both).  Three layout
+// levels, the best that fits the CU's LDS (fl_layout.h):
+//   * activation / delta rows lda = kp + 16 elements (levels 1, 2): a row stride of an odd
+//     multiple of 32 bytes, on which a b128 group (16 rows x 16 B) and a transposed read of 8
+//     CONSECUTIVE rows x 32 B both tile the 256-byte bank period exactly.  wgrad takes its 32
+//     row-k's as runs 4g..4g+3 / 16+4g..16+4g+3 per 16-lane group g (same order in both
+//     operands), so each transposed read covers 8 consecutive rows.  Level 0: kp + 8.
+//   * W images: row n at fl_wrow(n) = n*ldw*2 + (n/8)*wgap bytes, its 16-byte chunk c stored
+//     at chunk c ^ (wxor * bit 3 of n); lane lr of a forward tile reads W row
+//     fl_fwd_col(lr) = (lr + 4) & 15 and produces that output column.  Level 2: ldw = kp + 16,
+//     wgap 128, wxor 0 -- dgrad's transposed reads of rows {0-3, 8-11} (k-runs tied to the b128
+//     rows of the delta operand) land half a bank period apart, every read is conflict free.
+//     Levels 0/1: ldw = kp + 8, no gap, wxor 1 -- the forward reads are conflict free, dgrad's
+//     transposed W reads 2-way (the 10 KB of gaps and pads do not fit beside R = 32 rows of a
+//     (50, 200) model).
 //
 // Split-bf16 forward ("bf16x3").  Every forward pass computes z = a.W^T as
 // a_hi.W_hi^T + (a_lo.W_hi^T + a_hi.W_lo^T) with x_hi = bf16(x), x_lo = bf16(x - x_hi), fp32
@@ -68,14 +83,18 @@ struct MLPDesc {
 // buffers, unused during the forward pass).
 struct MLPDescB {
     int kp[FL_MAX_LAYERS + 1];        // roundup32(dim[l])
-    int lda[FL_MAX_LAYERS + 1];       // kp[l] + 8: row stride (elements) of act_l, D_l, and W_l rows
-    int w_off[FL_MAX_LAYERS];         // W_l  bf16 [kp[l+1]][lda[l]]  (hi parts)
+    int lda[FL_MAX_LAYERS + 1];       // row stride (elements) of act_l, D_l: kp[l] + 16 (level 0: + 8)
+    int ldw[FL_MAX_LAYERS];           // row stride (elements) of W_l: kp[l] + 16 (level 2) or + 8
+    int wgap;                         // bytes after every 8 W rows (level 2: 128)
+    int wxor;                         // W chunk swizzle (levels 0/1: 1)
+    int level;                        // bank layout level (2 = conflict free, see above)
+    int w_off[FL_MAX_LAYERS];         // W_l  bf16 kp[l+1] rows, fl_wbyte() positions (hi parts)
     int bias_off[FL_MAX_LAYERS];      // b_l  fp32 [kp[l+1]] (zero padded)
     int wlo_delta;                    // W_l lo parts at w_off[l] + wlo_delta (same layout)
     int act_off[FL_MAX_LAYERS + 1];   // act_l bf16 [R][lda[l]]   (l < L), hi parts
     int alo_off[FL_MAX_LAYERS + 1];   // act_l lo parts bf16 [R][lda[l]] (l < L; forward pass only)
     int dlt_off[FL_MAX_LAYERS + 1];   // D_l  bf16 [R][lda[l]]    (1 <= l <= L): dLoss/dz_l
-    int logit_off;                    // fp32 [R][16] classifier logits
+    int logit_off;                    // fp32 [R][FL_LOGIT_LD] classifier logits (16 columns)
     int head_split;                   // logits layer: K split over this many waves (1 = one wave)
     int part_off;                     // ... their fp32 partial logits [head_split][R][C]
     int cm_off;                       // int [16][16] confusion counters (fused evaluation)
@@ -84,6 +103,23 @@ struct MLPDescB {
     int param_bytes;                  // it is stored pre-packed in global memory and staged by a copy
     int lds_bytes;
 };
+
+// Packed bf16 W images (see the bank notes above): byte offset of row n (fl_wrow(kp rows) =
+// image bytes), the chunk swizzle of row n, the byte position of element (n, k), and the W
+// row / output column that lane lr of a forward tile computes.
+__host__ __device__ inline int fl_wrow(int n, int ldw, int wgap) { return n * ldw * 2 + (n >> 3) * wgap; }
+__host__ __device__ inline int fl_wswz(int n, int wxor) { return ((n >> 3) & 1) * wxor; }
+__host__ __device__ inline int fl_wbyte(const MLPDescB& e, int l, int n, int k) {
+    return fl_wrow(n, e.ldw[l], e.wgap) + ((((k >> 3) ^ fl_wswz(n, e.wxor)) << 4) | ((k & 7) << 1));
+}
+__host__ __device__ inline int fl_fwd_col(int lr) { return (lr + 4) & 15; }
+// The 4 accumulator rows of an MFMA lane (4g + j, 16-lane group g) go to LDS in 4 writes; in
+// write t a lane of an odd group writes row 4g + ((t + 1) & 3), so the two 16-lane groups of a
+// 32-lane write half are 5 or 1 rows apart instead of 4 (4 rows = 0 mod the 128-byte write
+// bank period at these strides).
+__host__ __device__ inline int fl_out_row(int lg, int t) { return 4 * lg + ((t + (lg & 1)) & 3); }
+// Logit rows: 17 floats apart (one row per lane in the loss epilogue: distinct banks).
+#define FL_LOGIT_LD 17
 
 struct FLConfig {
     int R;              // rows per workgroup (16 or 32)

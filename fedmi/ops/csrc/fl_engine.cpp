@@ -375,6 +375,8 @@ class FLEngine {
         if (dtype_ == 1) {
             pp_.pk = b_.pk_global;
             pp_.wlo_delta = e_.wlo_delta;
+            pp_.pk_wgap = e_.wgap;
+            pp_.pk_wxor = e_.wxor;
             pp_.L = d_.L;
             for (int l = 0; l < d_.L; ++l) {
                 const int K = d_.dim[l], N = d_.dim[l + 1];
@@ -384,7 +386,7 @@ class FLEngine {
                 pp_.ldw4[l] = fl_ldw(K) / 4;
                 pp_.k4[l] = ((K + 15) & ~15) / 4;
                 pp_.pk_w[l] = e_.w_off[l] - e_.param_off;
-                pp_.pk_lda[l] = e_.lda[l];
+                pp_.pk_lda[l] = e_.ldw[l];
                 pp_.pk_b[l] = e_.bias_off[l] - e_.param_off;
             }
         }
@@ -460,6 +462,7 @@ class FLEngine {
         o["ld"] = ld;
         o["dims"] = dims;
         o["lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : e_.lds_bytes;
+        o["bank_level"] = dtype_ == 0 ? -1 : e_.level;
         o["eval_lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : ev_.lds_bytes;
         o["eval_fedavg"] = peer_ != nullptr && !fused_ && eval_fedavg_fits();
         o["dtype"] = dtype_;

@@ -474,6 +474,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     __shared__ float lag_s[PEER_MAX_WORLD * (FL_MAX_CLASSES * FL_MAX_CLASSES + 1)];
     const int last_local_step = (local_step == c.local_steps - 1);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    FL_STAMP(0);
     const unsigned target = st->calls + 1;  // call index of this kernel's exchanges
     // Round state.  Fused evaluation (fl_common.h): wave 0 of EVERY block folds the previous
     // round's tail (anchor = this round's input image) into the previous state and decides
@@ -598,7 +599,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             const int q = di - d.w_off[l];
             const int n = q / K, k = q - n * K;
             j = d.iw_off[l] + n * fl_ldw(K) + k;
-            pk = e.w_off[l] - e.param_off + (n * e.lda[l] + k) * 2;
+            pk = e.w_off[l] - e.param_off + fl_wbyte(e, l, n, k);
         } else {
             j = d.ib_off[l] + (di - d.b_off[l]);
             pk = e.bias_off[l] - e.param_off + (di - d.b_off[l]) * 4;
@@ -639,16 +640,20 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             }
             if (!have_state) {
                 have_state = true;
+                FL_STAMP(1);
                 round_state();
+                FL_STAMP(2);
             }
 #pragma unroll
             for (int u = 0; u < ADAM_DEPTH; ++u) g += x[u];
         }
     }
     if (!have_state) round_state();
+    FL_STAMP(3);
     part[wave][lane] = g;
     lds_barrier();
     if (wave != 0) return;
+    FL_STAMP(4);
     const FLState S = S_sh;
     if (valid) {
         if (!S.live) {
@@ -658,6 +663,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
                         m0, v0, a0, sc0);
         }
     }
+    FL_STAMP(5);
     if (xchg) {
         // Adam-fused FedAvg of this block's 64 parameters (peer_device.h): publish, wait for
         // every rank's chunk, pull + sum in rank order; global image + packed bf16 image
@@ -668,6 +674,8 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             if (pack) pack_store(b.pk_global, pk, is_bias, e.wlo_delta, gsum);
         }
     }
+    if (b.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stamp the stores' completion
+    FL_STAMP(15);
 }
 
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,

@@ -88,7 +88,7 @@ __global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restri
             w = make_uint4(pack_lo_bf16x2(p0.x, p0.y), pack_lo_bf16x2(p0.z, p0.w), pack_lo_bf16x2(p1.x, p1.y),
                            pack_lo_bf16x2(p1.z, p1.w));
         }
-        char* dst = out + e.w_off[l] - e.param_off + (n * e.lda[l] + 8 * ch) * 2;
+        char* dst = out + e.w_off[l] - e.param_off + fl_wrow(n, e.ldw[l], e.wgap) + 16 * (ch ^ fl_wswz(n, e.wxor));
         *reinterpret_cast<uint4*>(dst) = v;
         *reinterpret_cast<uint4*>(dst + e.wlo_delta) = w;
         return;
@@ -218,8 +218,10 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
     const char* act = lds + e.act_off[l];
     const char* alo = lds + e.alo_off[l];
     const float* bias = reinterpret_cast<const float*>(lds + e.bias_off[l]);
+    const int wc = fl_fwd_col(lr);  // this lane's W row / output column within the tile
+    const int wlane = 16 * (lg ^ fl_wswz(wc, e.wxor));  // its chunk of each k-step (swizzled)
     for (int nt = wave; nt < ntiles; nt += FL_WAVES) {
-        const char* wrow = W + ((nt * 16 + lr) * lda + 8 * lg) * 2;
+        const char* wrow = W + fl_wrow(nt * 16 + wc, e.ldw[l], e.wgap) + wlane;
         const int aoff = (lr * lda + 8 * lg) * 2;
         f32x4 acc[RT], acl[RT];
 #pragma unroll
@@ -243,14 +245,18 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
                 acl[rt] = mfma32(av[rt], bl, acl[rt]);
             }
         }
-        const int n = nt * 16 + lr;
+        const int n = nt * 16 + wc;
         const float b = bias[n];
+        const bool odd = lg & 1;
         if (last) {
             float* z = reinterpret_cast<float*>(lds + e.logit_off);
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) z[(rt * 16 + 4 * lg + j) * 16 + n] = (acc[rt][j] + acl[rt][j]) + b;
+                for (int t = 0; t < 4; ++t) {
+                    const float v = odd ? acc[rt][(t + 1) & 3] + acl[rt][(t + 1) & 3] : acc[rt][t] + acl[rt][t];
+                    z[(rt * 16 + fl_out_row(lg, t)) * FL_LOGIT_LD + n] = v + b;
+                }
         } else {
             uint16_t* out = reinterpret_cast<uint16_t*>(lds + e.act_off[l + 1]);
             uint16_t* olo = reinterpret_cast<uint16_t*>(lds + e.alo_off[l + 1]);
@@ -258,9 +264,10 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float v = fmaxf((acc[rt][j] + acl[rt][j]) + b, 0.f);
-                    const int o = (rt * 16 + 4 * lg + j) * ldo + n;
+                for (int t = 0; t < 4; ++t) {
+                    const float z = odd ? acc[rt][(t + 1) & 3] + acl[rt][(t + 1) & 3] : acc[rt][t] + acl[rt][t];
+                    const float v = fmaxf(z + b, 0.f);
+                    const int o = (rt * 16 + fl_out_row(lg, t)) * ldo + n;
                     out[o] = (uint16_t)bf16_bits(v);
                     olo[o] = (uint16_t)lo_bits(v);
                 }
@@ -283,14 +290,14 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
     for (int t = wave; t < otiles * itiles; t += FL_WAVES) {
         const int ot = t / itiles, it = t - ot * itiles;
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        if (RT >= 2) {  // 32-row K chunks
+        if (RT >= 2) {  // 32-row K chunks; k-runs 4lg.. and 16+4lg.. (8 consecutive rows per read)
 #pragma unroll
             for (int h = 0; h < RT / 2; ++h) {
-                const int r0 = 32 * h + 8 * lg + lq;
+                const int r0 = 32 * h + 4 * lg + lq;
                 const char* pa = D + (r0 * ldd + ot * 16 + 4 * lp) * 2;
                 const char* pb = act + (r0 * lda + it * 16 + 4 * lp) * 2;
-                const bf16x8 a = cat8(ld_tr(pa), ld_tr(pa + 4 * ldd * 2));
-                const bf16x8 b = cat8(ld_tr(pb), ld_tr(pb + 4 * lda * 2));
+                const bf16x8 a = cat8(ld_tr(pa), ld_tr(pa + 16 * ldd * 2));
+                const bf16x8 b = cat8(ld_tr(pb), ld_tr(pb + 16 * lda * 2));
                 acc = mfma32(a, b, acc);
             }
         } else {
@@ -327,7 +334,7 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
     const int lr = lane & 15, lg = lane >> 4, lq = lr >> 2, lp = lr & 3;
     const int itiles = e.kp[l] >> 4;
     const int osteps = e.kp[l + 1] >> 5;
-    const int ldd = e.lda[l + 1], lda = e.lda[l];
+    const int ldd = e.lda[l + 1], lda = e.lda[l], ldw = e.ldw[l];
     const char* Dn = lds + e.dlt_off[l + 1];
     const char* W = lds + e.w_off[l];
     const uint16_t* act = reinterpret_cast<const uint16_t*>(lds + e.act_off[l]);
@@ -336,11 +343,13 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
         f32x4 acc[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        const char* pw = W + ((8 * lg + lq) * lda + it * 16 + 4 * lp) * 2;
+        // W rows 8lg+lq (+4), columns it*16 + 4lp..: 16-byte chunk 2it + lp/2, swizzled
+        const char* pw = W + fl_wrow(8 * lg + lq, ldw, e.wgap) + 32 * it + 16 * ((lp >> 1) ^ fl_wswz(8 * lg, e.wxor)) +
+                         8 * (lp & 1);
         const char* pa = Dn + (lr * ldd + 8 * lg) * 2;
         for (int os = 0; os < osteps; ++os) {
-            const char* pwk = pw + 32 * os * lda * 2;
-            const bf16x8 bv = cat8(ld_tr(pwk), ld_tr(pwk + 4 * lda * 2));
+            const char* pwk = pw + os * (64 * ldw + 4 * e.wgap);  // fl_wrow(32 os + r) - fl_wrow(r)
+            const bf16x8 bv = cat8(ld_tr(pwk), ld_tr(pwk + 4 * ldw * 2));
             bf16x8 av[RT];
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) av[rt] = ld128(pa + rt * 16 * ldd * 2 + os * 64);
@@ -348,12 +357,14 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
             for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(av[rt], bv, acc[rt]);
         }
         const int i = it * 16 + lr;
+        const bool odd = lg & 1;
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int o = (rt * 16 + 4 * lg + j) * lda + i;
-                out[o] = act[o] != 0 && !(act[o] & 0x8000u) ? (uint16_t)bf16_bits(acc[rt][j]) : (uint16_t)0;
+            for (int t = 0; t < 4; ++t) {
+                const float g = odd ? acc[rt][(t + 1) & 3] : acc[rt][t];
+                const int o = (rt * 16 + fl_out_row(lg, t)) * lda + i;
+                out[o] = act[o] != 0 && !(act[o] & 0x8000u) ? (uint16_t)bf16_bits(g) : (uint16_t)0;
             }
     }
 }
@@ -370,8 +381,9 @@ __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPD
     const int ksteps = e.kp[l] >> 5, kper = (ksteps + G - 1) / G;
     const int lda = e.lda[l];
     float* part = reinterpret_cast<float*>(lds + e.part_off);
+    const int wc = fl_fwd_col(lr);
     if (wave < G) {
-        const char* wrow = lds + e.w_off[l] + (lr * lda + 8 * lg) * 2;
+        const char* wrow = lds + e.w_off[l] + fl_wrow(wc, e.ldw[l], e.wgap) + 16 * (lg ^ fl_wswz(wc, e.wxor));
         const char* act = lds + e.act_off[l];
         const char* alo = lds + e.alo_off[l];
         const int aoff = (lr * lda + 8 * lg) * 2;
@@ -398,11 +410,11 @@ __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPD
                 acl[rt] = mfma32(av[rt], bl, acl[rt]);
             }
         }
-        if (lr < C) {
+        if (wc < C) {
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) part[(wave * RT * 16 + rt * 16 + 4 * lg + j) * C + lr] = acc[rt][j] + acl[rt][j];
+                for (int j = 0; j < 4; ++j) part[(wave * RT * 16 + rt * 16 + 4 * lg + j) * C + wc] = acc[rt][j] + acl[rt][j];
         }
     }
     lds_barrier();
@@ -412,7 +424,7 @@ __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPD
         const int row = i / C, c = i - row * C;
         float s = part[row * C + c];
         for (int w = 1; w < G; ++w) s += part[(w * RT * 16 + row) * C + c];
-        z[row * 16 + c] = s + bias[c];
+        z[row * FL_LOGIT_LD + c] = s + bias[c];
     }
 }
 
@@ -498,7 +510,7 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
                 // the scored model's argmax: counts -> b.cnt after the CE barrier below
                 const int r = threadIdx.x;
                 if (row0 + r < c.n_rows) {
-                    const float* zr = reinterpret_cast<const float*>(lds + e.logit_off) + r * 16;
+                    const float* zr = reinterpret_cast<const float*>(lds + e.logit_off) + r * FL_LOGIT_LD;
                     int best = 0;
                     float bv = zr[0];
                     for (int k = 1; k < C; ++k)
@@ -523,7 +535,7 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     float lossv = 0.f;
     if (threadIdx.x < R) {
         const int r = threadIdx.x, row = row0 + r;
-        const float* zr = z + r * 16;
+        const float* zr = z + r * FL_LOGIT_LD;
         uint16_t* dr = DL + r * ldL;
         if (row < c.n_rows) {
             const int y = ylab;
@@ -593,7 +605,7 @@ __device__ void eval_rows_bf16(const MLPDesc& d, const MLPDescB& e, const FLConf
     if (threadIdx.x < R) {
         const int r = threadIdx.x, row = row0 + r;
         if (row < c.n_rows) {
-            const float* zr = reinterpret_cast<const float*>(lds + e.logit_off) + r * 16;
+            const float* zr = reinterpret_cast<const float*>(lds + e.logit_off) + r * FL_LOGIT_LD;
             int best = 0;
             float bv = zr[0];
             for (int k = 1; k < C; ++k)

@@ -56,20 +56,24 @@ inline void fl_build_fp32_layout(const int* dims, int L, int R, MLPDesc* d) {
 }
 
 // bf16 LDS layouts (fl_common.h MLPDescB), byte offsets, 16-byte aligned pieces: `e` for the
-// train kernel, `ev` for the evaluation kernels (forward pass only).
-inline void fl_build_bf16_layout(const MLPDesc& d, int R, MLPDescB* e_out, MLPDescB* ev_out) {
+// train kernel, `ev` for the evaluation kernels (forward pass only), at bank layout `level`.
+inline void fl_build_bf16_layout_level(const MLPDesc& d, int R, int level, MLPDescB* e_out, MLPDescB* ev_out) {
     MLPDescB e, ev;
     std::memset(&e, 0, sizeof(e));
     const int L = d.L;
+    e.level = level;
+    e.wgap = level == 2 ? 128 : 0;
+    e.wxor = level == 2 ? 0 : 1;
     for (int l = 0; l <= L; ++l) {
         e.kp[l] = (d.dim[l] + 31) & ~31;
-        e.lda[l] = e.kp[l] + 8;
+        e.lda[l] = e.kp[l] + (level >= 1 ? 16 : 8);
+        if (l < L) e.ldw[l] = e.kp[l] + (level == 2 ? 16 : 8);
     }
     int off = 0;
     auto take = [&](int bytes) { const int o = off; off += (bytes + 15) & ~15; return o; };
     for (int l = 0; l < L; ++l) e.act_off[l] = take(R * e.lda[l] * 2);
     for (int l = 1; l <= L; ++l) e.dlt_off[l] = take(R * e.lda[l] * 2);
-    e.logit_off = take(R * 16 * 4);
+    e.logit_off = take(R * FL_LOGIT_LD * 4);
     e.cm_off = take(FL_CM_INTS * 4);
     // split-bf16 forward: lo parts of the layer inputs -- X in its own buffer, the hidden
     // activations in the delta buffers (same [R][lda] shape, free until the backward pass)
@@ -78,10 +82,10 @@ inline void fl_build_bf16_layout(const MLPDesc& d, int R, MLPDescB* e_out, MLPDe
     // parameter region: W hi images, biases, W lo images (each W size is a multiple of 16
     // bytes, so the lo images sit at one constant offset from their hi images)
     e.param_off = off;
-    for (int l = 0; l < L; ++l) e.w_off[l] = take(e.kp[l + 1] * e.lda[l] * 2);
+    for (int l = 0; l < L; ++l) e.w_off[l] = take(fl_wrow(e.kp[l + 1], e.ldw[l], e.wgap));
     for (int l = 0; l < L; ++l) e.bias_off[l] = take(e.kp[l + 1] * 4);
     e.wlo_delta = off - e.w_off[0];
-    for (int l = 0; l < L; ++l) take(e.kp[l + 1] * e.lda[l] * 2);
+    for (int l = 0; l < L; ++l) take(fl_wrow(e.kp[l + 1], e.ldw[l], e.wgap));
     e.param_bytes = off - e.param_off;
     e.lds_bytes = off;
     e.item_base[0] = 0;
@@ -92,7 +96,7 @@ inline void fl_build_bf16_layout(const MLPDesc& d, int R, MLPDescB* e_out, MLPDe
     off = 0;
     for (int l = 0; l < L; ++l) ev.act_off[l] = take(R * e.lda[l] * 2);
     for (int l = 1; l <= L; ++l) ev.dlt_off[l] = -1;
-    ev.logit_off = take(R * 16 * 4);
+    ev.logit_off = take(R * FL_LOGIT_LD * 4);
     ev.cm_off = take(FL_CM_INTS * 4);
     for (int l = 0; l < L; ++l) ev.alo_off[l] = take(R * e.lda[l] * 2);
     ev.param_off = off;
@@ -120,4 +124,13 @@ inline void fl_build_bf16_layout(const MLPDesc& d, int R, MLPDescB* e_out, MLPDe
     }
     *e_out = e;
     *ev_out = ev;
+}
+
+// The most conflict-free level whose train and evaluation layouts fit the CU's LDS (level 0
+// when none fits: the engine then refuses this R).
+inline void fl_build_bf16_layout(const MLPDesc& d, int R, MLPDescB* e_out, MLPDescB* ev_out) {
+    for (int level = 2; level >= 0; --level) {
+        fl_build_bf16_layout_level(d, R, level, e_out, ev_out);
+        if (std::max(e_out->lds_bytes, ev_out->lds_bytes) <= (int)FL_LDS_DYNAMIC_MAX) return;
+    }
 }

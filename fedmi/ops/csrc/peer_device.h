@@ -33,7 +33,8 @@ struct PeerPack {
     int ldw4[FL_MAX_LAYERS];        // float4s per image row of W_l
     int k4[FL_MAX_LAYERS];          // packed float4 columns per row: roundup16(K_l) / 4
     int pk_w[FL_MAX_LAYERS];        // byte offset of W_l in the packed region
-    int pk_lda[FL_MAX_LAYERS];      // packed row stride (bf16 elements)
+    int pk_lda[FL_MAX_LAYERS];      // packed W row stride (bf16 elements, MLPDescB::ldw)
+    int pk_wgap, pk_wxor;           // packed W row gaps / chunk swizzle (fl_common.h)
     int pk_b[FL_MAX_LAYERS];        // byte offset of b_l in the packed region
 };
 
@@ -106,7 +107,8 @@ __device__ __forceinline__ void peer_pack_store(const PeerPack& p, int i, float4
             if (c4 < p.k4[l]) {  // columns [roundup16(K), ldw) are the image's zero pad
                 const uint32_t hx = peer_bf16_rne(s.x), hy = peer_bf16_rne(s.y), hz = peer_bf16_rne(s.z),
                                hw = peer_bf16_rne(s.w);
-                char* dst = p.pk + p.pk_w[l] + (n * p.pk_lda[l] + 4 * c4) * 2;
+                char* dst = p.pk + p.pk_w[l] + fl_wrow(n, p.pk_lda[l], p.pk_wgap) + 16 * ((c4 >> 1) ^ fl_wswz(n, p.pk_wxor)) +
+                            8 * (c4 & 1);
                 *reinterpret_cast<uint2*>(dst) = make_uint2(hx | (hy << 16), hz | (hw << 16));
                 // lo parts: bf16(x - hi) (split-bf16 forward, fl_common.h)
                 *reinterpret_cast<uint2*>(dst + p.wlo_delta) =

@@ -2,7 +2,10 @@
 
 Train-kernel slots: 0 start, 1 staged, 10+l start of forward layer l, 2 forward done,
 3 CE done, 4.. backward phases, 15 end; 13/14 = s_memtime (core clock) at start / after
-forward, used to report the effective shader clock."""
+forward, used to report the effective shader clock.  Adam-kernel slots (parameter blocks):
+0 start, 1 first slab batch issued, 2 round state folded, 3 slab sums done, 4 partials
+combined, 5 update stored, 15 stores complete; "train->adam" = the gap between the last train
+workgroup's end and the first Adam block's start when the two are launched back to back."""
 import sys, numpy as np, torch
 sys.path.insert(0, ".")
 from fedmi.data.synthetic import make_income_like
@@ -21,6 +24,7 @@ nb = (rows + R - 1) // R
 dbg = torch.zeros(nb * 16, dtype=torch.int64, device=e.device)
 order = [0, 8, 9, 1, 10, 11, 12, 2, 3, 4, 5, 6, 7, 15]
 kinds = [(0, "train"), (2, "eval")] + ([(3, "train, lagged scoring")] if dtype == "bf16" else [])
+nadam = 1 + (e.engine.layout()["P"] + 63) // 64 if "P" in e.engine.layout() else None
 for which, name in kinds:
     for rep in range(5):
         dbg.zero_()
@@ -40,5 +44,33 @@ for which, name in kinds:
     prev = cols[0]
     for c in cols[1:]:
         d = (st[:, c] - st[:, prev]) * 10 / 1000
+        print(f"   phase {prev:2d}->{c:2d}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
+        prev = c
+
+# Adam kernel phases (parameter blocks only: block 0 is the metric-tail block)
+if nadam is not None:
+    dt = torch.zeros(nb * 16, dtype=torch.int64, device=e.device)
+    da = torch.zeros(max(nb, nadam) * 16, dtype=torch.int64, device=e.device)
+    gaps = []
+    for rep in range(5):
+        dt.zero_()
+        da.zero_()
+        e.engine.set_debug(dt.data_ptr())
+        e.engine.launch_one(e.rounds_issued - 1, 0, e._stream())
+        e.engine.set_debug(da.data_ptr())
+        e.engine.launch_one(e.rounds_issued - 1, 1, e._stream())
+        e.stream.synchronize()
+        e.engine.set_debug(0)
+        t = dt.view(nb, 16).cpu().numpy().astype(np.int64)
+        a = da.view(-1, 16).cpu().numpy().astype(np.int64)[1:nadam]
+        gaps.append((a[:, 0].min() - t[:, 15].max()) * 10 / 1000)
+    t0 = a[:, 0].min()
+    print(f"adam: param blocks={nadam - 1} dispatch spread={(a[:,0].max()-t0)*10/1000:.2f}us "
+          f"total={(a[:,15].max()-t0)*10/1000:.2f}us  train->adam gap median {np.median(gaps):.2f}us")
+    prev = 0
+    for c in [1, 2, 3, 4, 5, 15]:
+        if not (a[:, c] > 0).all():
+            continue
+        d = (a[:, c] - a[:, prev]) * 10 / 1000
         print(f"   phase {prev:2d}->{c:2d}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
         prev = c
