@@ -78,6 +78,8 @@ def parse_args(argv=None):
     ap.add_argument("--micro-batch", type=int, default=131072,
                     help="rows per micro-batch for --wide (about 112 KiB of activation buffers per row at 4096 wide: 14 GiB of HBM)")
     ap.add_argument("--eval-every", type=int, default=0, help="--wide: local accuracy every N rounds")
+    ap.add_argument("--wide-allreduce", default="fp32", choices=["fp32", "bf16"],
+                    help="--wide: FedAvg bucket dtype on the wire (fp32 master weights either way)")
     return ap.parse_args(argv)
 
 
@@ -86,7 +88,8 @@ def main_wide(a, comm):
     from fedmi.fl.wide import run_wide_fedavg
     dims = [14, *a.hidden, 2]
     res = run_wide_fedavg(comm, dims, a.synthetic_rows, a.rounds, micro_batch=a.micro_batch, dtype=a.dtype,
-                          lr=a.lr, eval_every=a.eval_every, seed=a.seed + 7, verbose=not a.quiet)
+                          lr=a.lr, eval_every=a.eval_every, seed=a.seed + 7, verbose=not a.quiet,
+                          allreduce_dtype=a.wide_allreduce)
     if comm.rank == 0:
         print(f"wide MLP {'-'.join(map(str, dims))}, {comm.size} client(s) x {a.synthetic_rows} rows: "
               f"{res['median_round_s'] * 1e3:.1f} ms/round, {res['tflops_per_client']:.1f} TFLOP/s per client, "

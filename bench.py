@@ -146,6 +146,8 @@ def main(argv=None):
     ap.add_argument("--wide-rows", type=int, default=131072,
                     help="rows per client (BASELINE config 3 names 1e8-row shards: 12500000 per client at k = 8)")
     ap.add_argument("--micro-batch", type=int, default=131072, help="--config wide: rows per micro-batch")
+    ap.add_argument("--wide-allreduce", default="fp32", choices=["fp32", "bf16"],
+                    help="--config wide: FedAvg bucket dtype on the wire (fp32 master weights either way)")
     a = ap.parse_args(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _self_launch(a, argv)
@@ -262,7 +264,7 @@ def main_wide(a) -> None:
     dims = [14, 4096, 4096, 4096, 2]
     X, y = synth_shard(a.wide_rows, comm.rank, comm.device)
     c = WideClient(X, y, dims, comm=comm if N > 1 else None, n_total=a.wide_rows * N, dtype="bf16", seed=0,
-                   micro_batch=a.micro_batch)
+                   micro_batch=a.micro_batch, allreduce_dtype=a.wide_allreduce)
 
     def barrier():
         if N > 1:
@@ -297,7 +299,8 @@ def main_wide(a) -> None:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": f"synthetic income-shaped (device Philox), {a.wide_rows} rows/client; random-init weights",
             "config": {"model": "MLP " + "-".join(map(str, dims)), "global_batch": a.wide_rows * N, "seq_len": 1,
-                       "parallelism": f"fedavg{N} (1 client/GPU, per-layer RCCL buckets)"},
+                       "parallelism": f"fedavg{N} (1 client/GPU, per-layer RCCL buckets, "
+                                      f"{a.wide_allreduce} on the wire)"},
             "tflops_per_client": c.flops_per_round / (dt / a.steps) / 1e12,
             "local_train_acc_synthetic": c.metrics()["accuracy"],
             "micro_batch": c.mb,

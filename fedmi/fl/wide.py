@@ -30,7 +30,7 @@ class WideClient:
     def __init__(self, X: torch.Tensor, y: torch.Tensor, dims: Sequence[int], comm=None, n_total: Optional[int] = None,
                  micro_batch: int = 131072, lr: float = 0.004, betas=(0.9, 0.999), eps: float = 1e-8,
                  step_size: int = 30, gamma: float = 0.5, seed: int = 0, dtype: str = "bf16",
-                 eval_rows: int = 0):
+                 eval_rows: int = 0, allreduce_dtype: str = "fp32"):
         from ..ops import native
         self.m = native()
         self.dev = X.device
@@ -47,6 +47,9 @@ class WideClient:
         self.step_size, self.gamma = step_size, gamma
         self.dtype = 1 if dtype == "bf16" else 0
         self.eval_rows = eval_rows
+        if allreduce_dtype not in ("fp32", "bf16"):
+            raise ValueError("allreduce_dtype: fp32 | bf16")
+        self.allreduce_dtype = allreduce_dtype
         f32 = dict(dtype=torch.float32, device=self.dev)
         flat = torch.as_tensor(init_flat(self.dims, seed), **f32)
         self.layout = param_layout(self.dims)
@@ -111,6 +114,10 @@ class WideClient:
             self.bhp = torch.zeros(256, **f32)
             self.logits_p = torch.empty(mb, 256, **f32)
             self.logits = self.logits_p[:, :dims[-1]]
+        # bf16 FedAvg buckets (allreduce_dtype="bf16"): the scaled weights cross the links as bf16
+        # (half the bytes), summed by RCCL in bf16 and widened back into the fp32 master copy
+        self.send_bf16 = (torch.empty(flat.numel(), dtype=torch.bfloat16, device=dev)
+                          if allreduce_dtype == "bf16" and self.world > 1 else None)
         self._quantize()
 
     # ------------------------------------------------------------------
@@ -320,8 +327,9 @@ class WideClient:
 
     def aggregate(self):
         """Sample-size-weighted FedAvg: per layer bucket [W_l | b_l], in forward order on the
-        comm stream: scale by n_i/N, all-reduce, re-quantise, record the bucket's event.  The
-        compute stream does not wait here: its next use of layer l waits on event l."""
+        comm stream: one all-reduce of n_i/N * bucket (fp32 buckets, or bf16 buckets filled by
+        one fused scale + round pass), re-quantise, record the bucket's event.  The compute
+        stream does not wait here: its next use of layer l waits on event l."""
         if self.world == 1:
             # FedAvg of one client is the identity: its operand copies are the local model's
             if not getattr(self, "_local_quantized", False):
@@ -330,10 +338,18 @@ class WideClient:
             return
         self.comm_stream.wait_stream(self.stream)  # the Adam step (and evaluation) are done
         for l, ((name, shape, off), (bn, bs, boff)) in enumerate(zip(self.layout[0::2], self.layout[1::2])):
+            end = boff + int(np.prod(bs))
             with torch.cuda.stream(self.comm_stream):
-                seg = self.params[off:boff + int(np.prod(bs))]
-                seg.mul_(self.agg)
-                self.comm.allreduce_(seg)
+                seg = self.params[off:end]
+                if self.send_bf16 is None:
+                    self.comm.allreduce_(seg, scale=self.agg)
+                else:
+                    # the n_i / N weight is applied by the fp32 -> bf16 pass that fills the bucket
+                    bseg = self.send_bf16[off:end]
+                    self.m.to_bf16(seg.data_ptr(), bseg.data_ptr(), seg.numel(), self.comm_stream.cuda_stream,
+                                   self.agg)
+                    self.comm.allreduce_(bseg)
+                    seg.copy_(bseg)
             self._quantize_layer(l, self.comm_stream)
             ev = torch.cuda.Event()
             ev.record(self.comm_stream)
@@ -394,7 +410,7 @@ class WideClient:
 
 def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int, micro_batch: int = 131072,
                     dtype: str = "bf16", lr: float = 0.004, eval_every: int = 0, seed: int = 7,
-                    verbose: bool = True) -> dict:
+                    verbose: bool = True, allreduce_dtype: str = "fp32") -> dict:
     """BASELINE config 3 driver: every rank is one client holding ``rows_per_client``
     synthetic income-shaped rows generated on its GPU, trains the wide MLP ``dims`` with
     full-batch (micro-batched) Adam steps and averages per layer bucket every round.
@@ -407,7 +423,7 @@ def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int
     world = comm.size if comm is not None else 1
     X, y = device_shard(rows_per_client, rank, dev, seed=seed)
     c = WideClient(X, y, dims, comm=comm if world > 1 else None, n_total=rows_per_client * world,
-                   micro_batch=micro_batch, lr=lr, dtype=dtype, seed=0)
+                   micro_batch=micro_batch, lr=lr, dtype=dtype, seed=0, allreduce_dtype=allreduce_dtype)
     losses, accs, times = [], [], []
     for r in range(rounds):
         t0 = time.perf_counter()

@@ -75,6 +75,10 @@ class RcclComm {
         NCCL_CHECK(ncclAllReduce(as_ptr<float>(buf), as_ptr<float>(buf), count, ncclFloat32, ncclSum,
                                  comm_, as_stream(stream)));
     }
+    void allreduce_bf16(uintptr_t buf, size_t count, uintptr_t stream) {
+        NCCL_CHECK(ncclAllReduce(as_ptr<void>(buf), as_ptr<void>(buf), count, ncclBfloat16, ncclSum, comm_,
+                                 as_stream(stream)));
+    }
     void allreduce_f64(uintptr_t buf, size_t count, uintptr_t stream) {
         NCCL_CHECK(ncclAllReduce(as_ptr<double>(buf), as_ptr<double>(buf), count, ncclFloat64, ncclSum,
                                  comm_, as_stream(stream)));
@@ -676,6 +680,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def_static("unique_id", &RcclComm::unique_id)
         .def("allreduce_f32", &RcclComm::allreduce_f32)
         .def("allreduce_f64", &RcclComm::allreduce_f64)
+        .def("allreduce_bf16", &RcclComm::allreduce_bf16)
         .def("allgather_f32", &RcclComm::allgather_f32)
         .def("broadcast_bytes", &RcclComm::broadcast_bytes)
         .def("abort", &RcclComm::abort)

@@ -257,9 +257,11 @@ __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ 
     }
 }
 
-__global__ void f32_to_bf16_kernel(const float* __restrict__ x, __hip_bfloat16* __restrict__ y, size_t n) {
+// y = bf16(scale * x) (scale 1: plain rounding; the wide FedAvg's bf16 buckets carry the
+// n_i / N weight in the same pass)
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, __hip_bfloat16* __restrict__ y, size_t n, float scale) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) y[i] = __float2bfloat16(x[i]);
+    if (i < n) y[i] = __float2bfloat16(x[i] * scale);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -363,8 +365,8 @@ hipError_t colsum_launch(const float* X, int M, int N, int ld, float* out, float
     return hipGetLastError();
 }
 
-hipError_t f32_to_bf16_launch(const float* x, void* y, size_t n, hipStream_t s) {
+hipError_t f32_to_bf16_launch(const float* x, void* y, size_t n, hipStream_t s, float scale) {
     hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
-                       reinterpret_cast<__hip_bfloat16*>(y), n);
+                       reinterpret_cast<__hip_bfloat16*>(y), n, scale);
     return hipGetLastError();
 }

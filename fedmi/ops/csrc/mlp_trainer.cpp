@@ -335,9 +335,9 @@ static void colsum_py(uintptr_t X, int M, int N, int ld, uintptr_t out, float be
                            nullptr, reinterpret_cast<hipStream_t>(stream)));
 }
 
-static void to_bf16_py(uintptr_t x, uintptr_t y, size_t n, uintptr_t stream) {
+static void to_bf16_py(uintptr_t x, uintptr_t y, size_t n, uintptr_t stream, float scale) {
     TR_CHECK(f32_to_bf16_launch(reinterpret_cast<const float*>(x), reinterpret_cast<void*>(y), n,
-                                reinterpret_cast<hipStream_t>(stream)));
+                                reinterpret_cast<hipStream_t>(stream), scale));
 }
 
 // Single-problem loss head (wide path): softmax CE (mode 0) / sklearn binary (mode 1).
@@ -437,5 +437,5 @@ void register_trainer(py::module_& m) {
         .def_property_readonly("P", &MLPTrainerT<double>::P);
     m.def("gemm", &gemm_py);
     m.def("colsum", &colsum_py);
-    m.def("to_bf16", &to_bf16_py);
+    m.def("to_bf16", &to_bf16_py, py::arg("x"), py::arg("y"), py::arg("n"), py::arg("stream"), py::arg("scale") = 1.f);
 }

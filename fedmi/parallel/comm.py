@@ -145,26 +145,39 @@ class Comm:
             os._exit(code)
 
     # ---- data plane ----
-    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place SUM over ranks on the current stream."""
+    def allreduce_(self, t: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
+        """In-place SUM over ranks on the current stream (fp32 / bf16 / fp64); with ``scale``,
+        the sum of ``scale * t``.  (RCCL's pre-multiplied-sum op would fold the scale into the
+        collective, but on this image's RCCL a one-rank communicator left the tail elements of
+        some counts unscaled, e.g. 40001-40008 elements: past index 40000 -- so the scale is an
+        explicit pass, or fused into the producer as in WideClient's bf16 buckets.)"""
         if self.size == 1:
-            return t
+            return t.mul_(scale) if scale is not None else t
         if t.is_cuda:
             if self.native is not None:
                 stream = torch.cuda.current_stream(t.device).cuda_stream
+                if scale is not None:
+                    t.mul_(scale)
                 if t.dtype == torch.float32:
                     self.native.allreduce_f32(t.data_ptr(), t.numel(), stream)
+                elif t.dtype == torch.bfloat16:
+                    self.native.allreduce_bf16(t.data_ptr(), t.numel(), stream)
                 elif t.dtype == torch.float64:
                     self.native.allreduce_f64(t.data_ptr(), t.numel(), stream)
                 else:
                     raise TypeError(f"allreduce_: unsupported dtype {t.dtype}")
-            elif self._nccl_group is not None:
+                return t
+            if scale is not None:
+                t.mul_(scale)
+            if self._nccl_group is not None:
                 dist.all_reduce(t, group=self._nccl_group)
             else:  # no device communicator: through the host (gloo)
                 h = t.cpu()
                 dist.all_reduce(h)
                 t.copy_(h)
         else:
+            if scale is not None:
+                t.mul_(scale)
             dist.all_reduce(t)
         return t
 

@@ -137,3 +137,34 @@ def test_partial_participation_over_gloo():
         parts = res[0][2][r][0]
         assert abs(h["loss"][r] - np.mean([res[k][2][r][4] for k in parts])) < 1e-6
         np.testing.assert_allclose(h["global"][r], h["per_rank"][r][parts].mean(axis=0), atol=1e-12)
+
+
+def _scaled_worker(rank, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch
+    torch.set_num_threads(1)
+    from fedmi.parallel.comm import Comm
+    comm = Comm(backend="gloo", device="cpu")
+    a = torch.full((7,), float(rank + 1))
+    b = torch.full((5,), float(rank + 1), dtype=torch.bfloat16)
+    comm.allreduce_(a, scale=0.25 * (rank + 1))          # sum of w_i * x_i
+    comm.allreduce_(b, scale=0.5)
+    q.put((rank, a.tolist(), b.float().tolist()))
+    comm.close()
+
+
+def test_comm_scaled_allreduce_over_gloo():
+    """Comm.allreduce_(t, scale): the sum of scale_i * t_i (FedAvg weights), fp32 and bf16."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scaled_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=60) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+    for _, a, b in out:
+        assert a == [0.25 * 1 + 0.5 * 2] * 7
+        assert b == [0.5 * 1 + 0.5 * 2] * 5

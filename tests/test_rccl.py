@@ -3,7 +3,8 @@ one-GPU box: RCCL cannot put two ranks on one device, so these run a ONE-rank co
 every call still goes through ``ncclCommInitRank`` / ``ncclAllReduce`` / ``ncclBroadcast`` /
 ``ncclAllGather`` on a real stream, eagerly and inside captured HIP graphs:
 
-* raw collectives (f32 / f64 all-reduce, byte broadcast, all-gather), eager and captured;
+* raw collectives (f32 / f64 / bf16 all-reduce, byte broadcast, all-gather), eager and
+  captured;
 * the fused round engine issuing its FedAvg all-reduce through RCCL (an emulating engine:
   ``emulate_clients`` keeps the multi-client round shape at world 1), eager and inside
   ``FLEngine.capture``: bit-identical to the same engine without a collective (a one-rank
@@ -46,6 +47,12 @@ def test_rccl_raw_collectives_eager_and_graph():
     s.synchronize()
     assert torch.equal(x, ref) and torch.equal(xd, refd) and torch.equal(out, ref)
     assert torch.equal(b.cpu(), torch.arange(256, dtype=torch.uint8))
+    xb = torch.randn(40001, device=dev).to(torch.bfloat16)
+    refb = xb.clone()
+    with torch.cuda.stream(s):
+        rc.allreduce_bf16(xb.data_ptr(), xb.numel(), s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(xb, refb)
     # captured: all-reduce of a buffer that a captured kernel rewrites before every replay
     g = torch.cuda.CUDAGraph()
     y = torch.zeros(4096, device=dev)
@@ -87,9 +94,11 @@ def test_round_engine_fedavg_through_rccl(dtype):
     rc.destroy()
 
 
-def test_wide_aggregate_through_rccl():
-    """WideClient.aggregate: per-layer buckets scaled by n_i/N and all-reduced over RCCL on the
-    comm stream (one rank: the scale is 1, so the weights must come back unchanged)."""
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_wide_aggregate_through_rccl(wire):
+    """WideClient.aggregate: per-layer buckets all-reduced as n_i/N-scaled sums on the comm
+    stream, fp32 or bf16 on the wire (one rank: the scale is 1, so the weights must come back
+    unchanged -- bf16: up to one bf16 rounding)."""
     import torch
     from fedmi.data.synthetic import make_income_like
     from fedmi.fl.wide import WideClient
@@ -103,11 +112,16 @@ def test_wide_aggregate_through_rccl():
     before = c.params.clone()
     # force the multi-client aggregate path with the one-rank RCCL communicator
     c.world, c.comm = 2, _OneRankDevComm(rc)
+    if wire == "bf16":
+        c.send_bf16 = torch.empty(c.params.numel(), dtype=torch.bfloat16, device=dev)
     c.aggregate()
     c.sync()
     torch.cuda.synchronize()
-    assert c.comm.calls == c.L
-    assert torch.equal(c.params, before)
+    assert c.comm.calls == c.L and c.comm.scales == ([c.agg] if wire == "fp32" else [None]) * c.L
+    if wire == "fp32":
+        assert torch.equal(c.params, before)
+    else:
+        assert torch.equal(c.params, before.to(torch.bfloat16).float())
     rc.destroy()
 
 
@@ -115,10 +129,17 @@ class _OneRankDevComm:
     """Comm stand-in whose device all-reduce is the one-rank RCCL communicator."""
 
     def __init__(self, rc):
-        self.rc, self.calls, self.size, self.rank = rc, 0, 1, 0
+        self.rc, self.calls, self.size, self.rank, self.scales = rc, 0, 1, 0, []
 
-    def allreduce_(self, t):
+    def allreduce_(self, t, scale=None):
         import torch
-        self.rc.allreduce_f32(t.data_ptr(), t.numel(), torch.cuda.current_stream(t.device).cuda_stream)
+        s = torch.cuda.current_stream(t.device).cuda_stream
+        if scale is not None:
+            t.mul_(scale)
+        if t.dtype == torch.bfloat16:
+            self.rc.allreduce_bf16(t.data_ptr(), t.numel(), s)
+        else:
+            self.rc.allreduce_f32(t.data_ptr(), t.numel(), s)
         self.calls += 1
+        self.scales.append(scale)
         return t
