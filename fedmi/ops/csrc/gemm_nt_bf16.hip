@@ -192,6 +192,78 @@ gemm_nt_bf16_kernel(NTArgs g) {
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// Epilogue of the 256x256 loops (ping-pong and full-line): the block's 256x256 bf16 output tile is
+// staged through the (now free) 128 KiB of LDS; see the comment inside.
+__device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (&acc)[8][4], int m0, int n0, int w,
+                                            int l) {
+    const int wr = w >> 2, wc = w & 3;
+    const int lr = l & 15, lg = l >> 4;
+
+    // Epilogue.  Every wave's LDS reads retired before that last barrier, so the 128 KiB of LDS
+    // now holds the block's 256x256 bf16 output tile as 512-byte rows whose 16-byte chunk index
+    // is XOR-ed with sw(row) = ((row >> 2) & 3) * 2 (the four 4-row lane groups of a 2-byte
+    // write land on distinct banks; a 16-lane read of 16 chunks of one row stays conflict-free).
+    // Each lane drops its bf16 values into the tile, then the block stores it with full 512-byte
+    // row segments (16 B per lane) instead of 2-byte scattered stores.  The dgrad ReLU mask is
+    // DMA-ed into the same slots first (full-line loads, same swizzle) and overwritten in place
+    // by the lane that reads it.
+    auto sw = [](int row) { return ((row >> 2) & 3) * 2; };
+    auto tile_off = [&](int row, int col) { return row * 512 + ((((col >> 3) ^ sw(row))) << 4) + (col & 7) * 2; };
+    __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
+    __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
+    if (g.mask != nullptr) {
+        const __hip_bfloat16* Mk = reinterpret_cast<const __hip_bfloat16*>(g.mask);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = i * 16 + w * 2, rr = row + (l >> 5);
+            glds16(Mk + (size_t)(m0 + rr) * g.ldmask + n0 + (((l & 31) ^ sw(rr)) << 3), smem + row * 512);
+        }
+        vm_wait<0>();
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        const int cl = wc * 64 + 16 * y + lr, n = n0 + cl;
+        const float bv = g.bias != nullptr ? g.bias[n] : 0.f;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) {
+            uint32_t tp[2];  // the lane's 4 consecutive rows of column n, packed for CbT
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int rl = wr * 128 + 16 * x + 4 * lg + j, mm = m0 + rl;
+                __hip_bfloat16* slot = reinterpret_cast<__hip_bfloat16*>(smem + tile_off(rl, cl));
+                float v = acc[x][y][j] * g.alpha + bv;
+                if (g.relu) v = fmaxf(v, 0.f);
+                if (g.mask != nullptr) v = __bfloat162float(*slot) > 0.f ? v : 0.f;
+                if (g.C != nullptr) {
+                    float* cp = g.C + (size_t)mm * g.ldc + n;
+                    if (g.beta != 0.f) v += g.beta * *cp;
+                    *cp = v;
+                }
+                const __hip_bfloat16 hv = __float2bfloat16(v);
+                if (Cb != nullptr) *slot = hv;
+                const uint32_t hb = __bfloat16_as_ushort(hv);
+                if (j & 1) tp[j >> 1] |= hb << 16;
+                else tp[j >> 1] = hb;
+            }
+            if (CbT != nullptr) {  // 8-byte store: rows mm .. mm+3 are contiguous in CbT's row n
+                const size_t off = (size_t)n * g.ldct + m0 + wr * 128 + 16 * x + 4 * lg;
+                *reinterpret_cast<uint2*>(CbT + off) = make_uint2(tp[0], tp[1]);
+            }
+        }
+    }
+    if (Cb != nullptr) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int rr = i * 16 + w * 2 + (l >> 5), p = l & 31;
+            const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * 512 + p * 16);
+            *reinterpret_cast<uint4*>(Cb + (size_t)(m0 + rr) * g.ldcb + n0 + ((p ^ sw(rr)) << 3)) = d;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(NT2_THREADS)
 gemm_nt_bf16_pp_kernel(NTArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
@@ -314,73 +386,169 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
         phase(4 * kt + 3, 3, true);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
-
-    // Epilogue.  Every wave's LDS reads retired before that last barrier, so the 128 KiB of LDS
-    // now holds the block's 256x256 bf16 output tile as 512-byte rows whose 16-byte chunk index
-    // is XOR-ed with sw(row) = ((row >> 2) & 3) * 2 (the four 4-row lane groups of a 2-byte
-    // write land on distinct banks; a 16-lane read of 16 chunks of one row stays conflict-free).
-    // Each lane drops its bf16 values into the tile, then the block stores it with full 512-byte
-    // row segments (16 B per lane) instead of 2-byte scattered stores.  The dgrad ReLU mask is
-    // DMA-ed into the same slots first (full-line loads, same swizzle) and overwritten in place
-    // by the lane that reads it.
-    auto sw = [](int row) { return ((row >> 2) & 3) * 2; };
-    auto tile_off = [&](int row, int col) { return row * 512 + ((((col >> 3) ^ sw(row))) << 4) + (col & 7) * 2; };
-    __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
-    __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
-    if (g.mask != nullptr) {
-        const __hip_bfloat16* Mk = reinterpret_cast<const __hip_bfloat16*>(g.mask);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int row = i * 16 + w * 2, rr = row + (l >> 5);
-            glds16(Mk + (size_t)(m0 + rr) * g.ldmask + n0 + (((l & 31) ^ sw(rr)) << 3), smem + row * 512);
-        }
-        vm_wait<0>();
-        __syncthreads();
-    }
-
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-        const int cl = wc * 64 + 16 * y + lr, n = n0 + cl;
-        const float bv = g.bias != nullptr ? g.bias[n] : 0.f;
-#pragma unroll
-        for (int x = 0; x < 8; ++x) {
-            uint32_t tp[2];  // the lane's 4 consecutive rows of column n, packed for CbT
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int rl = wr * 128 + 16 * x + 4 * lg + j, mm = m0 + rl;
-                __hip_bfloat16* slot = reinterpret_cast<__hip_bfloat16*>(smem + tile_off(rl, cl));
-                float v = acc[x][y][j] * g.alpha + bv;
-                if (g.relu) v = fmaxf(v, 0.f);
-                if (g.mask != nullptr) v = __bfloat162float(*slot) > 0.f ? v : 0.f;
-                if (g.C != nullptr) {
-                    float* cp = g.C + (size_t)mm * g.ldc + n;
-                    if (g.beta != 0.f) v += g.beta * *cp;
-                    *cp = v;
-                }
-                const __hip_bfloat16 hv = __float2bfloat16(v);
-                if (Cb != nullptr) *slot = hv;
-                const uint32_t hb = __bfloat16_as_ushort(hv);
-                if (j & 1) tp[j >> 1] |= hb << 16;
-                else tp[j >> 1] = hb;
-            }
-            if (CbT != nullptr) {  // 8-byte store: rows mm .. mm+3 are contiguous in CbT's row n
-                const size_t off = (size_t)n * g.ldct + m0 + wr * 128 + 16 * x + 4 * lg;
-                *reinterpret_cast<uint2*>(CbT + off) = make_uint2(tp[0], tp[1]);
-            }
-        }
-    }
-    if (Cb != nullptr) {
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int rr = i * 16 + w * 2 + (l >> 5), p = l & 31;
-            const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * 512 + p * 16);
-            *reinterpret_cast<uint4*>(Cb + (size_t)(m0 + rr) * g.ldcb + n0 + ((p ^ sw(rr)) << 3)) = d;
-        }
-    }
+    pp_epilogue(g, smem, acc, m0, n0, w, l);
 }
 
-static int g_nt_variant = 2;
+// ---------------------------------------------------------------------------------------------
+// 256x256 full-line variant (variant 3): variant 2's ping-pong phase structure (8 waves as 2 x 4,
+// four phases of 16 MFMAs per K-tile, counted vmcnt + raw barriers, staggered wave rows, same
+// per-element k order -- bit-identical results), with the operand tiles held as 128-byte LDS
+// rows (both k-halves of a row) and every LDS-DMA a piece of 8 WHOLE 128-byte lines (variant 2:
+// 16 half lines).  The timing experiment that moved variant 2's DMAs onto whole lines ran the
+// main loop 6-10 % faster (profiles/nt_ksweep_r1_experiments.log).
+//
+// LDS: two K-tile buffers of 64 KiB (tile parity), A [256][128 B] then B [256][128 B]; 16-byte
+// chunk c of row r at chunk c ^ ((r >> 1) & 7), which keeps every ds_read_b128 lane group on
+// 16 distinct bank slots.  A DMA piece is rows 8q .. 8q+7 of one operand: lane l lands at row
+// 8q + l/8, physical chunk l%8 (LDS-linear), fetched from logical chunk (l%8) ^ ((row >> 1) & 7).
+//
+// A piece can only be restaged >= 2 phases after the LAST phase that reads either k-half of its
+// rows (a phase's reads retire at the lgkmcnt(0) after its first barrier, and the other wave row
+// runs one barrier behind).  Phases read: r = 0: B ks0 + A m0 ks0 | r = 1: A m1 ks0 + B ks1
+// (fetched a phase early, so B's rows are done after phase 1) | r = 2: A m1 ks1 | r = 3: A m0 ks1.
+// DMA schedule for K-tile u (2 pieces per wave per phase, 8 per K-tile):
+//     phase (u-2).3: B pieces 0,1 | (u-1).0: B pieces 2,3 | (u-1).1: A m0 | (u-1).2: A m1
+// -- 2-4 phases after the last read of the slot's previous tile, 3-5 phases ahead of the first
+// read.  Waits (before a phase's first barrier, retiring what the NEXT phase reads; pieces still
+// allowed in flight, in issue order): r = 0: 4 (B01, B23 of u+1) | r = 3: 4 (A m1 of u+1, B01 of
+// u+2) | r = 1, 2: none.
+__global__ void __launch_bounds__(NT2_THREADS)
+gemm_nt_bf16_fl_kernel(NTArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
+    const int mt = g.M / NT2_BM, nt = g.N / NT2_BM;
+    const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
+    constexpr int GM = 8;  // grouped tile order (variant 2)
+    const int grp = bid / (GM * nt), first_m = grp * GM;
+    const int gsz = min(mt - first_m, GM);
+    const int in_grp = bid - grp * GM * nt;
+    const int m0 = (first_m + in_grp % gsz) * NT2_BM, n0 = (in_grp / gsz) * NT2_BM;
+    const __hip_bfloat16* A = reinterpret_cast<const __hip_bfloat16*>(g.A);
+    const __hip_bfloat16* B = reinterpret_cast<const __hip_bfloat16*>(g.B);
+    const int t = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63;
+    const int wr = w >> 2, wc = w & 3;
+    const int lr = l & 15, lg = l >> 4;
+
+    // lane offsets of a piece (bytes from the piece's first source row): row 8q + l/8, logical
+    // chunk (l%8) ^ ((4q + l/16) & 7) -- depends on the parity of q only
+    uint32_t voA[2], voB[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        const int c = (l & 7) ^ ((4 * par + (l >> 4)) & 7);
+        voA[par] = (uint32_t)(((l >> 3) * g.lda + c * 8) * 2);
+        voB[par] = (uint32_t)(((l >> 3) * g.ldb + c * 8) * 2);
+    }
+    // this wave's pieces: B rows 32w + 8i (i = 0..3); A m0 rows rm0 + 8i, A m1 rows rm0 + 64 + 8i
+    // (i = 0, 1) with rm0 = 16w (w < 4) or 128 + 16(w - 4): piece parities are i & 1
+    const int rm0 = (w < 4) ? 16 * w : 128 + 16 * (w - 4);
+    const char* sbB = reinterpret_cast<const char*>(B + (size_t)(n0 + 32 * w) * g.ldb);
+    const char* sbA0 = reinterpret_cast<const char*>(A + (size_t)(m0 + rm0) * g.lda);
+    const char* sbA1 = reinterpret_cast<const char*>(A + (size_t)(m0 + rm0 + 64) * g.lda);
+    const size_t rowB8 = (size_t)8 * g.ldb * 2, rowA8 = (size_t)8 * g.lda * 2;
+    auto dmaB = [&](int tile, int i) {
+        glds16(sbB + i * rowB8 + tile * 128 + voB[i & 1], smem + (tile & 1) * 65536 + 32768 + (32 * w + 8 * i) * 128);
+    };
+    auto dmaA = [&](int tile, int half, int i) {
+        const char* src = (half ? sbA1 : sbA0) + i * rowA8 + tile * 128 + voA[i & 1];
+        glds16(src, smem + (tile & 1) * 65536 + (rm0 + 64 * half + 8 * i) * 128);
+    };
+
+    // fragment reads: row (16-row group base) + lr, chunk 4 ks + lg swizzled by (lr >> 1) & 7
+    const int f = (lr >> 1) & 7;
+    const int fo0 = lr * 128 + ((lg ^ f) << 4), fo1 = lr * 128 + (((4 + lg) ^ f) << 4);
+    const int aoff = wr * 128 * 128, boff = 32768 + wc * 64 * 128;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[4], bfr[4], bfr1[4];
+
+    const int KT = g.K / 64;
+    // prologue: what phases (-2).3 .. (-1).3 would have issued -- tile 0, then tile 1's B01
+    dmaB(0, 0); dmaB(0, 1); dmaB(0, 2); dmaB(0, 3);
+    dmaA(0, 0, 0); dmaA(0, 0, 1); dmaA(0, 1, 0); dmaA(0, 1, 1);
+    if (KT > 1) {
+        dmaB(1, 0); dmaB(1, 1);
+        vm_wait<4>();  // phase 0 reads B and A m0 of tile 0
+    } else {
+        vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+
+    auto phase = [&](int kt, int r, bool tail) {
+        const char* buf = smem + (kt & 1) * 65536;
+        const int mh = (r == 1 || r == 2) ? 1 : 0;
+        const int fo = (r >= 2) ? fo1 : fo0;
+        if (r == 0) {
+            if (!tail || kt + 1 < KT) { dmaB(kt + 1, 2); dmaB(kt + 1, 3); }
+        } else if (r == 1) {
+            if (!tail || kt + 1 < KT) { dmaA(kt + 1, 0, 0); dmaA(kt + 1, 0, 1); }
+        } else if (r == 2) {
+            if (!tail || kt + 1 < KT) { dmaA(kt + 1, 1, 0); dmaA(kt + 1, 1, 1); }
+        } else {
+            if (!tail || kt + 2 < KT) { dmaB(kt + 2, 0); dmaB(kt + 2, 1); }
+        }
+        if (r == 0) {
+#pragma unroll
+            for (int y = 0; y < 4; ++y) bfr[y] = *reinterpret_cast<const bf16x8*>(buf + boff + y * 16 * 128 + fo0);
+        } else if (r == 1) {
+#pragma unroll
+            for (int y = 0; y < 4; ++y) bfr1[y] = *reinterpret_cast<const bf16x8*>(buf + boff + y * 16 * 128 + fo1);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+            af[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + (mh * 64 + x * 16) * 128 + fo);
+        // the last two K-tiles issue fewer pieces: exact counts there too (a vmcnt(0) right after
+        // an issue would expose a whole DMA latency per phase)
+        if (!tail || kt + 2 < KT) {
+            if (r == 0 || r == 3) vm_wait<4>();
+        } else if (kt + 2 == KT) {
+            if (r == 0) vm_wait<4>();       // A m1 of kt; B01, B23 of kt+1 may fly
+            else if (r == 3) vm_wait<2>();  // B, A m0 of kt+1; its A m1 may fly
+        } else if (r == 0) {
+            vm_wait<0>();                   // last tile: its A m1
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+        if (r <= 1) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                    acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr[y], acc[mh * 4 + x][y], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                    acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr1[y], acc[mh * 4 + x][y], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+    };
+
+    int kt = 0;
+    for (; kt + 2 < KT; ++kt) {
+        phase(kt, 0, false);
+        phase(kt, 1, false);
+        phase(kt, 2, false);
+        phase(kt, 3, false);
+    }
+    for (; kt < KT; ++kt) {
+        phase(kt, 0, true);
+        phase(kt, 1, true);
+        phase(kt, 2, true);
+        phase(kt, 3, true);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
+    pp_epilogue(g, smem, acc, m0, n0, w, l);
+}
+
+static int g_nt_variant = 3;  // 3: full-line 256x256 loop (default), 2: half-line, 1/0: 128x128
 void gemm_nt_set_variant(int v) { g_nt_variant = v; }
 
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
@@ -391,6 +559,14 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
         (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
         hipLaunchKernelGGL(gemm_nt_bf16_pp_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
+        return hipGetLastError();
+    }
+    if (g_nt_variant == 3 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
+        (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&
+        (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
+        (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
+        const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
+        hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
         return hipGetLastError();
     }
     const int blocks = (g.M / NT_BM) * (g.N / NT_BN);

@@ -276,9 +276,10 @@ def test_skinny_wgrad_bf16(C, trans, rows, splits):
 @pytest.mark.parametrize("M,N,K,pad", [(256, 512, 64, 0), (256, 256, 128, 0), (512, 768, 192, 64), (768, 512, 1024, 0),
                                        (2048, 1024, 4096, 8)])
 def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
-    """The 256x256 ping-pong main loop (variant 2) against the 128x128 loop (variant 1): same
-    per-element k order, so bit-identical, and both against an fp32 torch reference; row
-    strides wider than K exercise the DMA source addressing."""
+    """The 256x256 ping-pong main loops (variant 2: half-line DMA pieces, variant 3: whole-line
+    pieces and 128-byte LDS rows) against the 128x128 loop (variant 1): same per-element k
+    order, so bit-identical, and against an fp32 torch reference; row strides wider than K
+    exercise the DMA source addressing."""
     m = native()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
@@ -288,7 +289,7 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     bias = torch.randn(N, device=dev)
     outs = []
     try:
-        for v in (1, 2):
+        for v in (1, 2, 3):
             m.gemm_nt_set_variant(v)
             Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             CbT = torch.empty(N, M, dtype=torch.bfloat16, device=dev)
@@ -299,12 +300,12 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
             outs.append((C, Cb))
             assert torch.equal(CbT, Cb.t())
     finally:
-        m.gemm_nt_set_variant(2)
+        m.gemm_nt_set_variant(3)
     # ReLU-mask epilogue (dgrad: the mask tile is staged through LDS by the ping-pong loop)
     mask = torch.randn(M, N + 8, device=dev).to(torch.bfloat16)
     mouts = []
     try:
-        for v in (1, 2):
+        for v in (1, 2, 3):
             m.gemm_nt_set_variant(v)
             Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             m.gemm_nt(M, N, K, A.data_ptr(), K + pad, B.data_ptr(), K + pad, 0, 0, Cb.data_ptr(), N, 0, 0, 0,
@@ -312,13 +313,14 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
             torch.cuda.synchronize()
             mouts.append(Cb)
     finally:
-        m.gemm_nt_set_variant(2)
-    assert torch.equal(mouts[0], mouts[1])
+        m.gemm_nt_set_variant(3)
+    assert torch.equal(mouts[0], mouts[1]) and torch.equal(mouts[0], mouts[2])
     mref = torch.where(mask[:, :N].float() > 0, A[:, :K].float() @ B[:, :K].float().t(), torch.zeros(M, N, device=dev))
     assert ((mouts[1].float() - mref).abs().max() / mref.abs().max()).item() < 1e-2
     ref = (A[:, :K].float() @ B[:, :K].float().t() + bias).clamp_min(0)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    for v in (1, 2):
+        assert torch.equal(outs[0][0], outs[v][0])
+        assert torch.equal(outs[0][1], outs[v][1])
     assert ((outs[1][0] - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 

@@ -1,5 +1,7 @@
 """NT GEMM fixed (prologue + epilogue) vs per-K-tile cost: time M x N x K for a K sweep at fixed
-M, N (Cb bf16 output) and fit t(K) = f + K/64 * t_k per tile wave; hipBLASLt alongside."""
+M, N (Cb bf16 output) and fit t(K) = f + K/64 * t_k per tile wave; hipBLASLt alongside.
+
+    python tools/nt_ksweep.py [variant ...]      (default: 2 3)"""
 import sys, time
 import torch
 sys.path.insert(0, ".")
@@ -23,7 +25,10 @@ def bench(fn, n=30):
     return e0.elapsed_time(e1) / n * 1e-3
 
 
-for (M, N) in [(16384, 4096), (8192, 8192)]:
+variants = [int(v) for v in sys.argv[1:]] or [2, 3]
+for var, (M, N) in [(v, mn) for mn in [(16384, 4096), (8192, 8192)] for v in variants]:
+    m.gemm_nt_set_variant(var)
+    print(f"-- variant {var}", flush=True)
     Kmax = 8192
     A = (torch.rand(M, Kmax, device=dev) * 2 - 1).to(torch.bfloat16)
     B = (torch.rand(N, Kmax, device=dev) * 2 - 1).to(torch.bfloat16)

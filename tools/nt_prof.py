@@ -5,7 +5,7 @@ sys.path.insert(0, ".")
 from fedmi.ops import native
 
 M, N, K = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (16384, 4096, 4096)))
-v = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+v = int(sys.argv[4]) if len(sys.argv) > 4 else 3
 m = native()
 dev = torch.device("cuda", 0)
 s = torch.cuda.current_stream().cuda_stream

@@ -35,7 +35,7 @@ for (M, N, K) in [(16384, 4096, 4096), (4096, 4096, 16384), (8192, 8192, 8192)]:
         err = ((Cb.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
         line += f" | v{v} {dt*1e3:.3f} ms {2*M*N*K/dt/1e12:.0f} TF/s err {err:.1e}"
     print(line, flush=True)
-m.gemm_nt_set_variant(2)
+m.gemm_nt_set_variant(3)
 
 X, y = make_income_like(4096, seed=0)
 Xt = torch.as_tensor(X, device=dev); yt = torch.as_tensor(y, device=dev)
