@@ -552,12 +552,15 @@ def _split_bf16_reference_grad(flat, X, y, dims):
 def test_bf16_train_kernel_gradient(R):
     """The slab-reduced gradient of ONE fl_train_bf16 launch vs (a) a float64 host model of the
     kernel's own arithmetic (split-bf16 forward, bf16 backward operands): rel. err <= 1e-3 per
-    tensor, and (b) fp32 torch autograd of the exact model: rel. err <= 1e-2 per tensor."""
+    tensor, and (b) fp32 torch autograd of the exact model: rel. err <= 1e-2 per tensor.  R = 16
+    runs the conflict-free LDS layout (level 2: W row gaps), R = 32 the compact one (level 1:
+    swizzled W chunks) -- fl_common.h."""
     X, y = make_income_like(4000, seed=21)
     dims = DIMS
     flat = init_flat(dims, 8)
     e = HipRoundEngine(X, y, 2, EngineConfig(max_rounds=4, early_stop=False, rows_per_block=R, dtype="bf16",
                                              graph_rounds=0), None, flat)
+    assert e.engine.layout()["bank_level"] == (2 if R == 16 else 1)
     e.step_train()
     e.stream.synchronize()
     P = e.P
