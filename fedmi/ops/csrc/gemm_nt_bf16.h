@@ -13,6 +13,7 @@ struct NTArgs {
     const void* mask; int ldmask;  // optional bf16 [M][ldmask]: out = mask > 0 ? v : 0
     int relu;
     float alpha, beta;
+    unsigned long long* dbg;    // optional [blocks][8] s_memrealtime phase stamps (profiling; full-line loop)
 };
 
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s);
@@ -28,3 +29,5 @@ hipError_t skinny_wgrad_launch(const void* W, int ldw, int Nw, const void* S, in
                                int splits, float* slab, float* out, float beta, float* bias_out, hipStream_t s);
 // 0 = single-buffered two-barrier main loop, 1 = double-buffered (default)
 void gemm_nt_set_variant(int v);
+// phase stamps of the next launches (tools/nt_stamps.py); nullptr = off
+void gemm_nt_set_debug(unsigned long long* dbg);

@@ -415,6 +415,9 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
 __global__ void __launch_bounds__(NT2_THREADS)
 gemm_nt_bf16_fl_kernel(NTArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
+#define NT_STAMP(i)                                                                              \
+    if (g.dbg != nullptr && threadIdx.x == 0) g.dbg[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
+    NT_STAMP(0);
     const int mt = g.M / NT2_BM, nt = g.N / NT2_BM;
     const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
     constexpr int GM = 8;  // grouped tile order (variant 2)
@@ -477,6 +480,7 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
     }
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();
+    NT_STAMP(1);
 
     auto phase = [&](int kt, int r, bool tail) {
         const char* buf = smem + (kt & 1) * 65536;
@@ -538,6 +542,7 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
         phase(kt, 2, false);
         phase(kt, 3, false);
     }
+    NT_STAMP(2);
     for (; kt < KT; ++kt) {
         phase(kt, 0, true);
         phase(kt, 1, true);
@@ -545,13 +550,21 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
         phase(kt, 3, true);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
+    NT_STAMP(3);
     pp_epilogue(g, smem, acc, m0, n0, w, l);
+    if (g.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    NT_STAMP(4);
+#undef NT_STAMP
 }
 
 static int g_nt_variant = 3;  // 3: full-line 256x256 loop (default), 2: half-line, 1/0: 128x128
 void gemm_nt_set_variant(int v) { g_nt_variant = v; }
+static unsigned long long* g_nt_dbg = nullptr;
+void gemm_nt_set_debug(unsigned long long* dbg) { g_nt_dbg = dbg; }
 
-hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s) {
+hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
+    NTArgs g = g_in;
+    if (g.dbg == nullptr) g.dbg = g_nt_dbg;
     if (g.M % NT_BM || g.N % NT_BN || g.K % NT_BK || g.lda % 8 || g.ldb % 8) return hipErrorInvalidValue;
     if (g_nt_variant == 2 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
         (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&

@@ -418,6 +418,7 @@ void register_trainer(py::module_& m) {
     m.def("skinny_wgrad", &skinny_wgrad_py);
     m.def("gemm_nt", &gemm_nt_py);
     m.def("gemm_nt_set_variant", &gemm_nt_set_variant);
+    m.def("gemm_nt_set_debug", [](uintptr_t p) { gemm_nt_set_debug(reinterpret_cast<unsigned long long*>(p)); });
     m.def("transpose_bf16", &transpose_bf16_py);
     m.def("rowsum_bf16", &rowsum_bf16_py);
     m.def("pad_bf16", &pad_bf16_py);
