@@ -194,10 +194,34 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :
 
 // Epilogue of the 256x256 loops (ping-pong and full-line): the block's 256x256 bf16 output tile is
 // staged through the (now free) 128 KiB of LDS; see the comment inside.
+// Output configuration of an epilogue as compile-time flags (NT_EPI_*), so the unrolled
+// 128-element epilogue carries no per-element runtime branches or dead paths; -1 = read the
+// configuration from the arguments at run time.
+#define NT_EPI_C 1
+#define NT_EPI_CB 2
+#define NT_EPI_CBT 4
+#define NT_EPI_MASK 8
+#define NT_EPI_RELU 16
+#define NT_EPI_BIAS 32
+#define NT_EPI_BETA 64
+static inline int nt_epi_flags(const NTArgs& g) {
+    return (g.C != nullptr ? NT_EPI_C : 0) | (g.Cbf16 != nullptr ? NT_EPI_CB : 0) | (g.CbT != nullptr ? NT_EPI_CBT : 0) |
+           (g.mask != nullptr ? NT_EPI_MASK : 0) | (g.relu ? NT_EPI_RELU : 0) | (g.bias != nullptr ? NT_EPI_BIAS : 0) |
+           (g.C != nullptr && g.beta != 0.f ? NT_EPI_BETA : 0);
+}
+
+template <int F>
 __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (&acc)[8][4], int m0, int n0, int w,
                                             int l) {
     const int wr = w >> 2, wc = w & 3;
     const int lr = l & 15, lg = l >> 4;
+    const bool hC = F < 0 ? g.C != nullptr : (F & NT_EPI_C) != 0;
+    const bool hCb = F < 0 ? g.Cbf16 != nullptr : (F & NT_EPI_CB) != 0;
+    const bool hCbT = F < 0 ? g.CbT != nullptr : (F & NT_EPI_CBT) != 0;
+    const bool hMask = F < 0 ? g.mask != nullptr : (F & NT_EPI_MASK) != 0;
+    const bool hRelu = F < 0 ? g.relu != 0 : (F & NT_EPI_RELU) != 0;
+    const bool hBias = F < 0 ? g.bias != nullptr : (F & NT_EPI_BIAS) != 0;
+    const bool hBeta = F < 0 ? g.beta != 0.f : (F & NT_EPI_BETA) != 0;
 
     // Epilogue.  Every wave's LDS reads retired before that last barrier, so the 128 KiB of LDS
     // now holds the block's 256x256 bf16 output tile as 512-byte rows whose 16-byte chunk index
@@ -211,7 +235,7 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     auto tile_off = [&](int row, int col) { return row * 512 + ((((col >> 3) ^ sw(row))) << 4) + (col & 7) * 2; };
     __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(g.Cbf16);
     __hip_bfloat16* CbT = reinterpret_cast<__hip_bfloat16*>(g.CbT);
-    if (g.mask != nullptr) {
+    if (hMask) {
         const __hip_bfloat16* Mk = reinterpret_cast<const __hip_bfloat16*>(g.mask);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -225,7 +249,7 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
         const int cl = wc * 64 + 16 * y + lr, n = n0 + cl;
-        const float bv = g.bias != nullptr ? g.bias[n] : 0.f;
+        const float bv = hBias ? g.bias[n] : 0.f;
 #pragma unroll
         for (int x = 0; x < 8; ++x) {
             uint32_t tp[2];  // the lane's 4 consecutive rows of column n, packed for CbT
@@ -234,26 +258,26 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
                 const int rl = wr * 128 + 16 * x + 4 * lg + j, mm = m0 + rl;
                 __hip_bfloat16* slot = reinterpret_cast<__hip_bfloat16*>(smem + tile_off(rl, cl));
                 float v = acc[x][y][j] * g.alpha + bv;
-                if (g.relu) v = fmaxf(v, 0.f);
-                if (g.mask != nullptr) v = __bfloat162float(*slot) > 0.f ? v : 0.f;
-                if (g.C != nullptr) {
+                if (hRelu) v = fmaxf(v, 0.f);
+                if (hMask) v = __bfloat162float(*slot) > 0.f ? v : 0.f;
+                if (hC) {
                     float* cp = g.C + (size_t)mm * g.ldc + n;
-                    if (g.beta != 0.f) v += g.beta * *cp;
+                    if (hBeta) v += g.beta * *cp;
                     *cp = v;
                 }
                 const __hip_bfloat16 hv = __float2bfloat16(v);
-                if (Cb != nullptr) *slot = hv;
+                if (hCb) *slot = hv;
                 const uint32_t hb = __bfloat16_as_ushort(hv);
                 if (j & 1) tp[j >> 1] |= hb << 16;
                 else tp[j >> 1] = hb;
             }
-            if (CbT != nullptr) {  // 8-byte store: rows mm .. mm+3 are contiguous in CbT's row n
+            if (hCbT) {  // 8-byte store: rows mm .. mm+3 are contiguous in CbT's row n
                 const size_t off = (size_t)n * g.ldct + m0 + wr * 128 + 16 * x + 4 * lg;
                 *reinterpret_cast<uint2*>(CbT + off) = make_uint2(tp[0], tp[1]);
             }
         }
     }
-    if (Cb != nullptr) {
+    if (hCb) {
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -386,7 +410,7 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
         phase(4 * kt + 3, 3, true);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
-    pp_epilogue(g, smem, acc, m0, n0, w, l);
+    pp_epilogue<-1>(g, smem, acc, m0, n0, w, l);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -412,6 +436,7 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
 // read.  Waits (before a phase's first barrier, retiring what the NEXT phase reads; pieces still
 // allowed in flight, in issue order): r = 0: 4 (B01, B23 of u+1) | r = 3: 4 (A m1 of u+1, B01 of
 // u+2) | r = 1, 2: none.
+template <int F>
 __global__ void __launch_bounds__(NT2_THREADS)
 gemm_nt_bf16_fl_kernel(NTArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
@@ -551,9 +576,8 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
     NT_STAMP(3);
-    pp_epilogue(g, smem, acc, m0, n0, w, l);
-    if (g.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    NT_STAMP(4);
+    pp_epilogue<F>(g, smem, acc, m0, n0, w, l);
+    NT_STAMP(4);  // output stores issued (not waited for)
 #undef NT_STAMP
 }
 
@@ -579,7 +603,19 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
         (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
         (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
-        hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
+        // the output configurations of the wide client's GEMMs get their own instantiation
+        switch (nt_epi_flags(g)) {
+#define NT_FL_CASE(F) \
+    case F: hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel<F>, dim3(blocks), dim3(NT2_THREADS), 0, s, g); break;
+            NT_FL_CASE(NT_EPI_CB)                                                  // plain bf16 output
+            NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_BIAS | NT_EPI_RELU)         // hidden-layer forward
+            NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK)                       // dgrad (ReLU mask)
+            NT_FL_CASE(NT_EPI_C)                                                   // fp32 output
+            NT_FL_CASE(NT_EPI_C | NT_EPI_BETA)                                     // accumulating wgrad
+            NT_FL_CASE(NT_EPI_C | NT_EPI_BIAS)                                     // fp32 logits
+#undef NT_FL_CASE
+            default: hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel<-1>, dim3(blocks), dim3(NT2_THREADS), 0, s, g); break;
+        }
         return hipGetLastError();
     }
     const int blocks = (g.M / NT_BM) * (g.N / NT_BN);

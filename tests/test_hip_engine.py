@@ -324,6 +324,40 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     assert ((outs[1][0] - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
+@pytest.mark.parametrize("cfg", ["Cb", "Cb+CbT+bias+relu", "Cb+CbT+mask", "C", "C+beta", "C+bias"])
+def test_gemm_nt_bf16_epilogue_configs(cfg):
+    """Every output configuration the full-line loop compiles separately (wide forward, dgrad,
+    wgrad, logits, plain) is bit-identical to the 128x128 loop's runtime-configured epilogue."""
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    M, N, K = 512, 768, 320
+    torch.manual_seed(7)
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    B = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    mask = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    C0 = torch.randn(M, N, device=dev)
+    outs = []
+    try:
+        for v in (1, 3):
+            m.gemm_nt_set_variant(v)
+            C = C0.clone()
+            Cb = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+            CbT = torch.zeros(N, M, dtype=torch.bfloat16, device=dev)
+            has = lambda k: k in cfg.split("+")
+            m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, C.data_ptr() if has("C") else 0, N,
+                      Cb.data_ptr() if has("Cb") else 0, N, CbT.data_ptr() if has("CbT") else 0, M,
+                      bias.data_ptr() if has("bias") else 0, mask.data_ptr() if has("mask") else 0, N,
+                      1 if has("relu") else 0, 1.0, 0.5 if has("beta") else 0.0, s)
+            torch.cuda.synchronize()
+            outs.append((C, Cb, CbT))
+    finally:
+        m.gemm_nt_set_variant(3)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("M,N,beta", [(16384, 2, 0.0), (5000, 14, 1.0), (300, 50, 0.5), (700, 100, 1.0)])
 def test_colsum_vs_torch(M, N, beta):
     """Bias-gradient column sums (flat few-column kernel for N <= 64, wave-per-64-columns otherwise)."""
