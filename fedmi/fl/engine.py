@@ -76,6 +76,12 @@ class EngineConfig:
     # last round of every run() evaluates itself (fl_common.h FL_EVAL_LAGGED).  Metrics,
     # history, early-stop round and weights are identical to classic rounds.
     lagged_eval: bool = True
+    # bf16 fused kernels: storage of the per-workgroup gradient partials reduced by the Adam
+    # kernel -- 'fp16' (half the slab traffic; partial SUMS of the unscaled gradient, 1/n applied
+    # after the fp32 reduction, saturating at +-65504), 'fp32', or 'auto' = fp16 when every
+    # |feature| <= FP16_SLAB_MAX_ABS_X (standardised data: a partial over R <= 64 rows stays far
+    # inside fp16's range), else fp32.  The fp32 kernels always use an fp32 slab.
+    grad_slab: str = "auto"
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -88,6 +94,10 @@ def _metric_mode_id(mode: str) -> int:
     if mode not in ("mean", "pooled"):
         raise ValueError(f"metric_mode must be 'mean' or 'pooled', got {mode!r}")
     return 0 if mode == "mean" else 1
+
+
+# grad_slab='auto': the largest |feature| for which the bf16 kernels use fp16 gradient partials
+FP16_SLAB_MAX_ABS_X = 64.0
 
 
 def _dtype_id(dtype: str) -> int:
@@ -524,6 +534,7 @@ class HipRoundEngine(RoundEngineBase):
             "eval_fedavg": bool(cfg.eval_fedavg),
             "lagged_eval": self._lag,
             "emulate_clients": bool(emulate_clients),
+            "slab_f16": self._pick_slab_f16(cfg),
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),
@@ -546,6 +557,7 @@ class HipRoundEngine(RoundEngineBase):
                     raise
         self.R = R
         self.layout = self.engine.layout()
+        self.slab_f16 = bool(self.layout["slab_f16"])
         iw, ib, _ = image_layout(self.dims)
         if (self.layout["Pimg"], list(self.layout["iw_off"]), list(self.layout["ib_off"])) != (self.Pimg, iw, ib):
             raise RuntimeError(f"image layout mismatch between C++ and Python: {self.layout}")
@@ -567,6 +579,15 @@ class HipRoundEngine(RoundEngineBase):
             if self._peer is not None:
                 self.engine.attach_peer(self._peer)
         self._graph_ready = False
+
+    def _pick_slab_f16(self, cfg) -> bool:
+        if cfg.grad_slab not in ("auto", "fp16", "fp32"):
+            raise ValueError(f"grad_slab must be 'auto', 'fp16' or 'fp32', got {cfg.grad_slab!r}")
+        if cfg.dtype != "bf16" or cfg.grad_slab == "fp32":
+            return False
+        if cfg.grad_slab == "fp16":
+            return True
+        return bool(self.X.numel() == 0 or float(self.X.abs().max()) <= FP16_SLAB_MAX_ABS_X)
 
     def _round_tables(self, client_sizes=None):
         """Host-built device tables (fl_common.h FLBuffers::sched / rtab): per optimizer-step

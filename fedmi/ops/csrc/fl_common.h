@@ -130,6 +130,8 @@ struct FLConfig {
     float agg_scale;    // n_rank / N_total (sample-size-weighted FedAvg, C:110-116)
     int slab_stride;    // floats per slab row (dense P + loss slot, padded)
     int n_slabs;        // workgroups of the train kernel = ceil(n_rows / R)
+    int slab_f16;       // bf16 kernels: the slab holds fp16 partial SUMS (the 1/n is applied by
+                        // Adam after the fp32 reduction; fl_device.h slab_store_h)
     int tail_off;       // == Pimg: start of the per-rank metric tail in the comm buffer
     int tail_stride;    // C*C confusion counts + 1 loss slot
     int tail_len;       // world * tail_stride
@@ -175,7 +177,8 @@ struct FLState {
 struct FLBuffers {
     const float* X;     // [n_rows, dim0] row-major, device resident
     const int* y;       // [n_rows]
-    float* slab;        // [n_slabs, slab_stride] dense gradient partials
+    float* slab;        // [n_slabs, slab_stride] dense gradient partials (fp32; slab_f16: fp16 in the
+                        // first P halves of each row, the loss partial stays the fp32 at [P])
     float* local;       // [Pimg] post-step local weights (evaluated, C:148)
     float* m;           // [Pimg] Adam exp_avg
     float* v;           // [Pimg] Adam exp_avg_sq

@@ -34,6 +34,18 @@ __device__ __forceinline__ void slab_store(float* p, float v) {
 #endif
 }
 
+// fp16 slab of the bf16 kernels: per-workgroup partial sums of the UNscaled gradient (deltas
+// p - onehot, not (p - onehot) / n: |partial| <= rows x max|activation|, far inside fp16's range
+// for these models; clamped so an outlier saturates instead of becoming inf), rounded to fp16
+// (11 significant bits -- finer than the bf16 operands the partials are computed from) and
+// summed in fp32 by the Adam kernel, which applies the 1/n.  Half the bytes of the fp32 slab,
+// which is written and read back once per round.
+__device__ __forceinline__ void slab_store_h(uint16_t* p, float v) {
+    const float c = fminf(fmaxf(v, -65504.f), 65504.f);
+    const _Float16 h = (_Float16)c;
+    __builtin_nontemporal_store(*reinterpret_cast<const uint16_t*>(&h), p);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -152,6 +152,8 @@ class FLEngine {
         c_.agg_scale = cfg["agg_scale"].cast<float>();
         c_.slab_stride = ((d_.P + 1) + 3) & ~3;
         c_.n_slabs = (c_.n_rows + c_.R - 1) / c_.R;
+        // bf16 kernels: fp16 gradient partials unless the caller asks for fp32 (engine.py grad_slab)
+        c_.slab_f16 = dtype_ == 1 && (cfg.contains("slab_f16") ? cfg["slab_f16"].cast<bool>() : true) ? 1 : 0;
         c_.tail_off = d_.Pimg;
         c_.tail_stride = C * C + 1;
         c_.tail_len = c_.world * c_.tail_stride;
@@ -472,6 +474,7 @@ class FLEngine {
         o["dtype"] = dtype_;
         o["slab_stride"] = c_.slab_stride;
         o["n_slabs"] = c_.n_slabs;
+        o["slab_f16"] = c_.slab_f16;
         o["tail_off"] = c_.tail_off;
         o["tail_stride"] = c_.tail_stride;
         o["tail_len"] = c_.tail_len;

@@ -435,6 +435,7 @@ __device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& 
         float g = 0.f;
 #pragma unroll
         for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
+        if (c.slab_f16) g *= c.inv_n;  // fp16 slab: partial sums of the unscaled gradient
         if (c.weight_decay != 0.f) g += c.weight_decay * p;
         if (c.prox_mu != 0.f) g += c.prox_mu * (p - anc);
         // torch.optim.Adam single-tensor path: scalars in double, rounded to fp32 once;
@@ -627,27 +628,33 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     }
     float g = 0.f;
     bool have_state = false;
-    {
-        const float* sp = b.slab + (valid ? di : 0);
-        for (int s0 = wave; s0 < c.n_slabs; s0 += ADAM_WAVES * ADAM_DEPTH) {
-            float x[ADAM_DEPTH];
-#pragma unroll
-            for (int u = 0; u < ADAM_DEPTH; ++u) {
-                const int s = s0 + u * ADAM_WAVES;
-                // unpredicated; non-temporal: the slab is read once
-                const float v = __builtin_nontemporal_load(&sp[(size_t)(s < c.n_slabs ? s : 0) * c.slab_stride]);
-                x[u] = s < c.n_slabs ? v : 0.f;
-            }
-            if (!have_state) {
-                have_state = true;
-                FL_STAMP(1);
-                round_state();
-                FL_STAMP(2);
-            }
-#pragma unroll
-            for (int u = 0; u < ADAM_DEPTH; ++u) g += x[u];
-        }
+    // the slab rows of this block's 64 parameters, 16 rows in flight per lane; the element type
+    // is hoisted out of the loop (a per-element select on it would serialise the loads)
+#define FL_SLAB_REDUCE(LOAD)                                                                        \
+    for (int s0 = wave; s0 < c.n_slabs; s0 += ADAM_WAVES * ADAM_DEPTH) {                          \
+        float x[ADAM_DEPTH];                                                                        \
+        _Pragma("unroll") for (int u = 0; u < ADAM_DEPTH; ++u) {                                    \
+            const int s = s0 + u * ADAM_WAVES;                                                      \
+            const size_t row = (size_t)(s < c.n_slabs ? s : 0) * c.slab_stride;                     \
+            const float v = LOAD; /* unpredicated; non-temporal: the slab is read once */           \
+            x[u] = s < c.n_slabs ? v : 0.f;                                                         \
+        }                                                                                           \
+        if (!have_state) {                                                                          \
+            have_state = true;                                                                      \
+            FL_STAMP(1);                                                                            \
+            round_state();                                                                          \
+            FL_STAMP(2);                                                                            \
+        }                                                                                           \
+        _Pragma("unroll") for (int u = 0; u < ADAM_DEPTH; ++u) g += x[u];                           \
     }
+    if (c.slab_f16) {
+        const _Float16* sph = reinterpret_cast<const _Float16*>(b.slab) + (valid ? di : 0);
+        FL_SLAB_REDUCE((float)__builtin_nontemporal_load(&sph[2 * row]))
+    } else {
+        const float* sp = b.slab + (valid ? di : 0);
+        FL_SLAB_REDUCE(__builtin_nontemporal_load(&sp[row]))
+    }
+#undef FL_SLAB_REDUCE
     if (!have_state) round_state();
     FL_STAMP(3);
     part[wave][lane] = g;

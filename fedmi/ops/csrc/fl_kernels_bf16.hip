@@ -275,11 +275,16 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
     }
 }
 
-// dW_l[o][i] = sum_r D_{l+1}[r][o] act_l[r][i] (fp32 -> slab, dense [N][K]);
-// gb_l[o] = sum_r D_{l+1}[r][o].  Both operands are read transposed (K = rows).
-template <int RT>
-__device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, const char* lds,
-                                 float* __restrict__ gW, float* __restrict__ gb) {
+// dW_l[o][i] = sum_r D_{l+1}[r][o] act_l[r][i] (fp32 accumulate -> slab, dense [N][K]);
+// gb_l[o] = sum_r D_{l+1}[r][o].  Both operands are read transposed (K = rows).  F16: the slab
+// holds fp16 partials (element e at half e of the row, fl_device.h slab_store_h), else fp32.
+template <bool F16>
+__device__ __forceinline__ void slab_put(float* slab, int idx, float v) {
+    if (F16) slab_store_h(reinterpret_cast<uint16_t*>(slab) + idx, v);
+    else slab_store(slab + idx, v);
+}
+template <int RT, bool F16>
+__device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, const char* lds, float* __restrict__ slab) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4, lq = lr >> 2, lp = lr & 3;
     const int K = d.dim[l], N = d.dim[l + 1];
@@ -310,7 +315,7 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int o = ot * 16 + 4 * lg + j;
-            if (i < K && o < N) slab_store(&gW[o * K + i], acc[j]);
+            if (i < K && o < N) slab_put<F16>(slab, d.w_off[l] + o * K + i, acc[j]);
         }
     }
     const uint16_t* Dh = reinterpret_cast<const uint16_t*>(D);
@@ -321,7 +326,7 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
             s0 += bf16_to_f32(Dh[r * ldd + o]);
             s1 += bf16_to_f32(Dh[(r + 1) * ldd + o]);
         }
-        slab_store(&gb[o], s0 + s1);
+        slab_put<F16>(slab, d.b_off[l] + o, s0 + s1);
     }
 }
 
@@ -526,7 +531,9 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     }
     FL_STAMP(2);
 
-    // softmax cross-entropy (mean over the shard): D_L = (softmax - onehot) / n, bf16.
+    // softmax cross-entropy: D_L = softmax - onehot, bf16, times the mean's 1/n -- except with
+    // the fp16 slab, whose partials are sums of the unscaled gradient (the 1/n is applied by the
+    // Adam kernel after its fp32 reduction, so small gradients keep fp16's normal range).
     // Fused evaluation: the same logits score the previous round's model (argmax).
     const float* z = reinterpret_cast<const float*>(lds + e.logit_off);
     uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
@@ -556,7 +563,8 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
             lossv = (lse - zr[y]) * c.inv_n;
             for (int k = 0; k < C; ++k) {
                 const float p = __expf(zr[k] - mx) * inv_se;
-                dr[k] = (uint16_t)bf16_bits((p - (k == y ? 1.f : 0.f)) * c.inv_n);
+                const float dk = p - (k == y ? 1.f : 0.f);
+                dr[k] = (uint16_t)bf16_bits(c.slab_f16 ? dk : dk * c.inv_n);
             }
         } else {
             for (int k = 0; k < C; ++k) dr[k] = 0;
@@ -574,7 +582,8 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
 
     // backward, top layer first, one phase per layer (wgrad_l and dgrad_l are independent)
     for (int l = L - 1; l >= 0; --l) {
-        wgrad_layer_bf16<RT>(d, e, l, lds, slab + d.w_off[l], slab + d.b_off[l]);
+        if (c.slab_f16) wgrad_layer_bf16<RT, true>(d, e, l, lds, slab);
+        else wgrad_layer_bf16<RT, false>(d, e, l, lds, slab);
         if (l > 0) dgrad_layer_bf16<RT>(d, e, l, lds);
         lds_barrier();
         FL_STAMP(4 + (L - 1 - l));

@@ -108,3 +108,20 @@ def test_train_and_evaluate_early_stop_arguments_take_effect(backend):
     assert h["stop_round"] == stop == h["rounds_run"]
     with pytest.raises(RuntimeError):
         tr.train_and_evaluate(rounds=130, termination_patience=4, verbose=False)
+
+
+def test_grad_slab_selection_rule():
+    """EngineConfig.grad_slab: 'auto' chooses fp16 gradient partials for the bf16 kernels only
+    while every |feature| <= FP16_SLAB_MAX_ABS_X; fp32 kernels never; bad values are refused."""
+    from types import SimpleNamespace
+    from fedmi.fl.engine import FP16_SLAB_MAX_ABS_X, HipRoundEngine
+    pick = HipRoundEngine._pick_slab_f16
+    small = SimpleNamespace(X=torch.full((4, 3), FP16_SLAB_MAX_ABS_X))
+    big = SimpleNamespace(X=torch.full((4, 3), -2 * FP16_SLAB_MAX_ABS_X))
+    assert pick(small, EngineConfig(dtype="bf16"))
+    assert not pick(big, EngineConfig(dtype="bf16"))
+    assert pick(big, EngineConfig(dtype="bf16", grad_slab="fp16"))
+    assert not pick(small, EngineConfig(dtype="bf16", grad_slab="fp32"))
+    assert not pick(small, EngineConfig(dtype="fp32", grad_slab="fp16"))
+    with pytest.raises(ValueError):
+        pick(small, EngineConfig(dtype="bf16", grad_slab="bf16"))

@@ -489,6 +489,29 @@ def test_bf16_engine_tracks_fp32_oracle(R, hidden):
     assert abs(hb.history()["loss"][-1] - ref.history()["loss"][-1]) < 0.02
 
 
+def test_bf16_grad_slab_auto_and_formats_agree():
+    """grad_slab='auto' picks the fp16 slab for standardised features and the fp32 slab when a
+    feature exceeds FP16_SLAB_MAX_ABS_X (a partial sum could saturate fp16); 40 rounds with either
+    slab land on the same accuracy and loss."""
+    from fedmi.fl.engine import FP16_SLAB_MAX_ABS_X
+    X, y = make_income_like(3000, seed=5)
+    flat = init_flat(DIMS, 3)
+    mk = lambda X, **kw: HipRoundEngine(X, y, 2, EngineConfig(max_rounds=40, early_stop=False, dtype="bf16",
+                                                              **kw), None, flat)
+    auto = mk(X)
+    assert auto.slab_f16
+    big = X.copy()
+    big[0, 0] = 2 * FP16_SLAB_MAX_ABS_X
+    assert not mk(big).slab_f16
+    assert not mk(X, grad_slab="fp32").slab_f16
+    f32 = mk(X, grad_slab="fp32")
+    auto.run(40)
+    f32.run(40)
+    ha, hf = auto.history(), f32.history()
+    assert abs(ha["global"][-1, 0] - hf["global"][-1, 0]) < 0.01
+    assert abs(ha["loss"][-1] - hf["loss"][-1]) < 0.01
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_fused_eval_equals_classic_rounds(dtype):
     """One client: scoring round r inside round r+1's train kernel (fused evaluation) gives
@@ -549,7 +572,7 @@ def _bf(x):
     return x.to(torch.bfloat16).to(torch.float64)
 
 
-def _split_bf16_reference_grad(flat, X, y, dims):
+def _split_bf16_reference_grad(flat, X, y, dims, scaled_delta=False):
     """Host model of the bf16 train kernel's arithmetic (fl_kernels_bf16.hip), in float64:
     split-bf16 forward (hi.hi + lo.hi + hi.lo, hidden outputs split into hi/lo after ReLU),
     softmax-CE deltas rounded to bf16, backward on the hi parts with bf16 deltas."""
@@ -572,35 +595,44 @@ def _split_bf16_reference_grad(flat, X, y, dims):
     p = torch.softmax(z, 1)
     dz = p.clone()
     dz[torch.arange(n), yt] -= 1.0
-    dz = _bf(dz / n)
+    # fp16 slab: the kernels back-propagate the unscaled delta (Adam applies the 1/n); fp32
+    # slab: the delta of the mean loss
+    sc = 1.0 if scaled_delta else float(n)
+    dz = _bf(dz / n) if scaled_delta else _bf(dz)
     gW, gb = [None] * L, [None] * L
     for l in range(L - 1, -1, -1):
-        gW[l] = dz.T @ his[l]
-        gb[l] = dz.sum(0)
+        gW[l] = dz.T @ his[l] / sc
+        gb[l] = dz.sum(0) / sc
         if l:
             dz = _bf((dz @ _bf(Ws[l])) * (his[l] > 0))
     return torch.cat([torch.cat([gW[l].reshape(-1), gb[l]]) for l in range(L)]).numpy()
 
 
-@pytest.mark.parametrize("R", [16, 32])
-def test_bf16_train_kernel_gradient(R):
-    """The slab-reduced gradient of ONE fl_train_bf16 launch vs (a) a float64 host model of the
-    kernel's own arithmetic (split-bf16 forward, bf16 backward operands): rel. err <= 1e-3 per
-    tensor, and (b) fp32 torch autograd of the exact model: rel. err <= 1e-2 per tensor.  R = 16
-    runs the conflict-free LDS layout (level 2: W row gaps), R = 32 the compact one (level 1:
-    swizzled W chunks) -- fl_common.h."""
+@pytest.mark.parametrize("R,slab", [(16, "fp16"), (32, "fp16"), (32, "fp32")])
+def test_bf16_train_kernel_gradient(R, slab):
+    """The slab-reduced gradient of ONE fl_train_bf16 launch (reduced here in float64) vs (a) a
+    float64 host model of the kernel's own arithmetic (split-bf16 forward, bf16 backward
+    operands): rel. err <= 1e-3 per tensor, and (b) fp32 torch autograd of the exact model: rel.
+    err <= 1e-2 per tensor.  R = 16 runs the conflict-free LDS layout (level 2: W row gaps),
+    R = 32 the compact one (level 1: swizzled W chunks) -- fl_common.h.  slab fp16: partial sums
+    of the unscaled gradient (the Adam kernel applies the 1/n); fp32: partials of the mean."""
     X, y = make_income_like(4000, seed=21)
     dims = DIMS
     flat = init_flat(dims, 8)
     e = HipRoundEngine(X, y, 2, EngineConfig(max_rounds=4, early_stop=False, rows_per_block=R, dtype="bf16",
-                                             graph_rounds=0), None, flat)
+                                             graph_rounds=0, grad_slab=slab), None, flat)
     assert e.engine.layout()["bank_level"] == (2 if R == 16 else 1)
     e.step_train()
     e.stream.synchronize()
     P = e.P
-    stride = int(e.engine.layout()["slab_stride"])
-    g = e.slab.view(-1, stride)[:, :P].double().sum(0).cpu().numpy()
-    ref = _split_bf16_reference_grad(flat, X, y, dims)
+    lay = e.engine.layout()
+    stride = int(lay["slab_stride"])
+    assert lay["slab_f16"] == (slab == "fp16") == e.slab_f16
+    if slab == "fp16":
+        g = e.slab.view(torch.float16).view(-1, 2 * stride)[:, :P].double().sum(0).cpu().numpy() / len(X)
+    else:
+        g = e.slab.view(-1, stride)[:, :P].double().sum(0).cpu().numpy()
+    ref = _split_bf16_reference_grad(flat, X, y, dims, scaled_delta=slab == "fp32")
     model = TorchRoundEngine(X, y, 2, EngineConfig(max_rounds=2), None, flat)
     out = model.model(torch.as_tensor(X))
     torch.nn.functional.cross_entropy(out, torch.as_tensor(y, dtype=torch.long)).backward()

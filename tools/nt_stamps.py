@@ -1,5 +1,5 @@
 """In-kernel phase stamps (s_memrealtime, 100 MHz) of the full-line NT GEMM: per block, start ->
-prologue landed -> steady main loop done -> last two K-tiles done -> epilogue stores retired,
+prologue landed -> steady main loop done -> last two K-tiles done -> epilogue stores issued,
 plus the gap between a block's end and the next block's start on the same slot.
 
     python tools/nt_stamps.py [M N K]
@@ -29,14 +29,25 @@ m.gemm_nt_set_debug(dbg.data_ptr())
 run()
 torch.cuda.synchronize()
 m.gemm_nt_set_debug(0)
-st = dbg.view(nb, 8).cpu().numpy()[:, :5].astype(np.int64)
+st_all = dbg.view(nb, 8).cpu().numpy().astype(np.int64)
+st = st_all[:, :5]
 t0 = st[:, 0].min()
 us = (st - t0) * 0.01
 print(f"{M}x{N}x{K}: {nb} blocks, kernel span {us[:, 4].max():.1f} us (stamps)")
-names = ["prologue (start -> first K-tile landed)", "steady main loop", "last two K-tiles", "epilogue"]
+names = ["prologue (start -> first K-tile landed)", "steady main loop", "last two K-tiles",
+         "epilogue (until the stores are issued)"]
+order = np.argsort(us[:, 0])
+first = np.zeros(nb, bool)
+first[order[:min(256, nb)]] = True
 for i, nm in enumerate(names):
     d = us[:, i + 1] - us[:, i]
-    print(f"  {nm:42s} median {np.median(d):7.2f} us  p10 {np.percentile(d, 10):7.2f}  p90 {np.percentile(d, 90):7.2f}")
+    print(f"  {nm:42s} median {np.median(d):7.2f} us  p10 {np.percentile(d, 10):7.2f}  p90 {np.percentile(d, 90):7.2f}"
+          f"  | first wave {np.median(d[first]):7.2f}, later {np.median(d[~first]) if (~first).any() else 0:7.2f}")
+if (st_all[:, 5] > 0).all():
+    e = (st_all[:, [3, 5, 6, 4]] - t0) * 0.01
+    for nm, a, b in (("  epilogue: values into the LDS tile", 0, 1), ("  epilogue: barrier", 1, 2),
+                     ("  epilogue: LDS reads + global stores issued", 2, 3)):
+        print(f"  {nm:42s} median {np.median(e[:, b] - e[:, a]):7.2f} us")
 # slot reuse: sort blocks by start; the k-th block of wave w+1 starts after some block of wave w ends
 starts = np.sort(us[:, 0])
 ends = np.sort(us[:, 4])
