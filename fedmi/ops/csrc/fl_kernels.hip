@@ -424,8 +424,9 @@ __device__ __forceinline__ void pack_store(char* img, int pk, bool is_bias, int 
 
 // Adam step of one parameter (wave 0 lane of fl_adam_kernel) from the block's partial sums.
 // `p`, `m`, `v`, `anc`: the parameter, its Adam moments and its anchor value, loaded by the
-// caller at the start of the kernel (their latency hides behind the slab loads).
-__device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& b, float* __restrict__ comm,
+// caller at the start of the kernel (their latency hides behind the slab loads).  Returns the
+// FedAvg contribution p * scale (also stored into `comm` on the last local step).
+__device__ __forceinline__ float adam_update(const FLConfig& c, const FLBuffers& b, float* __restrict__ comm,
                                             const FLState& S, int local_step, int last_local_step, int pack, int j,
                                             int pk, bool is_bias, int wlo_delta, float (*part)[64], int lane, float p,
                                             float m, float v, float anc, float scale) {
@@ -454,6 +455,7 @@ __device__ __forceinline__ void adam_update(const FLConfig& c, const FLBuffers& 
     b.local[j] = p;
     if (pack) pack_store(b.pk_local, pk, is_bias, wlo_delta, p);
     if (last_local_step) comm[j] = p * scale;
+    return p * scale;
 }
 
 // Chunk ids of the Adam-fused exchange (peer_device.h): the final metric tails, the early lag
@@ -477,6 +479,10 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     FL_STAMP(0);
     const unsigned target = st->calls + 1;  // call index of this kernel's exchanges
+    // lag region A through LL slots (peer_device.h) when it fits one chunk's 64 positions:
+    // every rank pushes its whole region (zeros outside its own segment), receivers sum in rank
+    // order -- the same values as the pull protocol's sum
+    const bool ll_lag = pa.ll != nullptr && c.tail_len <= 64;
     // Round state.  Fused evaluation (fl_common.h): wave 0 of EVERY block folds the previous
     // round's tail (anchor = this round's input image) into the previous state and decides
     // whether this round is live -- the same deterministic computation everywhere, so no
@@ -491,9 +497,13 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         if (fold) {
             const bool need = c.es_enabled || blockIdx.x == 0;
             if (afold) {
-                if (need) {
+                if (need && ll_lag) {
+                    if (lane < c.tail_len) lag_s[lane] = peer_ll_sum(pa, ADAM_CHUNK_LAG * 64 + lane, target);
+                } else if (need) {
                     peer_chunk_wait(pa, ADAM_CHUNK_LAG, target);
                     for (int i = lane; i < c.tail_len; i += 64) lag_s[i] = peer_pull_sum(pa, c.lag_off + i);
+                }
+                if (need) {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     S0 = fold_round(d, c, b, lag_s, S0.next_round - 1, S0, blockIdx.x == 0);
                 }
@@ -522,11 +532,15 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             // kernel) and loss -- published at once: every block of every rank folds from it
             for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
                 const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
-                comm[c.lag_off + jj] = (k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
+                const float v = (k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
+                comm[c.lag_off + jj] = v;
+                if (ll_lag) peer_ll_push(pa, ADAM_CHUNK_LAG * 64 + jj, target, v);  // (jj < 64: wave 0)
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (wave == 0) peer_chunk_publish(pa, ADAM_CHUNK_LAG, target);
+            if (!ll_lag) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (wave == 0) peer_chunk_publish(pa, ADAM_CHUNK_LAG, target);
+            }
         }
         // first batch of loss loads in flight before the fold (one per thread up to 1024 slabs)
         const int s0 = threadIdx.x;
@@ -662,16 +676,29 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     if (wave != 0) return;
     FL_STAMP(4);
     const FLState S = S_sh;
+    float contrib = 0.f;  // this rank's FedAvg contribution of the lane's parameter
     if (valid) {
         if (!S.live) {
-            if (last_local_step) comm[j] = (c.rank == 0) ? a0 : 0.f;
+            contrib = (c.rank == 0) ? a0 : 0.f;
+            if (last_local_step) comm[j] = contrib;
         } else {
-            adam_update(c, b, comm, S, local_step, last_local_step, pack, j, pk, is_bias, e.wlo_delta, part, lane, p0,
-                        m0, v0, a0, sc0);
+            contrib = adam_update(c, b, comm, S, local_step, last_local_step, pack, j, pk, is_bias, e.wlo_delta, part,
+                                  lane, p0, m0, v0, a0, sc0);
         }
     }
     FL_STAMP(5);
-    if (xchg) {
+    if (xchg && pa.ll != nullptr) {
+        // Adam-fused FedAvg of this block's 64 parameters, LL chunks (peer_device.h): push the
+        // contribution with the call index into every rank's ring, poll this rank's ring, sum
+        // in rank order; global image + packed bf16 image
+        const int pos = (ADAM_CHUNK_W0 + pblk) * 64 + lane;
+        if (valid) peer_ll_push(pa, pos, target, contrib);
+        if (valid) {
+            const float gsum = peer_ll_sum(pa, pos, target);
+            pa.out[j] = gsum;
+            if (pack) pack_store(b.pk_global, pk, is_bias, e.wlo_delta, gsum);
+        }
+    } else if (xchg) {
         // Adam-fused FedAvg of this block's 64 parameters (peer_device.h): publish, wait for
         // every rank's chunk, pull + sum in rank order; global image + packed bf16 image
         peer_chunk_exchange_wait(pa, ADAM_CHUNK_W0 + pblk, target);

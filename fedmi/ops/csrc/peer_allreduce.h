@@ -40,6 +40,7 @@ class PeerAllReduce {
     int n_chunks() const { return n_chunks_; }
     bool is_open() const { return open_; }
     bool uncached() const { return uncached_; }         // send buffers in uncached memory
+    bool uses_ll() const { return use_ll_; }            // LL weight chunks (peer_device.h)
     void close();
 
   private:
@@ -47,6 +48,8 @@ class PeerAllReduce {
     long long n_;
     int n_chunks_ = 0;
     size_t buf_bytes_ = 0, total_ = 0;
+    size_t cf_off_ = 0, ll_off_ = 0, ll_bytes_ = 0;  // chunk-flag table, LL ring (byte offsets)
+    bool use_ll_ = false;
     char* base_ = nullptr;
     std::vector<char*> mapped_;        // peers' allocations, opened from their IPC handles
     char* peer_base_[PEER_MAX_WORLD] = {};

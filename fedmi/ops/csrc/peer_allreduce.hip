@@ -24,15 +24,18 @@
 //   * every wait is bounded (s_memrealtime): on a timeout the kernel sets a sticky error word
 //     instead of hanging the GPU, and the host checks it at each synchronisation point.
 //
-// The same allocation carries a chunk-flag table for the round engine's Adam-fused exchange
-// (peer_device.h): there the call index comes from the device round state and every Adam
-// block publishes / waits for / pulls its own 64-parameter chunk.  Start-up self-tests both
-// protocols on a known payload (fedmi/parallel/peer.py) before the engine may use them.
+// The same allocation carries a chunk-flag table and an LL ring for the round engine's
+// Adam-fused exchange (peer_device.h): there the call index comes from the device round state;
+// every Adam block PUSHES its 64 parameters' contributions, each with the call index in one
+// 8-byte store, into every rank's ring and polls its own ring (the metric chunks use the
+// chunk flags: publish / wait / pull).  Start-up self-tests all three protocols on a known
+// payload (fedmi/parallel/peer.py) before the engine may use them.
 #include "peer_allreduce.h"
 
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <stdint.h>
@@ -70,6 +73,15 @@ __global__ void __launch_bounds__(64) peer_chunk_test_kernel(PeerArgs a, unsigne
     if (pos < a.n) out[pos] = peer_pull_sum(a, pos);
 }
 
+// Self-test of the LL chunk exchange (peer_device.h): block c pushes floats [64c, 64c + 64) of
+// this rank's send buffer with call index `target` and sums every rank's values.
+__global__ void __launch_bounds__(64) peer_ll_test_kernel(PeerArgs a, unsigned target, float* out) {
+    const int pos = blockIdx.x * 64 + (int)threadIdx.x;
+    const bool valid = pos < a.n;
+    peer_ll_push(a, pos, target, valid ? a.src[a.rank][pos] : 0.f);
+    if (valid) out[pos] = peer_ll_sum(a, pos, target);
+}
+
 // Self-test payload: exact in fp32 for any summation order (multiples of 1/4 in [-256, 256)).
 __global__ void peer_fill_kernel(float* dst, long long n, int rank, unsigned salt) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -85,8 +97,15 @@ PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, doubl
     if (n <= 0 || n * 4 > (1ll << 30)) throw std::runtime_error("PeerAllReduce: 1..2^28 floats");
     PHIP(hipSetDevice(device));
     buf_bytes_ = ((size_t)n * 4 + 255) & ~(size_t)255;
-    // [send 0 | send 1 | control block | chunk flags: PEER_MAX_WORLD x n_chunks]
-    total_ = 2 * buf_bytes_ + sizeof(PeerCtl) + (((size_t)PEER_MAX_WORLD * n_chunks_ * 4 + 255) & ~(size_t)255);
+    // [send 0 | send 1 | control block | chunk flags: PEER_MAX_WORLD x n_chunks | LL ring:
+    //  2 x PEER_MAX_WORLD x n_chunks x 64 slots of 8 bytes]
+    cf_off_ = 2 * buf_bytes_ + sizeof(PeerCtl);
+    ll_off_ = cf_off_ + (((size_t)PEER_MAX_WORLD * n_chunks_ * 4 + 255) & ~(size_t)255);
+    ll_bytes_ = (size_t)2 * PEER_MAX_WORLD * n_chunks_ * 64 * 8;
+    total_ = ll_off_ + ll_bytes_;
+    // FEDMI_PEER_LL=0: weight chunks through publish / wait / pull instead (A/B)
+    const char* ll_env = std::getenv("FEDMI_PEER_LL");
+    use_ll_ = n_chunks_ > 0 && !(ll_env != nullptr && std::strcmp(ll_env, "0") == 0);
     // Uncached device memory (MTYPE UC, what RCCL uses for its xGMI buffers): peers write the
     // flags and read the send buffers over xGMI, and no L2 -- this GPU's or a peer's -- may
     // hold a stale copy of either.  The send buffers are written once per round (~50 KB),
@@ -176,8 +195,8 @@ void PeerAllReduce::clear() {
     PHIP(hipSetDevice(device_));
     PHIP(hipMemset(base_, 0, 2 * buf_bytes_));
     // chunk flags restart at 0: the engine's call index starts at 1 (self-test calls used it)
-    if (n_chunks_ > 0)
-        PHIP(hipMemset(base_ + 2 * buf_bytes_ + sizeof(PeerCtl), 0, (size_t)PEER_MAX_WORLD * n_chunks_ * 4));
+    // (and the LL ring's call indices: every slot reads "no call yet")
+    if (n_chunks_ > 0) PHIP(hipMemset(base_ + cf_off_, 0, total_ - cf_off_));
     PHIP(hipDeviceSynchronize());
 }
 
@@ -213,7 +232,12 @@ PeerArgs PeerAllReduce::args(int parity, float* out, long long n_w) const {
             a.cflag_dst[j] = reinterpret_cast<unsigned*>(peer_base_[j] + 2 * buf_bytes_ + sizeof(PeerCtl)) +
                              (size_t)rank_ * n_chunks_;
         a.cflags = reinterpret_cast<unsigned*>(base_ + 2 * buf_bytes_ + sizeof(PeerCtl));
+        if (use_ll_) {
+            for (int j = 0; j < world_; ++j) a.ll_dst[j] = reinterpret_cast<unsigned long long*>(peer_base_[j] + ll_off_);
+            a.ll = reinterpret_cast<unsigned long long*>(base_ + ll_off_);
+        }
     }
+    a.rank = rank_;
     return a;
 }
 
@@ -249,6 +273,16 @@ void register_peer(py::module_& m) {
                                     reinterpret_cast<hipStream_t>(stream), a, target, reinterpret_cast<float*>(out));
                  PHIP(hipGetLastError());
              })
+        .def("ll_test",
+             [](const PeerAllReduce& p, unsigned target, uintptr_t out, uintptr_t stream) {
+                 if (!p.uses_ll()) throw std::runtime_error("ll_test: no LL ring");
+                 const PeerArgs a = p.args((int)(target & 1), reinterpret_cast<float*>(out));
+                 const int blocks = (int)std::min<long long>(p.n_chunks(), (p.n_floats() + 63) / 64);
+                 hipLaunchKernelGGL(peer_ll_test_kernel, dim3(blocks), dim3(64), 0,
+                                    reinterpret_cast<hipStream_t>(stream), a, target, reinterpret_cast<float*>(out));
+                 PHIP(hipGetLastError());
+             })
+        .def_property_readonly("uses_ll", &PeerAllReduce::uses_ll)
         .def("fill_test",
              [](const PeerAllReduce& p, int parity, unsigned salt, uintptr_t stream) {
                  const long long n = p.n_floats();

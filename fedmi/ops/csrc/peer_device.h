@@ -67,6 +67,12 @@ struct PeerArgs {
     unsigned* cflag_dst[PEER_MAX_WORLD]; // &chunk_flags_j[rank * n_chunks]: my row in rank j's table
     unsigned* cflags;                    // my table: [world][n_chunks]
     int n_chunks;
+    int rank;
+    // Low-latency (LL) weight chunks of the Adam-fused exchange: 8-byte slots {value, call index}
+    // in a ring [2 parities][PEER_MAX_WORLD source ranks][n_chunks * 64] in every rank's
+    // allocation.  nullptr: the chunks go through the publish / wait / pull protocol.
+    unsigned long long* ll_dst[PEER_MAX_WORLD];  // rank j's ring (mapped)
+    unsigned long long* ll;                      // my ring
 };
 
 // All-reduce blocks of a fused evaluation + FedAvg kernel (FL_THREADS = 512 threads each):
@@ -339,6 +345,64 @@ __device__ __forceinline__ float peer_pull_sum(const PeerArgs& a, int pos) {
 #pragma unroll
     for (int k = 0; k < PEER_MAX_WORLD; ++k)
         if (k < a.world) v[k] = peer_load4(a.src[k], bytes, pos * 4);
+    float s = v[0];
+#pragma unroll
+    for (int k = 1; k < PEER_MAX_WORLD; ++k)
+        if (k < a.world) s += v[k];
+    return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// LL (low-latency) chunk exchange: the sender PUSHES each value, together with the call index,
+// as ONE 8-byte store into every rank's ring slot for (call parity, sender, position); the
+// receiver polls its own ring until every sender's slot carries this call's index, then sums
+// in rank order.  An aligned 8-byte store is single-copy atomic, so a slot showing the index
+// also shows the value: no fence, no flag store after an acknowledged data store, no remote
+// read round trip -- one one-way xGMI write per value instead of write + flag + pull.
+// Slots alternate by call parity: a sender writes call t + 2 into a slot only after every
+// rank joined call t + 1, which each does after finishing its reads of call t (kernel order).
+// The value of an inactive lane is never polled (same positions on every rank).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ size_t peer_ll_slot(const PeerArgs& a, unsigned target, int src, int pos) {
+    return ((size_t)((target & 1u) * PEER_MAX_WORLD + src) * a.n_chunks) * 64 + pos;
+}
+// this lane's value at ring position `pos` (= chunk * 64 + lane) into every rank's ring
+__device__ __forceinline__ void peer_ll_push(const PeerArgs& a, int pos, unsigned target, float v) {
+    const unsigned long long w = ((unsigned long long)target << 32) | __float_as_uint(v);
+    const size_t slot = peer_ll_slot(a, target, a.rank, pos);
+#pragma unroll
+    for (int k = 0; k < PEER_MAX_WORLD; ++k)
+        if (k < a.world) __hip_atomic_store(a.ll_dst[k] + slot, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Sum over ranks (rank order) of ring position `pos` for call `target`, polling (bounded by the
+// timeout: on expiry the sticky error word is set and missing values count 0).
+__device__ __forceinline__ float peer_ll_sum(const PeerArgs& a, int pos, unsigned target) {
+    float v[PEER_MAX_WORLD];
+    unsigned pend = 0;
+#pragma unroll
+    for (int k = 0; k < PEER_MAX_WORLD; ++k) {
+        v[k] = 0.f;
+        if (k < a.world) pend |= 1u << k;
+    }
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < PEER_MAX_WORLD; ++k)
+            if (pend & (1u << k)) {
+                const unsigned long long w =
+                    __hip_atomic_load(a.ll + peer_ll_slot(a, target, k, pos), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((unsigned)(w >> 32) == target) {
+                    v[k] = __uint_as_float((unsigned)w);
+                    pend &= ~(1u << k);
+                }
+            }
+        if (pend == 0) break;
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
+            __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
     float s = v[0];
 #pragma unroll
     for (int k = 1; k < PEER_MAX_WORLD; ++k)

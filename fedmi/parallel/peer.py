@@ -61,6 +61,17 @@ def selftest(h, comm, device, calls: int = 4, timeout_s: float = 10.0) -> bool:
             expect = sum(fill_values(n, r, salt) for r in range(comm.size)).astype(np.float32)[:m]
             ok = ok and bool(np.array_equal(got, expect))
             comm.Barrier()  # every rank has read this parity before it is refilled
+        # LL weight chunks (peer_device.h): values pushed with the call index, both parities
+        if bool(getattr(h, "uses_ll", False)):
+            for k in range(2):
+                salt, target = 3000 + k, 3 + k
+                out.zero_()
+                h.fill_test(target & 1, salt, s.cuda_stream)
+                comm.Barrier()  # every rank's payload is in place before anyone pushes it
+                h.ll_test(target, out.data_ptr(), s.cuda_stream)
+                got = out.cpu().numpy()[:m]
+                expect = sum(fill_values(n, r, salt) for r in range(comm.size)).astype(np.float32)[:m]
+                ok = ok and bool(np.array_equal(got, expect))
     ok = ok and h.error() == 0
     return ok
 

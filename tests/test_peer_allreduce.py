@@ -31,7 +31,7 @@ def _free_port():
 
 
 def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = True, lagged: bool = True,
-                hidden=(50, 200)):
+                hidden=(50, 200), expect_ll=None):
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
     comm.peer_allreduce = peer
     cfg = EngineConfig(hidden=tuple(hidden), max_rounds=30, early_stop=False, dtype=dtype, graph_rounds=4,
@@ -41,6 +41,8 @@ def _run_engine(comm, peer: bool, dtype: str, X, y, flat, eval_fedavg: bool = Tr
     assert e.aggregation == (("xgmi-oneshot+adam" if lag else "xgmi-oneshot") if peer else "host"), e.aggregation
     assert bool(e.engine.lagged) == lag, (e.engine.lagged, lagged, dtype)
     assert bool(e.engine.adam_exchange) == (lag and peer)
+    if expect_ll is not None:  # LL weight chunks of the Adam-fused exchange (peer_device.h)
+        assert bool(e._peer.uses_ll) == expect_ll
     e.run(3)                       # eager rounds
     cms = []
     for _ in range(2):             # reference step-by-step API
@@ -169,13 +171,19 @@ def _worker4(rank, world, port, q):
         # at once (each waits for the others' chunks; on separate GPUs that always holds)
         hidden = (24, 12)
         flat = init_flat([14, *hidden, 2], 5)
-        a = _run_engine(comm, True, "bf16", X, y, flat, hidden=hidden)
+        a = _run_engine(comm, True, "bf16", X, y, flat, hidden=hidden, expect_ll=True)
+        # the same exchange with publish / wait / pull weight chunks (FEDMI_PEER_LL=0)
+        os.environ["FEDMI_PEER_LL"] = "0"
+        try:
+            a0 = _run_engine(comm, True, "bf16", X, y, flat, hidden=hidden, expect_ll=False)
+        finally:
+            del os.environ["FEDMI_PEER_LL"]
         # classic rounds over the standalone peer kernel: the same rank-order sums (gloo's
         # 4-rank reduction order differs, so the host path is not a bitwise reference here)
         b = _run_engine(comm, True, "bf16", X, y, flat, True, False, hidden=hidden)
         torch.cuda.synchronize()
         comm.Barrier()
-        q.put((rank, (ok, a, b), None))
+        q.put((rank, (ok, a, b, a0), None))
         comm.close()
     except Exception:  # noqa: BLE001
         import traceback
@@ -184,8 +192,9 @@ def _worker4(rank, world, port, q):
 
 def test_peer_four_ranks_lagged_adam_exchange():
     """W = 4 (more ranks than the 2-rank test: the unrolled rank loops and chunk-flag rows):
-    self-tests pass and the lagged engine with FedAvg inside the Adam kernel equals classic
-    rounds over the standalone peer kernel bit for bit, with unequal shard sizes."""
+    self-tests pass and the lagged engine with FedAvg inside the Adam kernel -- LL weight chunks
+    (value + call index in one 8-byte push) and publish / wait / pull chunks alike -- equals
+    classic rounds over the standalone peer kernel bit for bit, with unequal shard sizes."""
     world = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -198,9 +207,12 @@ def test_peer_four_ranks_lagged_adam_exchange():
         p.join(timeout=30)
     for rank, res, err in out:
         assert err is None, f"rank {rank}:\n{err}"
-        ok, (wa, ha, ca), (wb, hb, cb) = res
+        ok, (wa, ha, ca), (wb, hb, cb), (w0, h0, c0) = res
         assert ok
         np.testing.assert_array_equal(wa, wb)
+        np.testing.assert_array_equal(w0, wb)
+        np.testing.assert_array_equal(h0["global"], hb["global"])
+        np.testing.assert_array_equal(c0, cb)
         np.testing.assert_array_equal(ha["global"], hb["global"])
         np.testing.assert_array_equal(ha["per_rank"], hb["per_rank"])
         np.testing.assert_array_equal(ca, cb)
