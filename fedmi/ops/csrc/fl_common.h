@@ -285,4 +285,4 @@ hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const in
 hipError_t fl_launch_synth(float* X, int* y, long long n_rows, int n_features,
                            unsigned long long seed, unsigned long long row_offset,
                            const float* teacher_w1, const float* teacher_w2, int teacher_hidden,
-                           hipStream_t s);
+                           hipStream_t s, float label_noise = 0.f);

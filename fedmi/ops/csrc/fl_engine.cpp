@@ -658,9 +658,9 @@ class FLEngine {
 
 // Thin wrappers used by tests and the synthetic-data path.
 static void synth(uintptr_t X, uintptr_t y, long long n, int F, unsigned long long seed, unsigned long long off,
-                  uintptr_t w1, uintptr_t w2, int H, uintptr_t stream) {
+                  uintptr_t w1, uintptr_t w2, int H, uintptr_t stream, float label_noise) {
     HIP_CHECK(fl_launch_synth(as_ptr<float>(X), as_ptr<int>(y), n, F, seed, off, as_ptr<const float>(w1),
-                              as_ptr<const float>(w2), H, as_stream(stream)));
+                              as_ptr<const float>(w2), H, as_stream(stream), label_noise));
 }
 
 static py::dict device_info(int dev) {
@@ -714,7 +714,8 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);
-    m.def("synth", &synth);
+    m.def("synth", &synth, py::arg("X"), py::arg("y"), py::arg("n"), py::arg("F"), py::arg("seed"), py::arg("off"),
+          py::arg("w1"), py::arg("w2"), py::arg("H"), py::arg("stream"), py::arg("label_noise") = 0.f);
     m.def("device_info", &device_info);
     m.attr("STATE_BYTES") = (int)sizeof(FLState);
     register_trainer(m);

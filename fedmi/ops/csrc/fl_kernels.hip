@@ -498,7 +498,8 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
             const bool need = c.es_enabled || blockIdx.x == 0;
             if (afold) {
                 if (need && ll_lag) {
-                    if (lane < c.tail_len) lag_s[lane] = peer_ll_sum(pa, ADAM_CHUNK_LAG * 64 + lane, target);
+                    const float lv = peer_ll_sum(pa, ADAM_CHUNK_LAG * 64 + lane, target, lane < c.tail_len);
+                    if (lane < c.tail_len) lag_s[lane] = lv;
                 } else if (need) {
                     peer_chunk_wait(pa, ADAM_CHUNK_LAG, target);
                     for (int i = lane; i < c.tail_len; i += 64) lag_s[i] = peer_pull_sum(pa, c.lag_off + i);
@@ -693,8 +694,8 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
         // in rank order; global image + packed bf16 image
         const int pos = (ADAM_CHUNK_W0 + pblk) * 64 + lane;
         if (valid) peer_ll_push(pa, pos, target, contrib);
+        const float gsum = peer_ll_sum(pa, pos, target, valid);
         if (valid) {
-            const float gsum = peer_ll_sum(pa, pos, target);
             pa.out[j] = gsum;
             if (pack) pack_store(b.pk_global, pk, is_bias, e.wlo_delta, gsum);
         }
@@ -813,7 +814,8 @@ __device__ __forceinline__ float u01(uint32_t x) { return ((x >> 8) + 0.5f) * (1
 
 __global__ void fl_synth_kernel(float* __restrict__ X, int* __restrict__ y, long long n, int F,
                                 unsigned long long seed, unsigned long long row_offset,
-                                const float* __restrict__ w1, const float* __restrict__ w2, int H) {
+                                const float* __restrict__ w1, const float* __restrict__ w2, int H,
+                                float label_noise) {
     const long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= n) return;
     const uint64_t gid = row_offset + (uint64_t)row;
@@ -840,7 +842,11 @@ __global__ void fl_synth_kernel(float* __restrict__ X, int* __restrict__ y, long
         for (int f = 0; f < F; ++f) a += w1[h * F + f] * x[f];
         score += w2[h] * fmaxf(a, 0.f);
     }
-    y[row] = score > w2[H] ? 1 : 0;  // w2[H] holds the balancing threshold
+    int label = score > w2[H] ? 1 : 0;  // w2[H] holds the balancing threshold
+    // label noise: flip with probability `label_noise` (its own Philox stream, column F), so the
+    // synthetic task has a Bayes accuracy like the income table's (~0.85) instead of 1
+    if (label_noise > 0.f && u01(philox4x32(gid, (uint32_t)F, seed).w) < label_noise) label ^= 1;
+    y[row] = label;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -955,11 +961,11 @@ hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const in
 
 hipError_t fl_launch_synth(float* X, int* y, long long n, int F, unsigned long long seed,
                            unsigned long long row_offset, const float* w1, const float* w2, int H,
-                           hipStream_t s) {
+                           hipStream_t s, float label_noise) {
     if (F > 32) return hipErrorInvalidValue;
     const long long blocks = (n + 255) / 256;
     hipLaunchKernelGGL(fl_synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, y, n, F, seed, row_offset,
-                       w1, w2, H);
+                       w1, w2, H, label_noise);
     return hipGetLastError();
 }
 

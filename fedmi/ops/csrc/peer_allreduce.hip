@@ -79,7 +79,8 @@ __global__ void __launch_bounds__(64) peer_ll_test_kernel(PeerArgs a, unsigned t
     const int pos = blockIdx.x * 64 + (int)threadIdx.x;
     const bool valid = pos < a.n;
     peer_ll_push(a, pos, target, valid ? a.src[a.rank][pos] : 0.f);
-    if (valid) out[pos] = peer_ll_sum(a, pos, target);
+    const float v = peer_ll_sum(a, pos, target, valid);
+    if (valid) out[pos] = v;
 }
 
 // Self-test payload: exact in fp32 for any summation order (multiples of 1/4 in [-256, 256)).

@@ -375,8 +375,10 @@ __device__ __forceinline__ void peer_ll_push(const PeerArgs& a, int pos, unsigne
         if (k < a.world) __hip_atomic_store(a.ll_dst[k] + slot, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // Sum over ranks (rank order) of ring position `pos` for call `target`, polling (bounded by the
-// timeout: on expiry the sticky error word is set and missing values count 0).
-__device__ __forceinline__ float peer_ll_sum(const PeerArgs& a, int pos, unsigned target) {
+// timeout: on expiry the sticky error word is set and missing values count 0).  Called by the
+// whole wave; lanes with `active` false (no value at their position) return 0.
+__device__ __forceinline__ float peer_ll_sum(const PeerArgs& a, int pos, unsigned target, bool active) {
+    if (!active) return 0.f;
     float v[PEER_MAX_WORLD];
     unsigned pend = 0;
 #pragma unroll

@@ -27,6 +27,7 @@ selects the device (fixes the reference's everyone-on-GPU-0).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import sys
 from typing import Any, List, Optional
@@ -55,6 +56,20 @@ def resolve_backend(backend: str, device_type: str) -> str:
         raise ValueError(f"FEDMI_DATA_PLANE={plane!r}: expected one of {DATA_PLANES}")
     return plane
 
+
+
+@contextlib.contextmanager
+def _c_stdout_to_stderr():
+    """File descriptor 1 -> 2 for the duration (output of native libraries included)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 class Comm:
     """``rccl=False`` (with ``backend='xgmi'``) skips the RCCL communicator: device
@@ -89,8 +104,11 @@ class Comm:
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29500")
                 from datetime import timedelta
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.size,
-                                        timeout=timedelta(seconds=timeout_s))
+                # gloo prints its connection report on the C-level stdout; send it to stderr so
+                # rank 0's stdout carries only the program's own output (bench.py's JSON line)
+                with _c_stdout_to_stderr():
+                    dist.init_process_group("gloo", rank=self.rank, world_size=self.size,
+                                            timeout=timedelta(seconds=timeout_s))
                 self._initialized_here = True
             if backend == "rccl" or (backend == "xgmi" and rccl):
                 from ..ops import native

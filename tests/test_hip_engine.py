@@ -137,6 +137,15 @@ def test_synthetic_device_generator():
     assert np.isfinite(Xc).all()
     assert abs(Xc[:, :6].mean()) < 0.02 and abs(Xc[:, :6].std() - 1) < 0.02
     assert 0.35 < yv.float().mean().item() < 0.65
+    # label noise: the same rows, each label flipped with probability 0.15 (own Philox stream)
+    Xn = torch.empty_like(X)
+    yn = torch.empty_like(yv)
+    m.synth(Xn.data_ptr(), yn.data_ptr(), n, 14, 7, 0, tw1.data_ptr(), tw2.data_ptr(), w1.shape[0],
+            torch.cuda.current_stream().cuda_stream, 0.15)
+    torch.cuda.synchronize()
+    assert torch.equal(Xn, X)
+    flip = (yn != yv).float().mean().item()
+    assert 0.145 < flip < 0.155, flip
 
 
 @pytest.mark.parametrize("dtype", [0, 1])

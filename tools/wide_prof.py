@@ -1,8 +1,9 @@
 """Wide-MLP round profiling driver (rocprofv3 --kernel-trace --stats): 14-4096^3-2, 131072 rows,
 micro-batch = argv[1] rows (default: the whole shard), bf16, 4 rounds."""
+import os
 import sys
 import torch
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedmi.fl.wide import WideClient
 
 dev = torch.device("cuda", 0)
