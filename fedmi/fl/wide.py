@@ -155,6 +155,18 @@ class WideClient:
             self.stream.wait_event(ev)
             self._bucket_ev[l] = None
 
+    def _rows_p(self, rows: int) -> Optional[int]:
+        """Rows a micro-batch of `rows` runs as on the padded NT path, or None (generic path:
+        a partial micro-batch pads only when every hidden layer runs on the NT GEMM, so every
+        operand's padded rows are written by the same pass)."""
+        if not self._pad:
+            return None
+        if rows % 128 == 0:
+            return rows
+        if not all(d % 128 == 0 for d in self.dims[1:-1]):
+            return None
+        return min((rows + 127) // 128 * 128, self.mb)
+
     @staticmethod
     def _nt_ok(M: int, N: int, K: int) -> bool:
         return M % 128 == 0 and N % 128 == 0 and K % 64 == 0
@@ -164,9 +176,16 @@ class WideClient:
         operand, ReLU mask) and, when training, bf16 transposed (wgrad B operand)."""
         m, s, mb = self.m, self._s(), self.mb
         x = self.X[r0:r0 + rows]
-        pad = self._pad and rows % 128 == 0
+        # a partial last micro-batch runs as rp = roundup(rows, 128) rows on the NT GEMM: its
+        # extra input rows are zeros, their deltas are zeroed before the backward pass (they add
+        # exact zeros to every gradient), and the loss / confusion kernels see the real rows only
+        rp = self._rows_p(rows)
+        pad = rp is not None
+        rp = rp if pad else rows
         if pad:
             m.pad_bf16(x.data_ptr(), rows, self.dims[0], self.dims[0], 1, self.xp.data_ptr(), 64, s)
+            if rp > rows:
+                self.xp[rows:rp].zero_()
             inp = self.xp
         elif self.dtype:
             m.to_bf16(x.data_ptr(), self.xq.data_ptr(), x.numel(), s)
@@ -177,14 +196,14 @@ class WideClient:
             K, N = self.dims[l], self.dims[l + 1]
             self._wait_bucket(l)
             if l == 0 and pad:  # K = 14 zero-padded to 64: NT GEMM, bias + ReLU, bf16 + transposed out
-                hT = self.hT[0].data_ptr() if keep_t else 0
-                m.gemm_nt(rows, N, 64, self.xp.data_ptr(), 64, self.W0p.data_ptr(), 64, 0, 0, self.hq[0].data_ptr(),
+                hT = self.hT[0].data_ptr() if (keep_t and self.L > 2) else 0
+                m.gemm_nt(rp, N, 64, self.xp.data_ptr(), 64, self.W0p.data_ptr(), 64, 0, 0, self.hq[0].data_ptr(),
                           N, hT, mb, self.b[0].data_ptr(), 0, 0, 1, 1.0, 0.0, s)
                 self.nt_calls += 1
                 inp = self.hq[0]
                 continue
             if l + 1 == self.L and pad:  # logits head, classes padded to 256: fp32 [rows][256]
-                m.gemm_nt(rows, 256, K, inp.data_ptr(), K, self.Whp.data_ptr(), K, self.logits_p.data_ptr(), 256,
+                m.gemm_nt(rp, 256, K, inp.data_ptr(), K, self.Whp.data_ptr(), K, self.logits_p.data_ptr(), 256,
                           0, 0, 0, 0, self.bhp.data_ptr(), 0, 0, 0, 1.0, 0.0, s)
                 self.nt_calls += 1
                 break
@@ -193,9 +212,11 @@ class WideClient:
                        self.logits.stride(0), 1, self.b[l].data_ptr(), 0, 0, 0, 1.0, 0.0, self.dtype, 1, 0, 0, s)
                 break
             hq = self.hq[l]
-            hT = self.hT[l].data_ptr() if (keep_t and self.dtype) else 0
-            if self._t_ok and self._nt_ok(rows, N, K):
-                m.gemm_nt(rows, N, K, inp.data_ptr(), K, self.Wq[l].data_ptr(), K, 0, 0, hq.data_ptr(), N, hT, mb,
+            # the transposed copy feeds layer l+1's NT weight gradient: none for the last hidden
+            # layer, whose consumer (the head's skinny / generic weight gradient) reads hq
+            hT = self.hT[l].data_ptr() if (keep_t and self.dtype and l + 2 < self.L) else 0
+            if self._t_ok and self._nt_ok(rp, N, K):
+                m.gemm_nt(rp, N, K, inp.data_ptr(), K, self.Wq[l].data_ptr(), K, 0, 0, hq.data_ptr(), N, hT, mb,
                           self.b[l].data_ptr(), 0, 0, 1, 1.0, 0.0, s)
                 self.nt_calls += 1
             else:
@@ -222,11 +243,15 @@ class WideClient:
         C = self.dims[-1]
         # output layer (N = classes): tiny GEMMs on the generic kernel
         K = self.dims[L - 1]
-        pad = self._pad and rows % 128 == 0
+        rp = self._rows_p(rows)  # (see _forward: padded rows carry zero deltas)
+        pad = rp is not None
+        rp = rp if pad else rows
         dzo, ldo = self.dzq[L - 1], C
         if pad:
             dzo, ldo = self.dzp, 64
             m.pad_bf16(self.dz_out.data_ptr(), rows, C, C, 1, dzo.data_ptr(), 64, s)
+            if rp > rows:
+                dzo[rows:rp].zero_()
         elif self.dtype:
             m.to_bf16(self.dz_out.data_ptr(), dzo.data_ptr(), rows * C, s)
         else:
@@ -246,7 +271,7 @@ class WideClient:
         if L >= 2 and pad:
             # dgrad into the last hidden layer: C classes zero-padded to K = 64 on the NT GEMM,
             # ReLU-masked, bf16 row-major + transposed outputs
-            m.gemm_nt(rows, K, 64, dzo.data_ptr(), 64, self.WhTp.data_ptr(), 64, 0, 0, self.dzq[L - 2].data_ptr(), K,
+            m.gemm_nt(rp, K, 64, dzo.data_ptr(), 64, self.WhTp.data_ptr(), 64, 0, 0, self.dzq[L - 2].data_ptr(), K,
                       self.dzT[L - 2].data_ptr(), mb, 0, self.hq[L - 2].data_ptr(), K, 0, 1.0, 0.0, s)
             self.nt_calls += 1
         elif L >= 2:
@@ -270,8 +295,8 @@ class WideClient:
             else:
                 inp = self.hq[l - 1]
             # wgrad (+= over micro-batches): dW[N][K] = dZ^T . in;  bias: row sums of dZ^T
-            if self._t_ok and l > 0 and self._nt_ok(N, K, rows):
-                m.gemm_nt(N, K, rows, self.dzT[l].data_ptr(), mb, self.hT[l - 1].data_ptr(), mb,
+            if self._t_ok and l > 0 and self._nt_ok(N, K, rp):
+                m.gemm_nt(N, K, rp, self.dzT[l].data_ptr(), mb, self.hT[l - 1].data_ptr(), mb,
                           self.gW[l].data_ptr(), K, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, beta, s)
                 self.nt_calls += 1
             elif l == 0 and self._skinny:
@@ -291,9 +316,12 @@ class WideClient:
             if l == 0:
                 break
             # dgrad: dIn[rows][K] = dZ . W, masked by in > 0
-            if self._t_ok and self._nt_ok(rows, K, N):
-                m.gemm_nt(rows, K, N, dq.data_ptr(), N, self.WqT[l].data_ptr(), N, 0, 0, self.dzq[l - 1].data_ptr(), K,
-                          self.dzT[l - 1].data_ptr(), mb, 0, self.hq[l - 1].data_ptr(), K, 0, 1.0, 0.0, s)
+            if self._t_ok and self._nt_ok(rp, K, N):
+                # dZ_{l-1}^T feeds the NT weight gradient and row sums of layer l-1; layer 0's
+                # skinny kernel reads dZ_0 row-major (weights and bias), so no transposed copy
+                dT = 0 if (l == 1 and self._skinny) else self.dzT[l - 1].data_ptr()
+                m.gemm_nt(rp, K, N, dq.data_ptr(), N, self.WqT[l].data_ptr(), N, 0, 0, self.dzq[l - 1].data_ptr(), K,
+                          dT, mb, 0, self.hq[l - 1].data_ptr(), K, 0, 1.0, 0.0, s)
                 self.nt_calls += 1
             else:
                 m.gemm(rows, K, N, dq.data_ptr(), N, 1, self.Wq[l].data_ptr(), K, 0, self.scratch.data_ptr(), K, 3, 0,

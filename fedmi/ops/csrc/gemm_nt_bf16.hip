@@ -609,7 +609,9 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
     case F: hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel<F>, dim3(blocks), dim3(NT2_THREADS), 0, s, g); break;
             NT_FL_CASE(NT_EPI_CB)                                                  // plain bf16 output
             NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_BIAS | NT_EPI_RELU)         // hidden-layer forward
+            NT_FL_CASE(NT_EPI_CB | NT_EPI_BIAS | NT_EPI_RELU)                      // forward, no transposed copy
             NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK)                       // dgrad (ReLU mask)
+            NT_FL_CASE(NT_EPI_CB | NT_EPI_MASK)                                    // dgrad, no transposed copy
             NT_FL_CASE(NT_EPI_C)                                                   // fp32 output
             NT_FL_CASE(NT_EPI_C | NT_EPI_BETA)                                     // accumulating wgrad
             NT_FL_CASE(NT_EPI_C | NT_EPI_BIAS)                                     // fp32 logits
