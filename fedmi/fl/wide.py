@@ -18,6 +18,7 @@ layer by layer on the grid-level MFMA GEMMs of ``fedmi/ops/csrc/gemm_mfma.hip``:
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -71,9 +72,13 @@ class WideClient:
         # activations / deltas of one micro-batch: row-major GEMM operands + transposed
         # (k = rows contiguous) copies for the NT weight-gradient GEMMs
         self.hq = [torch.empty(mb, d, dtype=gdt, device=dev) for d in dims[1:-1]]
-        self.hT = [torch.empty(d, mb, dtype=gdt, device=dev) for d in dims[1:-1]]
+        # (row stride ldt: 256 extra elements (FEDMI_WIDE_TPAD) break the power-of-two stride; the
+        # weight-gradient GEMM reading them as its A operand runs ~4 % faster, profiles/wide_tpad_r2.log)
+        self.ldt = mb + int(os.environ.get("FEDMI_WIDE_TPAD", "256"))
+        assert self.ldt % 8 == 0
+        self.hT = [torch.empty(d, self.ldt, dtype=gdt, device=dev) for d in dims[1:-1]]
         self.dzq = [torch.empty(mb, d, dtype=gdt, device=dev) for d in dims[1:]]
-        self.dzT = [torch.empty(d, mb, dtype=gdt, device=dev) for d in dims[1:-1]]
+        self.dzT = [torch.empty(d, self.ldt, dtype=gdt, device=dev) for d in dims[1:-1]]
         self.xq = torch.empty(mb, dims[0], dtype=gdt, device=dev)
         self.scratch = torch.empty(mb * max(dims[1:]), **f32)  # fp32 epilogue target of the generic GEMM
         self.logits = torch.empty(mb, dims[-1], **f32)
@@ -174,7 +179,7 @@ class WideClient:
     def _forward(self, r0: int, rows: int, keep_t: bool = True):
         """Forward of one micro-batch.  Hidden layers write bf16 row-major (next layer's A
         operand, ReLU mask) and, when training, bf16 transposed (wgrad B operand)."""
-        m, s, mb = self.m, self._s(), self.mb
+        m, s, mb = self.m, self._s(), self.ldt
         x = self.X[r0:r0 + rows]
         # a partial last micro-batch runs as rp = roundup(rows, 128) rows on the NT GEMM: its
         # extra input rows are zeros, their deltas are zeroed before the backward pass (they add
@@ -239,7 +244,7 @@ class WideClient:
         return max(1, min(self.sk_splits, rows // 256))
 
     def _backward(self, r0: int, rows: int, beta: float):
-        m, s, mb, L = self.m, self._s(), self.mb, self.L
+        m, s, mb, L = self.m, self._s(), self.ldt, self.L  # mb: row stride of the transposed operands
         C = self.dims[-1]
         # output layer (N = classes): tiny GEMMs on the generic kernel
         K = self.dims[L - 1]
