@@ -94,6 +94,11 @@ class WideClient:
         self.sk_slab = (torch.empty(self.sk_splits * max((dims[0] + 1) * dims[1], dims[-1] * dims[-2]), **f32)
                         if self._skinny else None)
         self.dz_out = torch.empty(mb, dims[-1], **f32)
+        # bias gradients of the hidden layers: column sums of each dgrad's bf16 output, one row per
+        # 128 output rows, written by the NT epilogue (NT_EPI_CSUM) and folded by colsum -- instead
+        # of re-reading the whole transposed delta (rowsum_bf16)
+        self.cs_slab = torch.empty((mb // 128) * max(dims[1:-1]), **f32) if len(dims) > 2 else None
+        self._cs_layer: Optional[int] = None
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         self.cm = torch.zeros(dims[-1] * dims[-1], dtype=torch.float32, device=dev)  # local confusion counts
         self.evaluated = False
@@ -160,6 +165,10 @@ class WideClient:
             self.stream.wait_event(ev)
             self._bucket_ev[l] = None
 
+    def _csum_ok(self, rp: int, n: int) -> bool:
+        """The dgrad of an [rp][n] delta can emit its column sums (256x256 NT loops)."""
+        return self.cs_slab is not None and rp % 256 == 0 and n % 256 == 0
+
     def _rows_p(self, rows: int) -> Optional[int]:
         """Rows a micro-batch of `rows` runs as on the padded NT path, or None (generic path:
         a partial micro-batch pads only when every hidden layer runs on the NT GEMM, so every
@@ -170,7 +179,8 @@ class WideClient:
             return rows
         if not all(d % 128 == 0 for d in self.dims[1:-1]):
             return None
-        return min((rows + 127) // 128 * 128, self.mb)
+        g = 256 if self.mb % 256 == 0 else 128  # (256: the column-sum epilogue's tile)
+        return min((rows + g - 1) // g * g, self.mb)
 
     @staticmethod
     def _nt_ok(M: int, N: int, K: int) -> bool:
@@ -251,6 +261,7 @@ class WideClient:
         rp = self._rows_p(rows)  # (see _forward: padded rows carry zero deltas)
         pad = rp is not None
         rp = rp if pad else rows
+        self._cs_layer = None
         dzo, ldo = self.dzq[L - 1], C
         if pad:
             dzo, ldo = self.dzp, 64
@@ -276,8 +287,11 @@ class WideClient:
         if L >= 2 and pad:
             # dgrad into the last hidden layer: C classes zero-padded to K = 64 on the NT GEMM,
             # ReLU-masked, bf16 row-major + transposed outputs
+            cs = self._csum_ok(rp, K)
             m.gemm_nt(rp, K, 64, dzo.data_ptr(), 64, self.WhTp.data_ptr(), 64, 0, 0, self.dzq[L - 2].data_ptr(), K,
-                      self.dzT[L - 2].data_ptr(), mb, 0, self.hq[L - 2].data_ptr(), K, 0, 1.0, 0.0, s)
+                      self.dzT[L - 2].data_ptr(), mb, 0, self.hq[L - 2].data_ptr(), K, 0, 1.0, 0.0, s,
+                      self.cs_slab.data_ptr() if cs else 0, K)
+            self._cs_layer = L - 2 if cs else None
             self.nt_calls += 1
         elif L >= 2:
             # dgrad into the last hidden layer (K = C: bandwidth-bound), ReLU-masked
@@ -313,6 +327,8 @@ class WideClient:
                        1.0, beta, self.dtype, self._wg_split(rows) if l == 0 else 1, self.wg_slab.data_ptr(), 0, s)
             if l == 0 and self._skinny:
                 pass  # bias gradient produced by the skinny weight-gradient kernel above
+            elif self._cs_layer == l:  # column sums from the dgrad epilogue that produced dZ_l
+                m.colsum(self.cs_slab.data_ptr(), rp // 128, N, N, self.gb[l].data_ptr(), beta, s)
             elif self.dtype and rows % 8 == 0 and mb % 8 == 0:
                 m.rowsum_bf16(self.dzT[l].data_ptr(), N, rows, mb, self.gb[l].data_ptr(), beta, s)
             else:
@@ -325,8 +341,11 @@ class WideClient:
                 # dZ_{l-1}^T feeds the NT weight gradient and row sums of layer l-1; layer 0's
                 # skinny kernel reads dZ_0 row-major (weights and bias), so no transposed copy
                 dT = 0 if (l == 1 and self._skinny) else self.dzT[l - 1].data_ptr()
+                cs = dT != 0 and self._csum_ok(rp, K)  # (layer 0 + skinny: its kernel sums the bias)
                 m.gemm_nt(rp, K, N, dq.data_ptr(), N, self.WqT[l].data_ptr(), N, 0, 0, self.dzq[l - 1].data_ptr(), K,
-                          dT, mb, 0, self.hq[l - 1].data_ptr(), K, 0, 1.0, 0.0, s)
+                          dT, mb, 0, self.hq[l - 1].data_ptr(), K, 0, 1.0, 0.0, s,
+                          self.cs_slab.data_ptr() if cs else 0, K)
+                self._cs_layer = l - 1 if cs else None
                 self.nt_calls += 1
             else:
                 m.gemm(rows, K, N, dq.data_ptr(), N, 1, self.Wq[l].data_ptr(), K, 0, self.scratch.data_ptr(), K, 3, 0,

@@ -14,6 +14,8 @@ struct NTArgs {
     int relu;
     float alpha, beta;
     unsigned long long* dbg;    // optional [blocks][8] s_memrealtime phase stamps (profiling; full-line loop)
+    float* csum; int ldcs;      // optional column sums of the bf16 output (bias gradient of a dgrad):
+                                // csum[m / 128][n] = sum of the tile half's 128 rows (256x256 loops only)
 };
 
 hipError_t gemm_nt_bf16_launch(const NTArgs& g, hipStream_t s);

@@ -204,10 +204,11 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :
 #define NT_EPI_RELU 16
 #define NT_EPI_BIAS 32
 #define NT_EPI_BETA 64
+#define NT_EPI_CSUM 128
 static inline int nt_epi_flags(const NTArgs& g) {
     return (g.C != nullptr ? NT_EPI_C : 0) | (g.Cbf16 != nullptr ? NT_EPI_CB : 0) | (g.CbT != nullptr ? NT_EPI_CBT : 0) |
            (g.mask != nullptr ? NT_EPI_MASK : 0) | (g.relu ? NT_EPI_RELU : 0) | (g.bias != nullptr ? NT_EPI_BIAS : 0) |
-           (g.C != nullptr && g.beta != 0.f ? NT_EPI_BETA : 0);
+           (g.C != nullptr && g.beta != 0.f ? NT_EPI_BETA : 0) | (g.csum != nullptr ? NT_EPI_CSUM : 0);
 }
 
 template <int F>
@@ -222,6 +223,7 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     const bool hRelu = F < 0 ? g.relu != 0 : (F & NT_EPI_RELU) != 0;
     const bool hBias = F < 0 ? g.bias != nullptr : (F & NT_EPI_BIAS) != 0;
     const bool hBeta = F < 0 ? g.beta != 0.f : (F & NT_EPI_BETA) != 0;
+    const bool hCsum = F < 0 ? g.csum != nullptr : (F & NT_EPI_CSUM) != 0;
 
     // Epilogue.  Every wave's LDS reads retired before that last barrier, so the 128 KiB of LDS
     // now holds the block's 256x256 bf16 output tile as 512-byte rows whose 16-byte chunk index
@@ -250,6 +252,7 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     for (int y = 0; y < 4; ++y) {
         const int cl = wc * 64 + 16 * y + lr, n = n0 + cl;
         const float bv = hBias ? g.bias[n] : 0.f;
+        float cs = 0.f;  // column n's sum over the lane's 32 rows of the bf16 output (hCsum)
 #pragma unroll
         for (int x = 0; x < 8; ++x) {
             uint32_t tp[2];  // the lane's 4 consecutive rows of column n, packed for CbT
@@ -267,6 +270,7 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
                 }
                 const __hip_bfloat16 hv = __float2bfloat16(v);
                 if (hCb) *slot = hv;
+                if (hCsum) cs += __bfloat162float(hv);
                 const uint32_t hb = __bfloat16_as_ushort(hv);
                 if (j & 1) tp[j >> 1] |= hb << 16;
                 else tp[j >> 1] = hb;
@@ -275,6 +279,12 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
                 const size_t off = (size_t)n * g.ldct + m0 + wr * 128 + 16 * x + 4 * lg;
                 *reinterpret_cast<uint2*>(CbT + off) = make_uint2(tp[0], tp[1]);
             }
+        }
+        if (hCsum) {
+            // + the other three lane groups of the column (fixed order): the wave's 128 rows
+            cs += __shfl_xor(cs, 16);
+            cs += __shfl_xor(cs, 32);
+            if (lg == 0) g.csum[(size_t)((m0 >> 7) + wr) * g.ldcs + n] = cs;
         }
     }
     if (hCb) {
@@ -611,6 +621,7 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
             NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_BIAS | NT_EPI_RELU)         // hidden-layer forward
             NT_FL_CASE(NT_EPI_CB | NT_EPI_BIAS | NT_EPI_RELU)                      // forward, no transposed copy
             NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK)                       // dgrad (ReLU mask)
+            NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK | NT_EPI_CSUM)         // dgrad + bias gradient
             NT_FL_CASE(NT_EPI_CB | NT_EPI_MASK)                                    // dgrad, no transposed copy
             NT_FL_CASE(NT_EPI_C)                                                   // fp32 output
             NT_FL_CASE(NT_EPI_C | NT_EPI_BETA)                                     // accumulating wgrad
@@ -620,6 +631,7 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
         }
         return hipGetLastError();
     }
+    if (g.csum != nullptr) return hipErrorInvalidValue;  // column sums: 256x256 loops only
     const int blocks = (g.M / NT_BM) * (g.N / NT_BN);
     if (g_nt_variant == 0)
         hipLaunchKernelGGL(gemm_nt_bf16_kernel<0>, dim3(blocks), dim3(NT_THREADS), 0, s, g);

@@ -363,8 +363,9 @@ static void adam_flat_py(uintptr_t p, uintptr_t m, uintptr_t v, uintptr_t g, siz
 // bf16 NT GEMM (gemm_nt_bf16.hip): C = alpha * A[M][K] . B[N][K]^T with fused epilogue.
 static void gemm_nt_py(int M, int N, int K, uintptr_t A, int lda, uintptr_t B, int ldb, uintptr_t C, int ldc,
                        uintptr_t Cbf16, int ldcb, uintptr_t CbT, int ldct, uintptr_t bias, uintptr_t mask, int ldmask,
-                       int relu, float alpha, float beta, uintptr_t stream) {
+                       int relu, float alpha, float beta, uintptr_t stream, uintptr_t csum, int ldcs) {
     NTArgs g{};
+    g.csum = reinterpret_cast<float*>(csum); g.ldcs = ldcs;
     g.M = M; g.N = N; g.K = K;
     g.A = reinterpret_cast<const void*>(A); g.lda = lda;
     g.B = reinterpret_cast<const void*>(B); g.ldb = ldb;
@@ -416,7 +417,10 @@ void register_trainer(py::module_& m) {
     m.def("logits_confusion", &logits_confusion_py);
     m.def("colsum_split", &colsum_split_py);
     m.def("skinny_wgrad", &skinny_wgrad_py);
-    m.def("gemm_nt", &gemm_nt_py);
+    m.def("gemm_nt", &gemm_nt_py, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("B"),
+          py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("Cbf16"), py::arg("ldcb"), py::arg("CbT"), py::arg("ldct"),
+          py::arg("bias"), py::arg("mask"), py::arg("ldmask"), py::arg("relu"), py::arg("alpha"), py::arg("beta"),
+          py::arg("stream"), py::arg("csum") = 0, py::arg("ldcs") = 0);
     m.def("gemm_nt_set_variant", &gemm_nt_set_variant);
     m.def("gemm_nt_set_debug", [](uintptr_t p) { gemm_nt_set_debug(reinterpret_cast<unsigned long long*>(p)); });
     m.def("transpose_bf16", &transpose_bf16_py);

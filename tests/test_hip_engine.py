@@ -368,6 +368,45 @@ def test_gemm_nt_bf16_epilogue_configs(cfg):
         assert torch.equal(a, b)
 
 
+def test_gemm_nt_bf16_dgrad_column_sums():
+    """NT_EPI_CSUM: the dgrad epilogue's per-128-row column sums of its bf16 output (bias
+    gradient) fold to torch's column sums of the same output; the other outputs are unchanged,
+    and the 128x128 loop refuses the option."""
+    m = native()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    M, N, K = 1024, 512, 320
+    torch.manual_seed(9)
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    B = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    mask = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    outs = []
+    for csum in (False, True):
+        Cb = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        CbT = torch.zeros(N, M, dtype=torch.bfloat16, device=dev)
+        cs = torch.full((M // 128, N), float("nan"), device=dev)
+        m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, CbT.data_ptr(), M, 0,
+                  mask.data_ptr(), N, 0, 1.0, 0.0, s, cs.data_ptr() if csum else 0, N)
+        torch.cuda.synchronize()
+        outs.append((Cb, CbT, cs))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    cs = outs[1][2]
+    ref = outs[1][0].float().view(M // 128, 128, N).sum(1)
+    assert torch.isfinite(cs).all()
+    assert ((cs - ref).abs().max() / ref.abs().max()).item() < 1e-5
+    gb = torch.zeros(N, device=dev)
+    m.colsum(cs.data_ptr(), M // 128, N, N, gb.data_ptr(), 0.0, s)
+    torch.cuda.synchronize()
+    assert ((gb - ref.sum(0)).abs().max() / ref.sum(0).abs().max()).item() < 1e-5
+    try:
+        m.gemm_nt_set_variant(1)
+        with pytest.raises(RuntimeError):
+            m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, outs[0][0].data_ptr(), N, 0, 0, 0,
+                      mask.data_ptr(), N, 0, 1.0, 0.0, s, cs.data_ptr(), N)
+    finally:
+        m.gemm_nt_set_variant(3)
+
+
 @pytest.mark.parametrize("M,N,beta", [(16384, 2, 0.0), (5000, 14, 1.0), (300, 50, 0.5), (700, 100, 1.0)])
 def test_colsum_vs_torch(M, N, beta):
     """Bias-gradient column sums (flat few-column kernel for N <= 64, wave-per-64-columns otherwise)."""
