@@ -36,12 +36,13 @@ __device__ __forceinline__ void slab_store(float* p, float v) {
 
 // fp16 slab of the bf16 kernels: per-workgroup partial sums of the UNscaled gradient (deltas
 // p - onehot, not (p - onehot) / n: |partial| <= rows x max|activation|, far inside fp16's range
-// for these models; clamped so an outlier saturates instead of becoming inf), rounded to fp16
-// (11 significant bits -- finer than the bf16 operands the partials are computed from) and
-// summed in fp32 by the Adam kernel, which applies the 1/n.  Half the bytes of the fp32 slab,
-// which is written and read back once per round.
+// for these models; clamped so an outlier saturates instead of becoming inf, while a NaN stays
+// NaN -- fmaxf would turn it into the clamp bound -- so the debug mode's non-finite check still
+// sees it), rounded to fp16 (11 significant bits -- finer than the bf16 operands the partials
+// are computed from) and summed in fp32 by the Adam kernel, which applies the 1/n.  Half the
+// bytes of the fp32 slab, which is written and read back once per round.
 __device__ __forceinline__ void slab_store_h(uint16_t* p, float v) {
-    const float c = fminf(fmaxf(v, -65504.f), 65504.f);
+    const float c = v == v ? fminf(fmaxf(v, -65504.f), 65504.f) : v;
     const _Float16 h = (_Float16)c;
     __builtin_nontemporal_store(*reinterpret_cast<const uint16_t*>(&h), p);
 }

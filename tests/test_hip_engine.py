@@ -510,6 +510,15 @@ def test_hip_debug_mode_and_profile():
     g = HipRoundEngine(X, y, 2, cfg, None, bad)
     with pytest.raises(FloatingPointError):
         g.run(1)
+    # bf16 kernels with the fp16 gradient slab: a NaN gradient partial stays NaN (it is not
+    # clamped to a finite bound), so the debug check sees it
+    Xn = X.copy()
+    Xn[5, 3] = np.nan
+    h = HipRoundEngine(Xn, y, 2, EngineConfig(max_rounds=20, debug=True, early_stop=False, dtype="bf16",
+                                              grad_slab="fp16"), None, init_flat([14, 50, 200, 2], 1))
+    assert h.slab_f16
+    with pytest.raises(FloatingPointError):
+        h.run(1)
 
 
 @pytest.mark.parametrize("R", [16, 32, 64])
