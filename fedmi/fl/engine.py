@@ -824,6 +824,12 @@ class HipRoundEngine(RoundEngineBase):
         r = self.rounds_issued
         s = self._stream()
         self.engine.finalize(r, s)
+        self.read_history()
+
+    def read_history(self) -> None:
+        """Copy the device history of the rounds issued into ``hist`` (after a finalize of
+        ``rounds_issued``: this engine's ``sync_history`` or its trial batch's)."""
+        r = self.rounds_issued
         st = self._read_state((r + 1) & 1)   # synchronizes the engine stream
         n = int(st["finalized"])
         self.hist.rounds_run = n

@@ -9,9 +9,12 @@ run of the [C] workload (``FL_CustomMLPCLassifierImplementation_Multiple_Rounds.
 with its own hidden sizes, learning rate and local steps per round, and a
 :class:`FedTrialGroup` runs K trials concurrently on every GPU:
 
-* each trial is a fused :class:`~fedmi.fl.engine.HipRoundEngine` on its own HIP stream, so
-  the small per-trial kernels of different trials overlap on the CUs, and a whole group
-  round (all trials, fork/join, shared all-reduce) is one captured HIP graph;
+* each trial is a fused :class:`~fedmi.fl.engine.HipRoundEngine`; trials of the same shape
+  (layer sizes, dtype) form a native ``TrialBatch`` that runs every kernel of a round ONCE
+  for all of them, with a trial grid dimension (K x 250 workgroups instead of K launches of
+  250 on a 256-CU chip; ``fl_engine.cpp``), different shapes run their batches on their own
+  HIP streams, and a whole group round (all batches, fork/join, shared all-reduce) is one
+  captured HIP graph;
 * all trials' FedAvg buffers are slices of ONE device allocation, so a round of all K
   trials costs one all-reduce (the per-trial weights, metric tails and early-stop inputs
   ride together), instead of K latency-bound collectives;
@@ -75,7 +78,8 @@ class FedTrialGroup:
     round's train kernel, no all-reduce); several: classic rounds sharing one collective."""
 
     def __init__(self, X, y, n_classes: int, trials: Sequence[FedTrial], comm, base: EngineConfig,
-                 n_total: Optional[int] = None, backend: str = "auto", seed: int = 0, group_graph_rounds: int = 16):
+                 n_total: Optional[int] = None, backend: str = "auto", seed: int = 0, group_graph_rounds: int = 16,
+                 batched: bool = True):
         self.trials = list(trials)
         self.comm = comm
         self.world = comm.size if comm is not None else 1
@@ -107,6 +111,17 @@ class FedTrialGroup:
             self.stream = torch.cuda.Stream(device=dev)
             self.stream.wait_stream(torch.cuda.current_stream(dev))
             self._native = comm.native if (comm is not None and self.world > 1) else None
+            # trial batches: same-shape engines, local steps descending (TrialBatch's order)
+            self.batches = []
+            if batched:
+                from ..ops import native
+                groups: Dict[tuple, List[int]] = {}
+                for i, t in enumerate(self.trials):
+                    groups.setdefault((tuple(t.hidden), self.engines[i].cfg.dtype), []).append(i)
+                for idx in groups.values():
+                    idx = sorted(idx, key=lambda i: -self.engines[i].cfg.local_steps)
+                    tb = native().TrialBatch([self.engines[i].engine for i in idx])
+                    self.batches.append((tb, idx, torch.cuda.Stream(device=dev)))
         elif backend == "torch":
             for cfg, flat in zip(cfgs, flats):
                 self.engines.append(TorchRoundEngine(X, y, n_classes, cfg, comm, flat, n_total=n_total))
@@ -117,14 +132,24 @@ class FedTrialGroup:
     # ---- HIP rounds ----
     def _issue_group_round(self, r: int) -> None:
         """Round r of every trial on the group stream (fork/join), plus the shared all-reduce."""
-        for e in self.engines:
-            e.stream.wait_stream(self.stream)
-            if self.world == 1:
-                e.engine.run(r, 1, e._stream(), None, close=False)   # fused evaluation round
-            else:
-                e.engine.run_local(r, e._stream())                   # classic round, no collective
-        for e in self.engines:
-            self.stream.wait_stream(e.stream)
+        if self.batches:
+            for tb, _, st in self.batches:
+                st.wait_stream(self.stream)
+                if self.world == 1:
+                    tb.run(r, 1, st.cuda_stream, close=False)   # fused evaluation rounds
+                else:
+                    tb.run_local(r, st.cuda_stream)              # classic rounds, no collective
+            for _, _, st in self.batches:
+                self.stream.wait_stream(st)
+        else:
+            for e in self.engines:
+                e.stream.wait_stream(self.stream)
+                if self.world == 1:
+                    e.engine.run(r, 1, e._stream(), None, close=False)   # fused evaluation round
+                else:
+                    e.engine.run_local(r, e._stream())                   # classic round, no collective
+            for e in self.engines:
+                self.stream.wait_stream(e.stream)
         if self.world > 1:
             buf = self.buffers[(r + 1) & 1]
             with torch.cuda.stream(self.stream):
@@ -138,6 +163,23 @@ class FedTrialGroup:
 
     def _steady(self) -> bool:
         return not any(e.engine.needs_eager_round() for e in self.engines)
+
+    def _sync_histories(self) -> None:
+        """Fold the pending metrics of every trial (one batched finalize per batch) and read
+        the histories."""
+        if self.batches:
+            r = self.rounds_issued_dev
+            for tb, _, st in self.batches:
+                st.wait_stream(self.stream)
+                tb.finalize(r, st.cuda_stream)
+                self.stream.wait_stream(st)
+            self.stream.synchronize()
+            for e in self.engines:
+                e.read_history()
+        else:
+            for e in self.engines:
+                e.stream.wait_stream(self.stream)
+                e.sync_history()
 
     def _capture(self) -> None:
         g = torch.cuda.CUDAGraph()
@@ -161,10 +203,9 @@ class FedTrialGroup:
                 r += 1
             for e in self.engines:
                 e.rounds_issued = r
+        self.rounds_issued_dev = r
         self.stream.synchronize()
-        for e in self.engines:
-            e.stream.wait_stream(self.stream)
-            e.sync_history()
+        self._sync_histories()
 
     def run(self, n_rounds: int) -> None:
         """Run ``n_rounds`` rounds of every trial (trials that stopped early idle)."""

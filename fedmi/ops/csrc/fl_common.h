@@ -235,6 +235,29 @@ struct FLBuffers {
 #define FL_CM_FLAG (FL_MAX_CLASSES * FL_MAX_CLASSES)
 #define FL_CM_INTS (FL_CM_FLAG + 4)
 
+// Trial batches (BASELINE config 5, fedmi/hpo/fed_sweep.py): K engines of the same shape --
+// same layer sizes, R, rows (one client's shard), dtype -- that differ in hyperparameters (lr,
+// local steps, FedProx mu, ...) advance in lock-step, and every kernel of a round runs ONCE for
+// all of them with a trial grid dimension (blockIdx.y = trial) instead of K launches.  Each
+// trial's configuration, buffers and the pointer bases its launches refer to sit in a device
+// table; a launch names each pointer argument as (base slot, byte offset), the same for every
+// trial of the batch (the recording engine checks that, fl_engine.cpp TrialBatch).
+#define FL_TB_BASES 8
+enum { FL_TB_PBUF0 = 0, FL_TB_PBUF1, FL_TB_ST0, FL_TB_ST1, FL_TB_LOCAL, FL_TB_LAG, FL_TB_PKG, FL_TB_PKL };
+struct FLTrialDesc {
+    FLConfig c;
+    FLBuffers b;
+    char* base[FL_TB_BASES];
+};
+struct FLSel {
+    int base;        // FL_TB_* slot, -1 = nullptr
+    int pad;
+    long long off;   // bytes
+};
+__host__ __device__ inline char* fl_sel(const FLTrialDesc& t, FLSel s) {
+    return s.base < 0 ? nullptr : t.base[s.base] + s.off;
+}
+
 struct PeerArgs;  // peer_device.h
 struct PeerPack;
 // Launchers (fl_kernels.hip). `pg` = image the round trains from (the previous round's
@@ -278,6 +301,26 @@ hipError_t fl_launch_eval_fedavg_bf16(const MLPDesc& d, const MLPDescB& e, const
                                       const float* params, float* comm, const FLState* st, const PeerArgs& a,
                                       const PeerPack& pk, hipStream_t s);
 hipError_t fl_launch_pack_bf16(const MLPDesc& d, const MLPDescB& e, const float* params, char* out, hipStream_t s);
+// Batched launches of K trials (FLTrialDesc table `T`, K = gridDim.y): the same kernels, every
+// pointer argument a selector into the trial's bases.  `cm` of the train launch and `comm` of
+// the eval launch follow the single-trial launchers (the eval's confusion slots are derived
+// from `comm` per trial).
+hipError_t fl_launch_train_batch(const MLPDesc& d, int R, int n_slabs, const FLTrialDesc* T, int K, FLSel pg,
+                                 FLSel si, FLSel so, int ls, int mode, FLSel cm, int fold_mask, hipStream_t s);
+hipError_t fl_launch_train_bf16_batch(const MLPDesc& d, const MLPDescB& e, int R, int n_slabs, const FLTrialDesc* T,
+                                      int K, FLSel pg, FLSel si, FLSel so, int ls, int stage_local, int mode, FLSel cm,
+                                      int fold_mask, hipStream_t s);
+hipError_t fl_launch_adam_batch(const MLPDesc& d, const MLPDescB* e, const FLTrialDesc* T, int K, FLSel pin,
+                                FLSel anchor, FLSel comm, FLSel st, int local_step, FLSel st_out, int fold, int tail_a,
+                                int fold_mask, hipStream_t s);
+hipError_t fl_launch_eval_batch(const MLPDesc& d, int R, int n_rows, const FLTrialDesc* T, int K, FLSel params,
+                                FLSel comm, FLSel st, hipStream_t s);
+hipError_t fl_launch_eval_bf16_batch(const MLPDesc& d, const MLPDescB& e, int R, int n_rows, const FLTrialDesc* T,
+                                     int K, FLSel params, FLSel comm, FLSel st, hipStream_t s);
+hipError_t fl_launch_pack_bf16_batch(const MLPDesc& d, const MLPDescB& e, const FLTrialDesc* T, int K, FLSel params,
+                                     FLSel out, hipStream_t s);
+hipError_t fl_launch_finalize_batch(const MLPDesc& d, const FLTrialDesc* T, int K, FLSel pg, FLSel si, FLSel so,
+                                    int mask, hipStream_t s);
 // Stand-alone forward + confusion on an arbitrary row set (held-out evaluation).
 hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const int* y, int n_rows,
                                const float* params, float* cm_out, hipStream_t s);

@@ -115,7 +115,20 @@ class RcclComm {
 // ---------------------------------------------------------------------------------------
 // Engine
 // ---------------------------------------------------------------------------------------
+class TrialBatch;
+
+// One launch of a round, as recorded for a trial batch (TrialBatch below) instead of issued.
+struct FLLaunchRec {
+    enum Kind { PACK, TRAIN, ADAM, EVAL, FINALIZE };
+    int kind;
+    int i[4];           // TRAIN: ls, stage_local, mode, fold_mask | ADAM: ls, fold, tail_a, fold_mask |
+                        // FINALIZE: mask
+    const void* p[5];   // pointer arguments in launcher order
+};
+
 class FLEngine {
+    friend class TrialBatch;
+
   public:
     FLEngine(std::vector<int> dims, py::dict cfg, py::dict bufs) {
         const int L = (int)dims.size() - 1;
@@ -272,7 +285,10 @@ class FLEngine {
         if (prev_lagged_)
             throw std::runtime_error("finalize: the last round is lagged (its metrics need one more round)");
         const int mask = (prev_scored_ && !prev_afold_ ? FL_FOLD_A : 0) | FL_FOLD_B;
-        HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s, mask));
+        if (rec_ != nullptr)
+            rec_->push_back({FLLaunchRec::FINALIZE, {mask, 0, 0, 0}, {pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1]}});
+        else
+            HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s, mask));
         cm_in_tail_ = false;
     }
 
@@ -488,7 +504,10 @@ class FLEngine {
     void launch_train(const float* pg, const FLState* si, FLState* so, int ls, hipStream_t s,
                       int mode = FL_EVAL_CLASSIC, float* cm_out = nullptr, int fold_mask = FL_FOLD_B) {
         if (dtype_ == 0) {
-            HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s, mode, cm_out, fold_mask));
+            if (rec_ != nullptr)
+                rec_->push_back({FLLaunchRec::TRAIN, {ls, 0, mode, fold_mask}, {pg, si, so, cm_out}});
+            else
+                HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s, mode, cm_out, fold_mask));
         } else {
             // the round's input weights -> packed bf16 image.  With one client the FedAvg
             // output IS the local model (agg_scale = 1), which the Adam kernel already packed,
@@ -497,6 +516,12 @@ class FLEngine {
             const bool solo = c_.world == 1 && c_.agg_scale == 1.0f && !need_pack_;
             // the peer all-reduce already wrote the packed image of its output
             const bool packed = solo || (peer_ != nullptr && !need_pack_);
+            if (rec_ != nullptr) {
+                if (ls == 0 && !packed) rec_->push_back({FLLaunchRec::PACK, {0, 0, 0, 0}, {pg, b_.pk_global}});
+                rec_->push_back({FLLaunchRec::TRAIN, {ls, solo ? 1 : 0, mode, fold_mask}, {pg, si, so, cm_out}});
+                need_pack_ = false;
+                return;
+            }
             if (ls == 0 && !packed) HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
             need_pack_ = false;
             HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo, mode, cm_out, fold_mask));
@@ -505,10 +530,19 @@ class FLEngine {
     void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
                      hipStream_t s, FLState* st_out = nullptr, int fold = 0, int tail_a = 0,
                      int fold_mask = FL_FOLD_B, const PeerArgs* peer = nullptr, int wx = 0, int afold = 0) {
+        if (rec_ != nullptr) {
+            if (peer != nullptr || wx || afold) throw std::runtime_error("trial batch: no in-kernel exchange");
+            rec_->push_back({FLLaunchRec::ADAM, {ls, fold, tail_a, fold_mask}, {pin, anchor, comm, st, st_out}});
+            return;
+        }
         HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr, st_out,
                                  fold, tail_a, fold_mask, peer, wx, afold));
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
+        if (rec_ != nullptr) {
+            rec_->push_back({FLLaunchRec::EVAL, {0, 0, 0, 0}, {params, comm, st}});
+            return;
+        }
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
         else HIP_CHECK(fl_launch_eval_bf16(d_, ev_, c_, b_, params, comm, st, s));
     }
@@ -610,6 +644,7 @@ class FLEngine {
         return eval_fedavg_ && 2 * lds <= (size_t)160 * 1024;
     }
     void issue_eval_fedavg(int r, hipStream_t s) {
+        if (rec_ != nullptr) throw std::runtime_error("trial batch: no peer all-reduce");
         const int p = (r + 1) & 1;
         const PeerArgs a = peer_->args(p, pbuf_[p], d_.Pimg);
         PeerPack pk;
@@ -654,6 +689,194 @@ class FLEngine {
     hipGraph_t graph_ = nullptr;
     hipGraphExec_t exec_ = nullptr;
     int graph_rounds_ = 0;
+    std::vector<FLLaunchRec>* rec_ = nullptr;  // TrialBatch: record launches instead of issuing them
+};
+
+// ---------------------------------------------------------------------------------------
+// Trial batch (fl_common.h FLTrialDesc): K engines of one shape run every kernel of a round as
+// ONE launch with a trial grid dimension.  Each engine's round logic (state machine, modes,
+// buffer parities) runs unchanged in recording mode; the recorded launches of the K engines
+// are matched launch by launch and issued batched.  Engines are ordered by local steps,
+// descending, so the trials taking part in a later local step are a prefix of the table.
+// ---------------------------------------------------------------------------------------
+class TrialBatch {
+  public:
+    explicit TrialBatch(std::vector<FLEngine*> engs) : engs_(std::move(engs)) {
+        K_ = (int)engs_.size();
+        if (K_ < 1) throw std::runtime_error("TrialBatch: no engines");
+        const FLEngine& a = *engs_[0];
+        for (int k = 0; k < K_; ++k) {
+            const FLEngine& e = *engs_[k];
+            if (e.peer_ != nullptr) throw std::runtime_error("TrialBatch: engines must not use the peer all-reduce");
+            if (e.dtype_ != a.dtype_ || std::memcmp(&e.d_, &a.d_, sizeof(MLPDesc)) != 0 ||
+                (a.dtype_ == 1 && (std::memcmp(&e.e_, &a.e_, sizeof(MLPDescB)) != 0 ||
+                                   std::memcmp(&e.ev_, &a.ev_, sizeof(MLPDescB)) != 0)))
+                throw std::runtime_error("TrialBatch: engines differ in shape or dtype");
+            if (e.c_.R != a.c_.R || e.c_.n_rows != a.c_.n_rows || e.c_.world != a.c_.world ||
+                e.c_.rank != a.c_.rank || e.c_.slab_f16 != a.c_.slab_f16 || e.c_.lag_off != a.c_.lag_off ||
+                e.fused_ != a.fused_ || e.lagged() != a.lagged() || e.emulate_ != a.emulate_)
+                throw std::runtime_error("TrialBatch: engines differ in rows, clients or round kind");
+            if (k > 0 && e.c_.local_steps > engs_[k - 1]->c_.local_steps)
+                throw std::runtime_error("TrialBatch: order the engines by local steps, descending");
+        }
+        HIP_CHECK(hipMalloc(&dT_, sizeof(FLTrialDesc) * K_));
+        upload(nullptr);
+    }
+    ~TrialBatch() {
+        if (dT_) (void)hipFree(dT_);
+    }
+    int size() const { return K_; }
+
+    // Rounds [r0, r0 + n) of every trial (FLEngine::run without a communicator).
+    void run(int r0, int n, uintptr_t stream, bool close) {
+        for (int r = r0; r < r0 + n; ++r) {
+            const bool last = close && r == r0 + n - 1;
+            issue([&](FLEngine* e) { e->run(r, 1, stream, nullptr, last); }, as_stream(stream));
+        }
+    }
+    // Local part of round r of every trial (the caller reduces the trials' shared buffer).
+    void run_local(int r, uintptr_t stream) {
+        issue([&](FLEngine* e) { e->run_local(r, stream); }, as_stream(stream));
+    }
+    void finalize(int r, uintptr_t stream) {
+        issue([&](FLEngine* e) { e->finalize(r, stream); }, as_stream(stream));
+    }
+    bool needs_eager_round() const {
+        for (auto* e : engs_)
+            if (e->needs_eager_round()) return true;
+        return false;
+    }
+
+  private:
+    void build_table(std::vector<FLTrialDesc>& T) const {
+        T.assign(K_, FLTrialDesc{});
+        for (int k = 0; k < K_; ++k) {
+            const FLEngine& e = *engs_[k];
+            T[k].c = e.c_;
+            T[k].b = e.b_;
+            char* const bases[FL_TB_BASES] = {(char*)e.pbuf_[0], (char*)e.pbuf_[1], (char*)e.st_[0], (char*)e.st_[1],
+                                              (char*)e.b_.local, (char*)e.lagbuf_, e.b_.pk_global, e.b_.pk_local};
+            std::memcpy(T[k].base, bases, sizeof(bases));
+        }
+    }
+    // (re)upload the table when an engine's configuration changed (e.g. set_early_stop);
+    // never inside a stream capture
+    void upload(hipStream_t s) {
+        std::vector<FLTrialDesc> T;
+        build_table(T);
+        if (!host_.empty() && std::memcmp(T.data(), host_.data(), sizeof(FLTrialDesc) * K_) == 0) return;
+        if (s != nullptr) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            HIP_CHECK(hipStreamIsCapturing(s, &cs));
+            if (cs != hipStreamCaptureStatusNone)
+                throw std::runtime_error("TrialBatch: a trial's configuration changed during a graph capture");
+            HIP_CHECK(hipStreamSynchronize(s));  // kernels still reading the old table
+        }
+        HIP_CHECK(hipMemcpy(dT_, T.data(), sizeof(FLTrialDesc) * K_, hipMemcpyHostToDevice));
+        host_ = std::move(T);
+    }
+    size_t base_bytes(const FLEngine& e, int i) const {
+        switch (i) {
+            case FL_TB_PBUF0: case FL_TB_PBUF1: return (size_t)e.comm_len_ * sizeof(float);
+            case FL_TB_ST0: case FL_TB_ST1: return sizeof(FLState);
+            case FL_TB_LOCAL: return (size_t)e.d_.Pimg * sizeof(float);
+            case FL_TB_LAG: return (FL_MAX_CLASSES * FL_MAX_CLASSES + 4) * sizeof(float);
+            default: return e.dtype_ == 1 ? (size_t)e.e_.param_bytes : 0;
+        }
+    }
+    FLSel resolve(int k, const void* p) const {
+        FLSel sel = {-1, 0, 0};
+        if (p == nullptr) return sel;
+        const char* q = static_cast<const char*>(p);
+        for (int i = 0; i < FL_TB_BASES; ++i) {
+            const char* b0 = host_[k].base[i];
+            if (b0 != nullptr && q >= b0 && q < b0 + base_bytes(*engs_[k], i)) {
+                sel.base = i;
+                sel.off = (long long)(q - b0);
+                return sel;
+            }
+        }
+        throw std::runtime_error("TrialBatch: launch argument outside the trial's buffers");
+    }
+    static bool same_launch(const FLLaunchRec& a, const FLLaunchRec& b) {
+        return a.kind == b.kind && std::memcmp(a.i, b.i, sizeof(a.i)) == 0;
+    }
+
+    template <class F>
+    void issue(F&& per_engine, hipStream_t s) {
+        upload(s);
+        std::vector<std::vector<FLLaunchRec>> recs(K_);
+        for (int k = 0; k < K_; ++k) {
+            engs_[k]->rec_ = &recs[k];
+            try {
+                per_engine(engs_[k]);
+            } catch (...) {
+                engs_[k]->rec_ = nullptr;
+                throw;
+            }
+            engs_[k]->rec_ = nullptr;
+        }
+        const FLEngine& e0 = *engs_[0];
+        std::vector<size_t> pos(K_, 0);
+        for (const FLLaunchRec& m : recs[0]) {
+            // trials whose next recorded launch is this one: a prefix of the table
+            int cnt = 0;
+            for (int k = 0; k < K_; ++k) {
+                const bool match = pos[k] < recs[k].size() && same_launch(recs[k][pos[k]], m);
+                if (match && k != cnt) throw std::runtime_error("TrialBatch: launch sequences do not align");
+                if (match) ++cnt;
+            }
+            FLSel sel[5];
+            for (int a = 0; a < 5; ++a) {
+                sel[a] = resolve(0, m.p[a]);
+                for (int k = 1; k < cnt; ++k) {
+                    const FLSel o = resolve(k, recs[k][pos[k]].p[a]);
+                    if (o.base != sel[a].base || o.off != sel[a].off)
+                        throw std::runtime_error("TrialBatch: trials disagree on a launch argument");
+                }
+            }
+            for (int k = 0; k < cnt; ++k) ++pos[k];
+            launch(e0, m, sel, cnt, s);
+        }
+        for (int k = 0; k < K_; ++k)
+            if (pos[k] != recs[k].size()) throw std::runtime_error("TrialBatch: launch sequences do not align");
+    }
+    void launch(const FLEngine& e, const FLLaunchRec& m, const FLSel* sel, int cnt, hipStream_t s) {
+        const FLConfig& c = e.c_;
+        switch (m.kind) {
+            case FLLaunchRec::PACK:
+                HIP_CHECK(fl_launch_pack_bf16_batch(e.d_, e.e_, dT_, cnt, sel[0], sel[1], s));
+                break;
+            case FLLaunchRec::TRAIN:
+                if (e.dtype_ == 0)
+                    HIP_CHECK(fl_launch_train_batch(e.d_, c.R, c.n_slabs, dT_, cnt, sel[0], sel[1], sel[2], m.i[0],
+                                                    m.i[2], sel[3], m.i[3], s));
+                else
+                    HIP_CHECK(fl_launch_train_bf16_batch(e.d_, e.e_, c.R, c.n_slabs, dT_, cnt, sel[0], sel[1], sel[2],
+                                                         m.i[0], m.i[1], m.i[2], sel[3], m.i[3], s));
+                break;
+            case FLLaunchRec::ADAM:
+                HIP_CHECK(fl_launch_adam_batch(e.d_, e.dtype_ == 1 ? &e.e_ : nullptr, dT_, cnt, sel[0], sel[1], sel[2],
+                                               sel[3], m.i[0], sel[4], m.i[1], m.i[2], m.i[3], s));
+                break;
+            case FLLaunchRec::EVAL:
+                if (e.dtype_ == 0)
+                    HIP_CHECK(fl_launch_eval_batch(e.d_, c.R, c.n_rows, dT_, cnt, sel[0], sel[1], sel[2], s));
+                else
+                    HIP_CHECK(fl_launch_eval_bf16_batch(e.d_, e.ev_, c.R, c.n_rows, dT_, cnt, sel[0], sel[1], sel[2],
+                                                        s));
+                break;
+            case FLLaunchRec::FINALIZE:
+                HIP_CHECK(fl_launch_finalize_batch(e.d_, dT_, cnt, sel[0], sel[1], sel[2], m.i[0], s));
+                break;
+            default: throw std::runtime_error("TrialBatch: unknown launch");
+        }
+    }
+
+    std::vector<FLEngine*> engs_;
+    int K_ = 0;
+    FLTrialDesc* dT_ = nullptr;
+    std::vector<FLTrialDesc> host_;
 };
 
 // Thin wrappers used by tests and the synthetic-data path.
@@ -714,6 +937,13 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);
+    py::class_<TrialBatch>(m, "TrialBatch")
+        .def(py::init<std::vector<FLEngine*>>(), py::keep_alive<1, 2>())
+        .def("run", &TrialBatch::run, py::arg("r0"), py::arg("n"), py::arg("stream"), py::arg("close") = true)
+        .def("run_local", &TrialBatch::run_local)
+        .def("finalize", &TrialBatch::finalize)
+        .def("needs_eager_round", &TrialBatch::needs_eager_round)
+        .def_property_readonly("size", &TrialBatch::size);
     m.def("synth", &synth, py::arg("X"), py::arg("y"), py::arg("n"), py::arg("F"), py::arg("seed"), py::arg("off"),
           py::arg("w1"), py::arg("w2"), py::arg("H"), py::arg("stream"), py::arg("label_noise") = 0.f);
     m.def("device_info", &device_info);

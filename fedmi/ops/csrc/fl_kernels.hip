@@ -291,11 +291,13 @@ __device__ void forward_block(const MLPDesc& d, float* acts, const float* li, un
 // ---------------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------------
+// (one body, two entry points: the single-engine kernel takes its arguments as kernel
+// arguments, the trial-batch kernel from the FLTrialDesc table row of blockIdx.y)
 template <int RT>
-__global__ void __launch_bounds__(FL_THREADS)
-fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
-                const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step, int mode,
-                float* __restrict__ cm_out, int fold_mask) {
+__device__ __forceinline__ void
+fl_train_body(const MLPDesc& d, const FLConfig c, const FLBuffers b, const float* __restrict__ pg,
+              const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step, int mode,
+              float* __restrict__ cm_out, int fold_mask) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
@@ -399,6 +401,24 @@ fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg
     FL_STAMP(15);
 }
 
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
+                const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step, int mode,
+                float* __restrict__ cm_out, int fold_mask) {
+    fl_train_body<RT>(d, c, b, pg, st_in, st_out, local_step, mode, cm_out, fold_mask);
+}
+
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_train_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pg, FLSel si, FLSel so, int local_step,
+                      int mode, FLSel cm, int fold_mask) {
+    const FLTrialDesc& t = T[blockIdx.y];
+    fl_train_body<RT>(d, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, pg)),
+                      reinterpret_cast<const FLState*>(fl_sel(t, si)), reinterpret_cast<FLState*>(fl_sel(t, so)),
+                      local_step, mode, reinterpret_cast<float*>(fl_sel(t, cm)), fold_mask);
+}
+
 // Slab reduction + Adam + StepLR + FedAvg pre-scale.  Block = 16 waves x 64 DENSE
 // parameters: wave w sums slab rows w, w+16, ... of its 64 columns with 16 rows in flight
 // per lane (one 4-byte load per row would leave ~1 KB in flight per wave: latency bound);
@@ -466,12 +486,12 @@ __device__ __forceinline__ float adam_update(const FLConfig& c, const FLBuffers&
 
 // Block 0 is the tail block (dispatched first: with the in-kernel fold every other block may
 // wait for its lag chunk); blocks 1.. own 64 dense parameters each.
-__global__ void __launch_bounds__(ADAM_WAVES * 64)
-fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
-               const float* __restrict__ anchor, float* __restrict__ comm,
-               const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
-               FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, PeerArgs pa, int xchg,
-               int afold) {
+__device__ __forceinline__ void
+fl_adam_body(const MLPDesc& d, const FLConfig c, const FLBuffers b, const float* __restrict__ pin,
+             const float* __restrict__ anchor, float* __restrict__ comm,
+             const FLState* __restrict__ st, int local_step, const MLPDescB& e, int pack,
+             FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, const PeerArgs& pa, int xchg,
+             int afold) {
     __shared__ float part[ADAM_WAVES][64];
     __shared__ FLState S_sh;
     __shared__ float lag_s[PEER_MAX_WORLD * (FL_MAX_CLASSES * FL_MAX_CLASSES + 1)];
@@ -713,6 +733,28 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
     FL_STAMP(15);
 }
 
+__global__ void __launch_bounds__(ADAM_WAVES * 64)
+fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
+               const float* __restrict__ anchor, float* __restrict__ comm,
+               const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
+               FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, PeerArgs pa, int xchg,
+               int afold) {
+    fl_adam_body(d, c, b, pin, anchor, comm, st, local_step, e, pack, st_out, fold, tail_a, fold_mask, pa, xchg,
+                 afold);
+}
+
+// Trial batch (no peer exchange: the trials' FedAvg is one shared collective outside).
+__global__ void __launch_bounds__(ADAM_WAVES * 64)
+fl_adam_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pin, FLSel anchor, FLSel comm, FLSel st,
+                     int local_step, MLPDescB e, int pack, FLSel st_out, int fold, int tail_a, int fold_mask) {
+    const FLTrialDesc& t = T[blockIdx.y];
+    const PeerArgs pa = {};
+    fl_adam_body(d, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, pin)),
+                 reinterpret_cast<const float*>(fl_sel(t, anchor)), reinterpret_cast<float*>(fl_sel(t, comm)),
+                 reinterpret_cast<const FLState*>(fl_sel(t, st)), local_step, e, pack,
+                 reinterpret_cast<FLState*>(fl_sel(t, st_out)), fold, tail_a, fold_mask, pa, 0, 0);
+}
+
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,
 // argmax, confusion counts into this rank's tail (exact: integer-valued fp32 < 2^24).
 template <int RT>
@@ -784,6 +826,27 @@ __global__ void fl_finalize_kernel(MLPDesc d, FLConfig c, FLBuffers b, const flo
     if (threadIdx.x != 0) return;
     S.live = 0;
     *st_out = S;
+}
+
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_eval_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel params, FLSel comm, FLSel st) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const FLTrialDesc& t = T[blockIdx.y];
+    const FLState* s = reinterpret_cast<const FLState*>(fl_sel(t, st));
+    if (s != nullptr && !s->live) return;
+    float* cm = reinterpret_cast<float*>(fl_sel(t, comm)) + t.c.tail_off + t.c.rank * t.c.tail_stride;
+    eval_rows<RT>(d, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, params)), cm, blockIdx.x, lds);
+}
+
+__global__ void fl_finalize_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pg, FLSel si, FLSel so,
+                                         int mask) {
+    const FLTrialDesc& t = T[blockIdx.y];
+    FLState S = finalize_state(d, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, pg)),
+                               *reinterpret_cast<const FLState*>(fl_sel(t, si)), true, mask);
+    if (threadIdx.x != 0) return;
+    S.live = 0;
+    *reinterpret_cast<FLState*>(fl_sel(t, so)) = S;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -944,6 +1007,61 @@ hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffe
     return hipGetLastError();
 }
 
+hipError_t fl_launch_train_batch(const MLPDesc& d, int R, int n_slabs, const FLTrialDesc* T, int K, FLSel pg,
+                                 FLSel si, FLSel so, int ls, int mode, FLSel cm, int fold_mask, hipStream_t s) {
+    if (K < 1 || mode == FL_EVAL_LAGGED || (mode == FL_EVAL_FUSED && cm.base < 0)) return hipErrorInvalidValue;
+    const dim3 grid(n_slabs, K);
+    switch (R) {
+        case 16:
+            hipLaunchKernelGGL(fl_train_batch_kernel<1>, grid, dim3(FL_THREADS), lds_bytes(d), s, d, T, pg, si, so,
+                               ls, mode, cm, fold_mask);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_train_batch_kernel<2>, grid, dim3(FL_THREADS), lds_bytes(d), s, d, T, pg, si, so,
+                               ls, mode, cm, fold_mask);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t fl_launch_adam_batch(const MLPDesc& d, const MLPDescB* e, const FLTrialDesc* T, int K, FLSel pin,
+                                FLSel anchor, FLSel comm, FLSel st, int local_step, FLSel st_out, int fold, int tail_a,
+                                int fold_mask, hipStream_t s) {
+    if (K < 1 || (fold && st_out.base < 0)) return hipErrorInvalidValue;
+    const int blocks = (d.P + 63) / 64 + 1;
+    MLPDescB ee = {};
+    if (e != nullptr) ee = *e;
+    hipLaunchKernelGGL(fl_adam_batch_kernel, dim3(blocks, K), dim3(ADAM_WAVES * 64), 0, s, d, T, pin, anchor, comm,
+                       st, local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask);
+    return hipGetLastError();
+}
+
+hipError_t fl_launch_eval_batch(const MLPDesc& d, int R, int n_rows, const FLTrialDesc* T, int K, FLSel params,
+                                FLSel comm, FLSel st, hipStream_t s) {
+    if (K < 1) return hipErrorInvalidValue;
+    const dim3 grid(nblocks(n_rows, R), K);
+    switch (R) {
+        case 16:
+            hipLaunchKernelGGL(fl_eval_batch_kernel<1>, grid, dim3(FL_THREADS), lds_bytes(d), s, d, T, params, comm,
+                               st);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_eval_batch_kernel<2>, grid, dim3(FL_THREADS), lds_bytes(d), s, d, T, params, comm,
+                               st);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t fl_launch_finalize_batch(const MLPDesc& d, const FLTrialDesc* T, int K, FLSel pg, FLSel si, FLSel so,
+                                    int mask, hipStream_t s) {
+    if (K < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fl_finalize_batch_kernel, dim3(1, K), dim3(64), 0, s, d, T, pg, si, so, mask);
+    return hipGetLastError();
+}
+
 hipError_t fl_launch_confusion(const MLPDesc& d, int R, const float* X, const int* y, int n_rows,
                                const float* params, float* cm_out, hipStream_t s) {
     FLConfig c = {};
@@ -978,7 +1096,9 @@ hipError_t fl_set_lds_limit(size_t bytes) {
     if (e == hipSuccess)                                                                                \
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, b)
     FL_SET(fl_train_kernel<1>); FL_SET(fl_train_kernel<2>);
+    FL_SET(fl_train_batch_kernel<1>); FL_SET(fl_train_batch_kernel<2>);
     FL_SET(fl_eval_kernel<1>); FL_SET(fl_eval_kernel<2>);
+    FL_SET(fl_eval_batch_kernel<1>); FL_SET(fl_eval_batch_kernel<2>);
     FL_SET(fl_eval_fedavg_kernel<1>); FL_SET(fl_eval_fedavg_kernel<2>);
 #undef FL_SET
     return e;

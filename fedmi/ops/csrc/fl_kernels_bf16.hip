@@ -67,7 +67,8 @@ __device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
 // fp32 global image (fl_common.h layout) -> packed bf16 parameter region (MLPDescB layout,
 // W_l then b_l, byte offsets relative to param_off).  One thread per 8-element item (two
 // float4 loads, one 16-byte store); rows/columns of padding come out zero.
-__global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restrict__ params, char* __restrict__ out) {
+__device__ __forceinline__ void fl_pack_bf16_body(const MLPDesc& d, const MLPDescB& e, const float* __restrict__ params,
+                                                  char* __restrict__ out) {
     const int id = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = e.item_base[d.L];
     if (id < total) {
@@ -102,6 +103,16 @@ __global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restri
         }
         bid -= e.kp[l + 1];
     }
+}
+
+__global__ void fl_pack_bf16_kernel(MLPDesc d, MLPDescB e, const float* __restrict__ params, char* __restrict__ out) {
+    fl_pack_bf16_body(d, e, params, out);
+}
+
+__global__ void fl_pack_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel params,
+                                          FLSel out) {
+    const FLTrialDesc& t = T[blockIdx.y];
+    fl_pack_bf16_body(d, e, reinterpret_cast<const float*>(fl_sel(t, params)), fl_sel(t, out));
 }
 
 // Stage the packed parameter region AND this block's input rows with every global load in
@@ -446,11 +457,13 @@ __device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDe
 // ---------------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------------
+// (one body, two entry points: the single-engine kernel and the trial-batch kernel, whose
+// configuration / buffers come from the FLTrialDesc table row of blockIdx.y)
 template <int RT>
-__global__ void __launch_bounds__(FL_THREADS)
-fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
-                     const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
-                     int stage_local, int mode, float* __restrict__ cm_out, int fold_mask) {
+__device__ __forceinline__ void
+fl_train_bf16_body(const MLPDesc& d, const MLPDescB& e, const FLConfig c, const FLBuffers b,
+                   const float* __restrict__ pg, const FLState* __restrict__ st_in, FLState* __restrict__ st_out,
+                   int local_step, int stage_local, int mode, float* __restrict__ cm_out, int fold_mask) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     __shared__ FLState S_sh;
     FL_STAMP(0);
@@ -591,6 +604,24 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
     FL_STAMP(15);
 }
 
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
+                     const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
+                     int stage_local, int mode, float* __restrict__ cm_out, int fold_mask) {
+    fl_train_bf16_body<RT>(d, e, c, b, pg, st_in, st_out, local_step, stage_local, mode, cm_out, fold_mask);
+}
+
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_train_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel pg, FLSel si, FLSel so,
+                           int local_step, int stage_local, int mode, FLSel cm, int fold_mask) {
+    const FLTrialDesc& t = T[blockIdx.y];
+    fl_train_bf16_body<RT>(d, e, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, pg)),
+                           reinterpret_cast<const FLState*>(fl_sel(t, si)), reinterpret_cast<FLState*>(fl_sel(t, so)),
+                           local_step, stage_local, mode, reinterpret_cast<float*>(fl_sel(t, cm)), fold_mask);
+}
+
 // Local evaluation of one row block (rows [blk*R, blk*R + R)) of the post-step model:
 // forward, argmax, confusion counts added to cm_out (exact: integer-valued fp32 < 2^24).
 template <int RT>
@@ -635,6 +666,18 @@ fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float*
     extern __shared__ __attribute__((aligned(16))) char lds[];
     if (st != nullptr && !st->live) return;
     eval_rows_bf16<RT>(d, e, c, b, params, cm_out, blockIdx.x, lds);
+}
+
+template <int RT>
+__global__ void __launch_bounds__(FL_THREADS)
+fl_eval_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel params, FLSel comm,
+                          FLSel st) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const FLTrialDesc& t = T[blockIdx.y];
+    const FLState* s = reinterpret_cast<const FLState*>(fl_sel(t, st));
+    if (s != nullptr && !s->live) return;
+    float* cm = reinterpret_cast<float*>(fl_sel(t, comm)) + t.c.tail_off + t.c.rank * t.c.tail_stride;
+    eval_rows_bf16<RT>(d, e, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, params)), cm, blockIdx.x, lds);
 }
 
 // Local evaluation + FedAvg in one kernel (world > 1, one-shot xGMI all-reduce;
@@ -737,6 +780,62 @@ hipError_t fl_launch_pack_bf16(const MLPDesc& d, const MLPDescB& e, const float*
     return hipGetLastError();
 }
 
+hipError_t fl_launch_train_bf16_batch(const MLPDesc& d, const MLPDescB& e, int R, int n_slabs, const FLTrialDesc* T,
+                                      int K, FLSel pg, FLSel si, FLSel so, int ls, int stage_local, int mode, FLSel cm,
+                                      int fold_mask, hipStream_t s) {
+    if (K < 1 || mode == FL_EVAL_LAGGED || (mode == FL_EVAL_FUSED && cm.base < 0)) return hipErrorInvalidValue;
+    const size_t lds = (size_t)e.lds_bytes;
+    const dim3 grid(n_slabs, K);
+    switch (R) {
+        case 16:
+            hipLaunchKernelGGL(fl_train_bf16_batch_kernel<1>, grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
+                               stage_local, mode, cm, fold_mask);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_train_bf16_batch_kernel<2>, grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
+                               stage_local, mode, cm, fold_mask);
+            break;
+        case 64:
+            hipLaunchKernelGGL(fl_train_bf16_batch_kernel<4>, grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
+                               stage_local, mode, cm, fold_mask);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t fl_launch_eval_bf16_batch(const MLPDesc& d, const MLPDescB& e, int R, int n_rows, const FLTrialDesc* T,
+                                     int K, FLSel params, FLSel comm, FLSel st, hipStream_t s) {
+    if (K < 1) return hipErrorInvalidValue;
+    const dim3 grid((n_rows + R - 1) / R, K);
+    switch (R) {
+        case 16:
+            hipLaunchKernelGGL(fl_eval_bf16_batch_kernel<1>, grid, dim3(FL_THREADS), e.lds_bytes, s, d, e, T, params,
+                               comm, st);
+            break;
+        case 32:
+            hipLaunchKernelGGL(fl_eval_bf16_batch_kernel<2>, grid, dim3(FL_THREADS), e.lds_bytes, s, d, e, T, params,
+                               comm, st);
+            break;
+        case 64:
+            hipLaunchKernelGGL(fl_eval_bf16_batch_kernel<4>, grid, dim3(FL_THREADS), e.lds_bytes, s, d, e, T, params,
+                               comm, st);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t fl_launch_pack_bf16_batch(const MLPDesc& d, const MLPDescB& e, const FLTrialDesc* T, int K, FLSel params,
+                                     FLSel out, hipStream_t s) {
+    if (K < 1) return hipErrorInvalidValue;
+    int bias_items = 0;
+    for (int l = 0; l < d.L; ++l) bias_items += e.kp[l + 1];
+    const int n = e.item_base[d.L] + bias_items;
+    hipLaunchKernelGGL(fl_pack_bf16_batch_kernel, dim3((n + 255) / 256, K), dim3(256), 0, s, d, e, T, params, out);
+    return hipGetLastError();
+}
+
 hipError_t fl_set_lds_limit_bf16(size_t bytes) {
     const int v = (int)bytes;
     hipError_t r = hipSuccess;
@@ -745,6 +844,9 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
     r = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, v)
     FLB_SET(fl_train_bf16_kernel<1>); FLB_SET(fl_train_bf16_kernel<2>); FLB_SET(fl_train_bf16_kernel<4>);
     FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>); FLB_SET(fl_eval_bf16_kernel<4>);
+    FLB_SET(fl_train_bf16_batch_kernel<1>); FLB_SET(fl_train_bf16_batch_kernel<2>);
+    FLB_SET(fl_train_bf16_batch_kernel<4>);
+    FLB_SET(fl_eval_bf16_batch_kernel<1>); FLB_SET(fl_eval_bf16_batch_kernel<2>); FLB_SET(fl_eval_bf16_batch_kernel<4>);
     FLB_SET(fl_eval_fedavg_bf16_kernel<1>); FLB_SET(fl_eval_fedavg_bf16_kernel<2>);
 #undef FLB_SET
     return r;

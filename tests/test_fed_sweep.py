@@ -52,20 +52,27 @@ def test_federated_sweep_entrypoint_two_clients_gloo():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_hip_group_matches_standalone_engines(dtype):
+@pytest.mark.parametrize("batched", [True, False])
+@pytest.mark.parametrize("fused", [True, False])
+def test_hip_group_matches_standalone_engines(dtype, batched, fused):
+    """Eager group rounds -- trial batches (one launch per kernel for every same-shape trial,
+    mixed local steps) or one stream per trial; fused or classic (separate eval kernel)
+    evaluation -- give every trial the history of its own engine run alone."""
     X, y = make_income_like(3000, seed=4)
     trials = grid([(50, 200), (16,)], [0.004, 0.01], [1, 2])
-    base = EngineConfig(max_rounds=12, early_stop=True, patience=3, tolerance=5e-3, dtype=dtype, graph_rounds=0)
-    g = FedTrialGroup(X, y, 2, trials, None, base, backend="hip")
+    base = EngineConfig(max_rounds=12, early_stop=True, patience=3, tolerance=5e-3, dtype=dtype, graph_rounds=0,
+                        fused_eval=fused)
+    g = FedTrialGroup(X, y, 2, trials, None, base, backend="hip", batched=batched)
+    assert len(g.batches) == (2 if batched else 0)
     g.run(12)
-    for t in (trials[0], trials[5], trials[7]):
-        cfg = EngineConfig(hidden=t.hidden, lr=t.lr, local_steps=t.local_steps, max_rounds=12, early_stop=True,
-                           patience=3, tolerance=5e-3, dtype=dtype, graph_rounds=0)
+    for t, ge in ((trials[0], g.engines[0]), (trials[5], g.engines[5]), (trials[7], g.engines[7])):
+        cfg = replace(base, hidden=t.hidden, lr=t.lr, local_steps=t.local_steps)
         e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *t.hidden, 2], 0))
         e.run(12)
         h = e.history()
         assert h["rounds_run"] == t.history["rounds_run"] and h["stop_round"] == t.history["stop_round"]
         np.testing.assert_array_equal(h["global"], t.history["global"])
+        np.testing.assert_array_equal(e.global_flat(), ge.global_flat())
 
 
 def test_reference_h_client_api_runs_grid_and_returns_best():
@@ -88,7 +95,8 @@ def test_reference_h_client_api_runs_grid_and_returns_best():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_group_graph_equals_standalone_engines(dtype):
+@pytest.mark.parametrize("batched", [True, False])
+def test_group_graph_equals_standalone_engines(dtype, batched):
     """One client: the packed group (K trials' rounds captured into one graph, fused
     evaluation) gives every trial bit-identical weights and history to its own engine run
     alone; early stopping inside the group is per trial."""
@@ -96,7 +104,7 @@ def test_group_graph_equals_standalone_engines(dtype):
     trials = grid([(16,), (24, 8)], [0.004, 0.02], [1, 2])
     base = EngineConfig(max_rounds=60, patience=3, tolerance=3e-3, dtype=dtype, graph_rounds=8)
     from fedmi.hpo.fed_sweep import FedTrialGroup
-    g = FedTrialGroup(X, y, 2, trials, None, base, group_graph_rounds=8)
+    g = FedTrialGroup(X, y, 2, trials, None, base, group_graph_rounds=8, batched=batched)
     g.run(3)     # eager rounds first, then graph replays from an odd start
     g.run(41)
     assert g.graph is not None

@@ -3,8 +3,10 @@
 {1,2}, 8000 rows, 100 rounds), for
 
   * sequential: one trial after another, each engine replaying its own 16-round HIP graphs;
-  * packed K:  K trials at once (fedmi.hpo.fed_sweep.FedTrialGroup: every trial on its own
-               stream, the whole K-trial round captured into ONE graph and replayed).
+  * packed K:  K trials at once (fedmi.hpo.fed_sweep.FedTrialGroup: same-shape trials as one
+               native trial batch -- every kernel of the round launched once for all of them --
+               shapes on their own streams, the whole K-trial round captured into ONE graph);
+  * streams K: the same without trial batches (every trial on its own stream, round-2 design).
 
     python tools/fed_sweep_bench.py [--rounds 100]
 """
@@ -26,9 +28,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=100)
     a = ap.parse_args()
     X, y = make_income_like(8000, seed=1)
-    trials = grid(((50, 200), (100, 50), (50, 100)), (0.002, 0.004), (1, 2))
+    mixed = grid(((50, 200), (100, 50), (50, 100)), (0.002, 0.004), (1, 2))
+    same = grid(((50, 200),), (0.001, 0.002, 0.003, 0.004, 0.006, 0.01), (1, 2))  # one shape: one batch of 12
     R = a.rounds
-    for dtype in ("fp32", "bf16"):
+    for name, trials, dtype in (("mixed", mixed, "fp32"), ("mixed", mixed, "bf16"), ("same-shape", same, "bf16")):
+        print(f"-- {name} grid: {len(trials)} trials, shapes {sorted({t.hidden for t in trials})}", flush=True)
         base = EngineConfig(max_rounds=R + 48, early_stop=False, dtype=dtype, graph_rounds=16)
         # warm-up: compile / first launches
         run_fed_sweep(X, y, 2, None, trials[:2], rounds=20, trials_per_gpu=2, base=base)
@@ -48,8 +52,9 @@ def main():
         seq = len(trials) * R / dt
         print(f"{dtype} sequential graph-replayed engines: {len(trials)} trials x {R} rounds in {dt * 1e3:.1f} ms "
               f"({seq:.0f} trial-rounds/s)", flush=True)
-        for k in (1, 4, 12):
-            groups = [FedTrialGroup(X, y, 2, trials[g:g + k], None, base) for g in range(0, len(trials), k)]
+        for k, batched in ((1, True), (4, True), (12, True), (12, False)):
+            groups = [FedTrialGroup(X, y, 2, trials[g:g + k], None, base, batched=batched)
+                      for g in range(0, len(trials), k)]
             for g in groups:
                 g.run(16)                   # group graph captured + replayed once outside the timing
             torch.cuda.synchronize()
@@ -60,7 +65,7 @@ def main():
             dt = time.perf_counter() - t0
             done = [t for g in groups for t in g.trials]
             best = max(done, key=lambda t: t.final["accuracy"])
-            print(f"{dtype} packed trials_per_gpu={k:2d}: {len(done)} trials x {R} rounds in {dt * 1e3:.1f} ms "
+            print(f"{dtype} {'packed' if batched else 'streams'} trials_per_gpu={k:2d}: {len(done)} trials x {R} rounds in {dt * 1e3:.1f} ms "
                   f"({len(done) * R / dt:.0f} trial-rounds/s, {len(done) * R / dt / seq:.2f}x sequential); "
                   f"best {best.hidden} lr={best.lr} ls={best.local_steps} acc={best.final['accuracy']:.4f}",
                   flush=True)
