@@ -155,6 +155,21 @@ void PeerAllReduce::open(const std::vector<py::bytes>& handles) {
     if (open_) throw std::runtime_error("PeerAllReduce: already open");
     if ((int)handles.size() != world_) throw std::runtime_error("PeerAllReduce: need one handle per rank");
     PHIP(hipSetDevice(device_));
+    // Peer mappings of every other visible GPU (one process per GPU sees the whole node): the
+    // kernels read the peers' send buffers and write their flags directly over xGMI.  The IPC
+    // open below enables access lazily for the handle's device; enabling it up front for all
+    // peers makes the mapping independent of how the handle's device is resolved.
+    int n_dev = 0;
+    PHIP(hipGetDeviceCount(&n_dev));
+    for (int d = 0; d < n_dev; ++d) {
+        int can = 0;
+        if (d == device_ || hipDeviceCanAccessPeer(&can, device_, d) != hipSuccess || !can) continue;
+        const hipError_t e = hipDeviceEnablePeerAccess(d, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            throw std::runtime_error(std::string("PeerAllReduce: peer access to device ") + std::to_string(d) +
+                                     ": " + hipGetErrorString(e));
+        (void)hipGetLastError();
+    }
     for (int j = 0; j < world_; ++j) {
         if (j == rank_) {
             peer_base_[j] = base_;
