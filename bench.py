@@ -149,7 +149,8 @@ def main(argv=None):
     ap.add_argument("--wide-allreduce", default="fp32", choices=["fp32", "bf16"],
                     help="--config wide: FedAvg bucket dtype on the wire (fp32 master weights either way)")
     a = ap.parse_args(argv)
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    from fedmi.parallel.comm import launch_env
+    if a.gpus > 1 and launch_env()[3] is None:
         return _self_launch(a, argv)
     if a.config == "wide":
         return main_wide(a)

@@ -22,8 +22,10 @@ working, but the data plane is different:
     want torch to own the communicator.
   - ``gloo``  -- CPU tensors (BASELINE config 1: "2-client FedAvg ... CPU + gloo").
 
-Launch with ``torchrun --nproc-per-node N --master-addr 127.0.0.1 ...``; ``LOCAL_RANK``
-selects the device (fixes the reference's everyone-on-GPU-0).
+Launch with ``torchrun --nproc-per-node N --master-addr 127.0.0.1 ...`` or, like the reference,
+``mpiexec -n N python ...`` (Open MPI / MPICH / PMIx / Slurm environments are recognised,
+:func:`launch_env`); the node-local rank selects the device (fixes the reference's
+everyone-on-GPU-0).
 """
 from __future__ import annotations
 
@@ -39,6 +41,30 @@ import torch.distributed as dist
 def _env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
     return int(v) if v not in (None, "") else default
+
+
+# Rank / size / node-local rank as set by the launcher that started this process: torchrun, or
+# the MPI launchers the reference is run with (``mpiexec -n k python <script>``, SURVEY §1 L0 --
+# Open MPI's and MPICH/Hydra's environment, Slurm's srun).  mpi4py is not needed: the control
+# plane is gloo over a TCP store, so an MPI launch only has to tell every process who it is.
+_LAUNCH_VARS = (
+    ("RANK", "WORLD_SIZE", "LOCAL_RANK"),                                              # torchrun
+    ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"),    # Open MPI
+    ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"),                                       # MPICH / Hydra
+    ("PMIX_RANK", "PMIX_SIZE", "PMIX_LOCAL_RANK"),                                     # PMIx
+    ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"),                                 # srun
+)
+
+
+def launch_env() -> tuple:
+    """``(rank, world_size, local_rank, launcher)`` of this process (``(0, 1, 0, None)`` when
+    started alone).  The first launcher whose rank and size variables are both set wins; a
+    missing local rank defaults to the rank (one node)."""
+    for i, (r, n, lr) in enumerate(_LAUNCH_VARS):
+        if os.environ.get(r, "") != "" and os.environ.get(n, "") != "":
+            rank, size = _env_int(r, 0), _env_int(n, 1)
+            return rank, size, _env_int(lr, rank), ("torchrun", "openmpi", "mpich", "pmix", "slurm")[i]
+    return 0, 1, 0, None
 
 
 DATA_PLANES = ("xgmi", "rccl", "nccl")
@@ -78,9 +104,7 @@ class Comm:
 
     def __init__(self, backend: str = "auto", device: Optional[str] = None, timeout_s: float = 600.0,
                  rccl: bool = True):
-        self.rank = _env_int("RANK", 0)
-        self.size = _env_int("WORLD_SIZE", 1)
-        self.local_rank = _env_int("LOCAL_RANK", self.rank)
+        self.rank, self.size, self.local_rank, self.launcher = launch_env()
         if device is None or device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
         if device.startswith("cuda"):
