@@ -139,10 +139,12 @@ def main(argv=None):
                     help="MFMA operand type of the fused kernels (fp32 accumulate, fp32 master weights)")
     ap.add_argument("--no-convergence", action="store_true")
     ap.add_argument("--no-anchor", action="store_true", help="skip the same-box eager torch anchor")
-    ap.add_argument("--config", default="c", choices=["c", "wide"],
+    ap.add_argument("--config", default="c", choices=["c", "wide", "sweep"],
                     help="c: the reference [C] workload (default, the headline metric) | wide: BASELINE config 3, "
                          "MLP 14-4096-4096-4096-2 on --wide-rows synthetic rows per client, bf16 NT GEMMs, "
-                         "per-layer FedAvg buckets over RCCL")
+                         "per-layer FedAvg buckets over RCCL | sweep: BASELINE config 5, --trials FedAvg trials "
+                         "({hidden} x {lr} x {local steps} grid) packed per GPU, a step = one round of every trial")
+    ap.add_argument("--trials", type=int, default=12, help="--config sweep: trials per GPU (first K of the grid)")
     ap.add_argument("--wide-rows", type=int, default=131072,
                     help="rows per client (BASELINE config 3 names 1e8-row shards: 12500000 per client at k = 8)")
     ap.add_argument("--micro-batch", type=int, default=131072, help="--config wide: rows per micro-batch")
@@ -154,6 +156,8 @@ def main(argv=None):
         return _self_launch(a, argv)
     if a.config == "wide":
         return main_wide(a)
+    if a.config == "sweep":
+        return main_sweep(a)
 
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
     from fedmi.models.mlp import init_flat
@@ -307,6 +311,69 @@ def main_wide(a) -> None:
             "micro_batch": c.mb,
         }), flush=True)
     comm.close()
+
+
+def main_sweep(a) -> int:
+    """BASELINE config 5 under the same contract: every GPU (client) runs ``--trials`` FedAvg
+    trials of the [C] workload at once -- hidden {(50,200),(100,50),(50,100)} x lr {0.002,0.004}
+    x local steps {1,2} (fedmi.hpo.fed_sweep; same-shape trials as native trial batches, the
+    whole K-trial round one HIP graph, one shared all-reduce for all trials).  A step is one
+    round of every trial; ``value`` = trial-rounds/s summed over GPUs."""
+    from fedmi.fl.engine import EngineConfig
+    from fedmi.hpo.fed_sweep import FedTrialGroup, grid
+    from fedmi.parallel.comm import get_world, resolve_backend
+    import torch.distributed as dist
+
+    a.backend = resolve_backend(a.backend, "cuda")
+    comm = get_world(backend="rccl" if a.backend == "xgmi" else a.backend, device="cuda")
+    N = comm.size
+    if N != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
+    trials = grid(((50, 200), (100, 50), (50, 100)), (0.002, 0.004), (1, 2))
+    trials = (trials * ((a.trials + len(trials) - 1) // len(trials)))[:a.trials]
+    X, y = synth_shard(a.rows_per_client, comm.rank, comm.device)
+    g_rounds = 16
+    base = EngineConfig(max_rounds=a.warmup + a.steps + 2 * g_rounds + 4, early_stop=False, dtype=a.dtype,
+                        graph_rounds=g_rounds)
+    grp = FedTrialGroup(X, y, 2, trials, comm if N > 1 else None, base, n_total=a.rows_per_client * N,
+                        group_graph_rounds=g_rounds)
+
+    def barrier():
+        if N > 1:
+            dist.barrier()
+
+    grp.run(max(a.warmup, g_rounds))   # includes the group graph's capture and first replay
+    torch.cuda.synchronize(comm.device)
+    barrier()
+    torch.cuda.synchronize(comm.device)
+    t0 = time.perf_counter()
+    grp.run(a.steps)
+    torch.cuda.synchronize(comm.device)
+    barrier()
+    dt = time.perf_counter() - t0
+    if N > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = len(trials) * a.steps * N / dt
+    best = grp.best()
+    if comm.rank == 0:
+        print(json.dumps({
+            "metric": "trial-rounds/s, packed federated hyperparameter sweep (BASELINE config 5)", "value": value,
+            "unit": "trial-rounds/s (sum over GPUs; step = one federated round of every trial incl. eval + FedAvg)",
+            "n_gpus": N, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "data": f"synthetic income-shaped (device Philox), {a.rows_per_client} rows/client; random-init weights",
+            "config": {"model": "MLP 14-{hidden}-2 grid", "global_batch": a.rows_per_client * N, "seq_len": 1,
+                       "parallelism": f"fedavg{N} x {len(trials)} trials/GPU ({len(grp.batches)} trial batches, "
+                                      f"one all-reduce per round)",
+                       "trials": [[list(t.hidden), t.lr, t.local_steps] for t in trials]},
+            "us_per_trial_round": dt / (a.steps * len(trials)) * 1e6,
+            "best_trial": {"hidden": list(best.hidden), "lr": best.lr, "local_steps": best.local_steps,
+                           "train_acc_synthetic": best.final["accuracy"]},
+        }), flush=True)
+    comm.close()
+    return 0
 
 
 if __name__ == "__main__":

@@ -187,6 +187,7 @@ class FedTrialGroup:
             for r in range(self.graph_rounds):   # parities 0, 1, ...: replayed from even rounds
                 self._issue_group_round(r)
         self.graph = g
+        self._graph_flags = [e.engine.flags() for e in self.engines]
 
     def _run_hip(self, n_rounds: int) -> None:
         r, end = self.rounds_issued, self.rounds_issued + n_rounds
@@ -197,6 +198,10 @@ class FedTrialGroup:
                     self._capture()
                 with torch.cuda.stream(self.stream):
                     self.graph.replay()
+                # the replayed rounds' effect on each engine's round bookkeeping: the state the
+                # captured rounds left (a finalize in between may have changed it)
+                for e, f in zip(self.engines, self._graph_flags):
+                    e.engine.set_flags(f)
                 r += G
             else:
                 self._issue_group_round(r)

@@ -69,7 +69,7 @@ def _compile(src: str) -> str:
 
 def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
     srcs = _sources()
-    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc"))
     stamp = os.path.join(BUILD, "stamp")
     digest = _digest(srcs + headers)
     if not force and os.path.isfile(TARGET) and os.path.isfile(stamp):

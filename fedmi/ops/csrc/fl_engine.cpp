@@ -339,6 +339,22 @@ class FLEngine {
 
     int graph_rounds() const { return graph_rounds_; }
 
+    // Host-side round bookkeeping (which metrics the last issued round left pending) as a bit
+    // set.  A caller that captures rounds of this engine into its own graph (a trial group)
+    // reads it after the capture and restores it after every replay of that graph.
+    int flags() const {
+        return (pending_cm_ ? 1 : 0) | (cm_in_tail_ ? 2 : 0) | (prev_lagged_ ? 4 : 0) | (prev_scored_ ? 8 : 0) |
+               (prev_afold_ ? 16 : 0) | (need_pack_ ? 32 : 0);
+    }
+    void set_flags(int f) {
+        pending_cm_ = f & 1;
+        cm_in_tail_ = f & 2;
+        prev_lagged_ = f & 4;
+        prev_scored_ = f & 8;
+        prev_afold_ = f & 16;
+        need_pack_ = f & 32;
+    }
+
     // The captured rounds assume the steady state of their kind: a fused graph must not
     // start behind a classic round (whose counts already sit in the tail), a classic graph
     // not behind a fused one (whose counts were never computed).
@@ -922,6 +938,8 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("finalize", &FLEngine::finalize)
         .def("capture", &FLEngine::capture, py::arg("n"), py::arg("stream"), py::arg("comm") = nullptr)
         .def("replay", &FLEngine::replay)
+        .def("flags", &FLEngine::flags)
+        .def("set_flags", &FLEngine::set_flags)
         .def("graph_rounds", &FLEngine::graph_rounds)
         .def("time_kernels", &FLEngine::time_kernels)
         .def("set_debug", &FLEngine::set_debug)

@@ -291,132 +291,27 @@ __device__ void forward_block(const MLPDesc& d, float* acts, const float* li, un
 // ---------------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------------
-// (one body, two entry points: the single-engine kernel takes its arguments as kernel
-// arguments, the trial-batch kernel from the FLTrialDesc table row of blockIdx.y)
-template <int RT>
-__device__ __forceinline__ void
-fl_train_body(const MLPDesc& d, const FLConfig c, const FLBuffers b, const float* __restrict__ pg,
-              const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step, int mode,
-              float* __restrict__ cm_out, int fold_mask) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ FLState S_sh;
-    FL_STAMP(0);
-    if (b.dbg != nullptr && threadIdx.x == 0) b.dbg[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime();
-    int* cm_s = reinterpret_cast<int*>(lds + d.cm_off);
-    const int C = d.dim[d.L];
-    if (threadIdx.x < 64) {  // wave 0: round bookkeeping while the other waves stage
-        FLState S0 = *st_in;
-        if (local_step == 0) {
-            if (mode == FL_EVAL_CLASSIC) {
-                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0, fold_mask);
-                if (threadIdx.x == 0) {
-                    S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-                    if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
-                    if (blockIdx.x == 0) *st_out = S0;
-                }
-            } else if (threadIdx.x == 0) {
-                // fused (fl_common.h): the Adam kernel folds and decides; train tentatively
-                S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-            }
-        }
-        if (threadIdx.x == 0) {
-            S_sh = S0;
-            cm_s[FL_CM_FLAG] = (local_step == 0 && mode == FL_EVAL_FUSED && S0.next_round > S0.finalized) ? 1 : 0;
-        }
-    }
-    for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
-    const float* params = (local_step == 0) ? pg : b.local;
-    const int R = RT * 16;
-    const int row0 = blockIdx.x * R;
-    const int L = d.L;
-    float* acts = lds;
-    float* li = lds + d.img_lds;
-    // staging does not depend on the state: it overlaps the finalize above
-    // labels are needed only after the forward pass: issue the load now
-    const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
-    stage_image(d, params, li);
-    stage_rows<RT>(b.X, c.n_rows, d.dim[0], row0, acts + d.act_off[0], d.ld[0]);
-    lds_barrier();
-    FL_STAMP(1);
-    if (!S_sh.live) return;
-    float* slab = b.slab + (size_t)blockIdx.x * c.slab_stride;
-    forward_block<RT>(d, acts, li, b.dbg);
-    FL_STAMP(2);
-    if (b.dbg != nullptr && threadIdx.x == 0) b.dbg[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
-
-    // softmax cross-entropy (mean over the local shard): dZ = (softmax - onehot) / n.
-    // Fused evaluation: the same logits score the previous round's model (argmax).
-    float* z = acts + d.act_off[L];
-    const int ldz = d.ld[L];
-    const bool score = cm_s[FL_CM_FLAG] != 0;
-    float lossv = 0.f;
-    if (threadIdx.x < R) {
-        const int r = threadIdx.x, row = row0 + r;
-        float* zr = z + r * ldz;
-        if (row < c.n_rows) {
-            const int y = ylab;
-            float mx = zr[0], bv = zr[0];
-            int best = 0;
-            for (int k = 1; k < C; ++k) {
-                mx = fmaxf(mx, zr[k]);
-                if (zr[k] > bv) { bv = zr[k]; best = k; }  // torch.max(dim=1): first maximum
-            }
-            if (score) atomicAdd(&cm_s[y * C + best], 1);
-            float se = 0.f;
-            for (int k = 0; k < C; ++k) se += expf(zr[k] - mx);
-            const float lse = mx + logf(se);
-            lossv = (lse - zr[y]) * c.inv_n;
-            for (int k = 0; k < C; ++k) {
-                const float p = expf(zr[k] - mx) / se;
-                zr[k] = (p - (k == y ? 1.f : 0.f)) * c.inv_n;
-            }
-        } else {
-            for (int k = 0; k < C; ++k) zr[k] = 0.f;
-        }
-        for (int k = C; k < ((C + 15) & ~15); ++k) zr[k] = 0.f;
-    }
-    if (threadIdx.x < 64) {
-        lossv = wave_sum(lossv);
-        if (threadIdx.x == 0) slab[d.P] = lossv;  // R <= 64: wave 0 holds every row
-    }
-    lds_barrier();
-    if (score)
-        for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
-            if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
-    FL_STAMP(3);
-
-    // backward, top layer first, ONE phase per layer: wgrad_l (reads dZ_{l+1}, act_l) and
-    // dgrad_l (reads dZ_{l+1}, W_l, act_l; writes dH_l into its own buffer) are independent.
-    for (int l = L - 1; l >= 0; --l) {
-        const float* dz = (l == L - 1) ? acts + d.act_off[L] : acts + d.dlt_off[l + 1];
-        const float* act = acts + d.act_off[l];
-        wgrad_layer<RT>(d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act, d.ld[l], slab + d.w_off[l],
-                        slab + d.b_off[l]);
-        if (l > 0)
-            dgrad_layer<RT>(li + d.iw_off[l], fl_ldw(d.dim[l]), d.dim[l], d.dim[l + 1], dz, d.ld[l + 1], act,
-                            d.ld[l], acts + d.dlt_off[l]);
-        lds_barrier();
-        FL_STAMP(4 + (L - 1 - l));
-    }
-    FL_STAMP(15);
-}
-
+// Kernel body shared by the single-engine and trial-batch entry points (fl_train_body.inc).
 template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                 const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step, int mode,
                 float* __restrict__ cm_out, int fold_mask) {
-    fl_train_body<RT>(d, c, b, pg, st_in, st_out, local_step, mode, cm_out, fold_mask);
+#include "fl_train_body.inc"
 }
 
 template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
-fl_train_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pg, FLSel si, FLSel so, int local_step,
-                      int mode, FLSel cm, int fold_mask) {
+fl_train_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pg_sel, FLSel si_sel, FLSel so_sel,
+                      int local_step, int mode, FLSel cm_sel, int fold_mask) {
     const FLTrialDesc& t = T[blockIdx.y];
-    fl_train_body<RT>(d, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, pg)),
-                      reinterpret_cast<const FLState*>(fl_sel(t, si)), reinterpret_cast<FLState*>(fl_sel(t, so)),
-                      local_step, mode, reinterpret_cast<float*>(fl_sel(t, cm)), fold_mask);
+    const FLConfig c = t.c;
+    const FLBuffers b = t.b;
+    const float* __restrict__ pg = reinterpret_cast<const float*>(fl_sel(t, pg_sel));
+    const FLState* __restrict__ st_in = reinterpret_cast<const FLState*>(fl_sel(t, si_sel));
+    FLState* __restrict__ st_out = reinterpret_cast<FLState*>(fl_sel(t, so_sel));
+    float* __restrict__ cm_out = reinterpret_cast<float*>(fl_sel(t, cm_sel));
+#include "fl_train_body.inc"
 }
 
 // Slab reduction + Adam + StepLR + FedAvg pre-scale.  Block = 16 waves x 64 DENSE
@@ -486,273 +381,32 @@ __device__ __forceinline__ float adam_update(const FLConfig& c, const FLBuffers&
 
 // Block 0 is the tail block (dispatched first: with the in-kernel fold every other block may
 // wait for its lag chunk); blocks 1.. own 64 dense parameters each.
-__device__ __forceinline__ void
-fl_adam_body(const MLPDesc& d, const FLConfig c, const FLBuffers b, const float* __restrict__ pin,
-             const float* __restrict__ anchor, float* __restrict__ comm,
-             const FLState* __restrict__ st, int local_step, const MLPDescB& e, int pack,
-             FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, const PeerArgs& pa, int xchg,
-             int afold) {
-    __shared__ float part[ADAM_WAVES][64];
-    __shared__ FLState S_sh;
-    __shared__ float lag_s[PEER_MAX_WORLD * (FL_MAX_CLASSES * FL_MAX_CLASSES + 1)];
-    const int last_local_step = (local_step == c.local_steps - 1);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    FL_STAMP(0);
-    const unsigned target = st->calls + 1;  // call index of this kernel's exchanges
-    // lag region A through LL slots (peer_device.h) when it fits one chunk's 64 positions:
-    // every rank pushes its whole region (zeros outside its own segment), receivers sum in rank
-    // order -- the same values as the pull protocol's sum
-    const bool ll_lag = pa.ll != nullptr && c.tail_len <= 64;
-    // Round state.  Fused evaluation (fl_common.h): wave 0 of EVERY block folds the previous
-    // round's tail (anchor = this round's input image) into the previous state and decides
-    // whether this round is live -- the same deterministic computation everywhere, so no
-    // block waits for another; block 0 publishes it.  Without early stopping the fold cannot
-    // change the decision and only block 0 (history) runs it.  Called after the wave issued
-    // its first slab loads, so the fold's double-precision metrics overlap them.  `afold`: the
-    // previous round was lagged; its metrics are region A of every rank's send buffer,
-    // exchanged right here (chunk ADAM_CHUNK_LAG), so the live decision is taken in time.
-    auto round_state = [&]() {
-        if (wave != 0) return;
-        FLState S0 = *st;
-        if (fold) {
-            const bool need = c.es_enabled || blockIdx.x == 0;
-            if (afold) {
-                if (need && ll_lag) {
-                    const float lv = peer_ll_sum(pa, ADAM_CHUNK_LAG * 64 + lane, target, lane < c.tail_len);
-                    if (lane < c.tail_len) lag_s[lane] = lv;
-                } else if (need) {
-                    peer_chunk_wait(pa, ADAM_CHUNK_LAG, target);
-                    for (int i = lane; i < c.tail_len; i += 64) lag_s[i] = peer_pull_sum(pa, c.lag_off + i);
-                }
-                if (need) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    S0 = fold_round(d, c, b, lag_s, S0.next_round - 1, S0, blockIdx.x == 0);
-                }
-            } else if (need) {
-                S0 = finalize_state(d, c, b, anchor, S0, blockIdx.x == 0, fold_mask);
-            }
-            if (lane == 0) {
-                S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-                if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
-                if (xchg || afold) S0.calls += 1;  // every rank counts its exchange calls alike
-                if (blockIdx.x == 0) *st_out = S0;
-            }
-        }
-        if (lane == 0) S_sh = S0;
-    };
-    if (blockIdx.x == 0) {
-        // tail block: this rank's confusion slots are zeroed (the eval pass accumulates
-        // into them); its loss slot gets the per-workgroup CE partials, summed in a fixed order
-        if (!last_local_step) {
-            round_state();
-            return;
-        }
-        const int CC = c.tail_stride - 1;
-        if (afold) {
-            // lag region A first -- the previous round's counts (scored by this round's train
-            // kernel) and loss -- published at once: every block of every rank folds from it
-            for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
-                const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
-                const float v = (k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
-                comm[c.lag_off + jj] = v;
-                if (ll_lag) peer_ll_push(pa, ADAM_CHUNK_LAG * 64 + jj, target, v);  // (jj < 64: wave 0)
-            }
-            if (!ll_lag) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (wave == 0) peer_chunk_publish(pa, ADAM_CHUNK_LAG, target);
-            }
-        }
-        // first batch of loss loads in flight before the fold (one per thread up to 1024 slabs)
-        const int s0 = threadIdx.x;
-        float lp = s0 < c.n_slabs ? b.slab[(size_t)s0 * c.slab_stride + d.P] : 0.f;
-        round_state();
-        for (int s = s0 + blockDim.x; s < c.n_slabs; s += blockDim.x) lp += b.slab[(size_t)s * c.slab_stride + d.P];
-        part[wave][lane] = lp;
-        lds_barrier();
-        const FLState S = S_sh;
-        if (wave == 0) {
-            float t = 0.f;
-#pragma unroll
-            for (int w = 0; w < ADAM_WAVES; ++w) t += part[w][lane];
-            t = wave_sum(t);
-            part[0][lane] = t;
-        }
-        lds_barrier();
-        const float loss = part[0][0];
-        for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
-            const int i = d.Pimg + jj;
-            if (!S.live) {
-                comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
-                continue;
-            }
-            const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
-            comm[i] = (k == c.rank && e == c.tail_stride - 1) ? loss : 0.f;
-        }
-        if (c.lag_off > 0) {
-            // lag region A (FL_EVAL_LAGGED, FedAvg outside this kernel): the previous round's
-            // counts and loss when `tail_a`, folded one round later from the all-reduce
-            if (!afold)
-                for (int jj = threadIdx.x; jj < c.tail_len; jj += blockDim.x) {
-                    const int i = c.lag_off + jj;
-                    if (!S.live) {
-                        comm[i] = (c.rank == 0) ? anchor[i] : 0.f;
-                        continue;
-                    }
-                    const int k = jj / c.tail_stride, e = jj - k * c.tail_stride;
-                    comm[i] = (tail_a && k == c.rank) ? (e < CC ? b.cnt[e] : b.lbuf[0]) : 0.f;
-                }
-            __syncthreads();  // every read of cnt / lbuf is done
-            // this round's loss is kept for the next round; the counts cleared for the next
-            // train kernel
-            if (S.live) {
-                for (int e = threadIdx.x; e < CC; e += blockDim.x) b.cnt[e] = 0.f;
-                if (threadIdx.x == 0) b.lbuf[0] = loss;
-            }
-        }
-        if (xchg) {
-            // Adam-fused FedAvg of the metric tails (peer_device.h)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // every wave's tail stores are acknowledged
-            if (wave == 0) {
-                peer_chunk_exchange_wait(pa, ADAM_CHUNK_TAIL, target);
-                for (int i = d.Pimg + lane; i < (int)pa.n; i += 64) pa.out[i] = peer_pull_sum(pa, i);
-            }
-        }
-        return;
-    }
-    const int pblk = blockIdx.x - 1;
-    const int di = pblk * 64 + lane;  // dense index
-    const bool valid = di < d.P;
-    // dense index -> image index (and, in bf16 mode, -> packed bf16 LDS-layout position)
-    int j = 0, pk = 0;
-    bool is_bias = false;
-    if (valid) {
-        int l = 0;
-        while (l + 1 < d.L && di >= d.w_off[l + 1]) ++l;
-        const int K = d.dim[l];
-        if (di < d.b_off[l]) {
-            const int q = di - d.w_off[l];
-            const int n = q / K, k = q - n * K;
-            j = d.iw_off[l] + n * fl_ldw(K) + k;
-            pk = e.w_off[l] - e.param_off + fl_wbyte(e, l, n, k);
-        } else {
-            j = d.ib_off[l] + (di - d.b_off[l]);
-            pk = e.bias_off[l] - e.param_off + (di - d.b_off[l]) * 4;
-            is_bias = true;
-        }
-    }
-    // past the stop: rank 0 contributes the (identical) global weights, others 0, so the
-    // all-reduce returns them bit-exactly.  Classic rounds know the state on entry and skip
-    // the reduction; fused rounds learn it at the barrier below.
-    if (!fold && !st->live) {
-        if (wave == 0 && valid && last_local_step) comm[j] = (c.rank == 0) ? anchor[j] : 0.f;
-        return;
-    }
-    // wave 0's operands of the update, issued before the slab loads so their latency overlaps
-    float p0 = 0.f, m0 = 0.f, v0 = 0.f, a0 = 0.f, sc0 = 0.f;
-    if (wave == 0 && valid) {
-        p0 = pin[j];
-        m0 = b.m[j];
-        v0 = b.v[j];
-        a0 = anchor[j];
-        // the round this step belongs to whenever it is live: the folded state's next round, or
-        // the running one
-        const int rg = fold ? st->next_round : st->cur_round;
-        sc0 = b.rtab[4 * (size_t)min(max(rg, 0), c.max_rounds - 1)];
-    }
-    float g = 0.f;
-    bool have_state = false;
-    // the slab rows of this block's 64 parameters, 16 rows in flight per lane; the element type
-    // is hoisted out of the loop (a per-element select on it would serialise the loads)
-#define FL_SLAB_REDUCE(LOAD)                                                                        \
-    for (int s0 = wave; s0 < c.n_slabs; s0 += ADAM_WAVES * ADAM_DEPTH) {                          \
-        float x[ADAM_DEPTH];                                                                        \
-        _Pragma("unroll") for (int u = 0; u < ADAM_DEPTH; ++u) {                                    \
-            const int s = s0 + u * ADAM_WAVES;                                                      \
-            const size_t row = (size_t)(s < c.n_slabs ? s : 0) * c.slab_stride;                     \
-            const float v = LOAD; /* unpredicated; non-temporal: the slab is read once */           \
-            x[u] = s < c.n_slabs ? v : 0.f;                                                         \
-        }                                                                                           \
-        if (!have_state) {                                                                          \
-            have_state = true;                                                                      \
-            FL_STAMP(1);                                                                            \
-            round_state();                                                                          \
-            FL_STAMP(2);                                                                            \
-        }                                                                                           \
-        _Pragma("unroll") for (int u = 0; u < ADAM_DEPTH; ++u) g += x[u];                           \
-    }
-    if (c.slab_f16) {
-        const _Float16* sph = reinterpret_cast<const _Float16*>(b.slab) + (valid ? di : 0);
-        FL_SLAB_REDUCE((float)__builtin_nontemporal_load(&sph[2 * row]))
-    } else {
-        const float* sp = b.slab + (valid ? di : 0);
-        FL_SLAB_REDUCE(__builtin_nontemporal_load(&sp[row]))
-    }
-#undef FL_SLAB_REDUCE
-    if (!have_state) round_state();
-    FL_STAMP(3);
-    part[wave][lane] = g;
-    lds_barrier();
-    if (wave != 0) return;
-    FL_STAMP(4);
-    const FLState S = S_sh;
-    float contrib = 0.f;  // this rank's FedAvg contribution of the lane's parameter
-    if (valid) {
-        if (!S.live) {
-            contrib = (c.rank == 0) ? a0 : 0.f;
-            if (last_local_step) comm[j] = contrib;
-        } else {
-            contrib = adam_update(c, b, comm, S, local_step, last_local_step, pack, j, pk, is_bias, e.wlo_delta, part,
-                                  lane, p0, m0, v0, a0, sc0);
-        }
-    }
-    FL_STAMP(5);
-    if (xchg && pa.ll != nullptr) {
-        // Adam-fused FedAvg of this block's 64 parameters, LL chunks (peer_device.h): push the
-        // contribution with the call index into every rank's ring, poll this rank's ring, sum
-        // in rank order; global image + packed bf16 image
-        const int pos = (ADAM_CHUNK_W0 + pblk) * 64 + lane;
-        if (valid) peer_ll_push(pa, pos, target, contrib);
-        const float gsum = peer_ll_sum(pa, pos, target, valid);
-        if (valid) {
-            pa.out[j] = gsum;
-            if (pack) pack_store(b.pk_global, pk, is_bias, e.wlo_delta, gsum);
-        }
-    } else if (xchg) {
-        // Adam-fused FedAvg of this block's 64 parameters (peer_device.h): publish, wait for
-        // every rank's chunk, pull + sum in rank order; global image + packed bf16 image
-        peer_chunk_exchange_wait(pa, ADAM_CHUNK_W0 + pblk, target);
-        if (valid) {
-            const float gsum = peer_pull_sum(pa, j);
-            pa.out[j] = gsum;
-            if (pack) pack_store(b.pk_global, pk, is_bias, e.wlo_delta, gsum);
-        }
-    }
-    if (b.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stamp the stores' completion
-    FL_STAMP(15);
-}
-
+// Kernel body shared by the single-engine and trial-batch entry points (fl_adam_body.inc).
 __global__ void __launch_bounds__(ADAM_WAVES * 64)
 fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
                const float* __restrict__ anchor, float* __restrict__ comm,
                const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
                FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, PeerArgs pa, int xchg,
                int afold) {
-    fl_adam_body(d, c, b, pin, anchor, comm, st, local_step, e, pack, st_out, fold, tail_a, fold_mask, pa, xchg,
-                 afold);
+#include "fl_adam_body.inc"
 }
 
 // Trial batch (no peer exchange: the trials' FedAvg is one shared collective outside).
 __global__ void __launch_bounds__(ADAM_WAVES * 64)
-fl_adam_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pin, FLSel anchor, FLSel comm, FLSel st,
-                     int local_step, MLPDescB e, int pack, FLSel st_out, int fold, int tail_a, int fold_mask) {
+fl_adam_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pin_sel, FLSel anchor_sel, FLSel comm_sel,
+                     FLSel st_sel, int local_step, MLPDescB e, int pack, FLSel st_out_sel, int fold, int tail_a,
+                     int fold_mask) {
     const FLTrialDesc& t = T[blockIdx.y];
+    const FLConfig c = t.c;
+    const FLBuffers b = t.b;
+    const float* __restrict__ pin = reinterpret_cast<const float*>(fl_sel(t, pin_sel));
+    const float* __restrict__ anchor = reinterpret_cast<const float*>(fl_sel(t, anchor_sel));
+    float* __restrict__ comm = reinterpret_cast<float*>(fl_sel(t, comm_sel));
+    const FLState* __restrict__ st = reinterpret_cast<const FLState*>(fl_sel(t, st_sel));
+    FLState* __restrict__ st_out = reinterpret_cast<FLState*>(fl_sel(t, st_out_sel));
     const PeerArgs pa = {};
-    fl_adam_body(d, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, pin)),
-                 reinterpret_cast<const float*>(fl_sel(t, anchor)), reinterpret_cast<float*>(fl_sel(t, comm)),
-                 reinterpret_cast<const FLState*>(fl_sel(t, st)), local_step, e, pack,
-                 reinterpret_cast<FLState*>(fl_sel(t, st_out)), fold, tail_a, fold_mask, pa, 0, 0);
+    const int xchg = 0, afold = 0;
+#include "fl_adam_body.inc"
 }
 
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,

@@ -457,169 +457,27 @@ __device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDe
 // ---------------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------------
-// (one body, two entry points: the single-engine kernel and the trial-batch kernel, whose
-// configuration / buffers come from the FLTrialDesc table row of blockIdx.y)
-template <int RT>
-__device__ __forceinline__ void
-fl_train_bf16_body(const MLPDesc& d, const MLPDescB& e, const FLConfig c, const FLBuffers b,
-                   const float* __restrict__ pg, const FLState* __restrict__ st_in, FLState* __restrict__ st_out,
-                   int local_step, int stage_local, int mode, float* __restrict__ cm_out, int fold_mask) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    __shared__ FLState S_sh;
-    FL_STAMP(0);
-    int* cm_s = reinterpret_cast<int*>(lds + e.cm_off);
-    const int C = d.dim[d.L];
-    if (threadIdx.x < 64) {  // wave 0: round bookkeeping while the other waves stage
-        FLState S0 = *st_in;
-        if (local_step == 0) {
-            if (mode == FL_EVAL_CLASSIC) {
-                S0 = finalize_state(d, c, b, pg, S0, blockIdx.x == 0, fold_mask);
-                if (threadIdx.x == 0) {
-                    S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-                    if (S0.live) { S0.cur_round = S0.next_round; S0.next_round += 1; }
-                    if (blockIdx.x == 0) *st_out = S0;
-                }
-            } else if (threadIdx.x == 0) {
-                // FUSED / FUSED_SKIP / LAGGED: the Adam kernel folds the previous round and
-                // decides; train on the tentative decision (a stop only turns this round into a
-                // no-op later)
-                S0.live = (!S0.stopped && S0.next_round < c.max_rounds) ? 1 : 0;
-            }
-        }
-        if (threadIdx.x == 0) {
-            S_sh = S0;
-            // score the rows for the previous round iff its metrics are still pending
-            cm_s[FL_CM_FLAG] = (local_step == 0 && mode == FL_EVAL_FUSED && S0.next_round > S0.finalized) ? 1 : 0;
-        }
-    }
-    for (int i = threadIdx.x; i < C * C; i += FL_THREADS) cm_s[i] = 0;
-    const float* params = (local_step == 0) ? pg : b.local;
-    const int R = RT * 16;
-    const int row0 = blockIdx.x * R;
-    const int L = d.L;
-    const int ylab = (threadIdx.x < R) ? b.y[min(row0 + (int)threadIdx.x, c.n_rows - 1)] : 0;
-    // FL_EVAL_LAGGED (first local step): the previous round's local model, still intact in
-    // pk_local (this round's Adam has not run), is staged and scored first; the round's own
-    // weights are loaded meanwhile and replace it in LDS before the training pass
-    const bool lagged = mode == FL_EVAL_LAGGED && local_step == 0;
-    const char* img = (local_step == 0 && !stage_local) ? b.pk_global : b.pk_local;
-    stage_params_rows_bf16<RT>(e, lagged ? b.pk_local : img, b.X, c.n_rows, d.dim[0], row0, lds);
-    FL_STAMP(8);
-    {   // padding columns [C, kp[L]) of D_L never change: zero them here, off the CE's path
-        const int padc = e.kp[L] - C;
-        uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
-        for (int i = threadIdx.x; i < R * padc; i += FL_THREADS) {
-            const int r = i / padc;
-            DL[r * e.lda[L] + C + (i - r * padc)] = 0;
-        }
-    }
-    FL_STAMP(9);
-    lds_barrier();
-    FL_STAMP(1);
-    if (!S_sh.live) return;
-    float* slab = b.slab + (size_t)blockIdx.x * c.slab_stride;
-    // lagged: pass 0 scores the previous local model (C:148), pass 1 trains; one call site of
-    // the forward pass (inlined, so the prefetched weights stay in registers across it)
-    ParamRegs pr;
-    if (lagged) params_load(e, img, pr);
-    for (int pass = lagged ? 0 : 1; pass < 2; ++pass) {
-        if (pass == 1 && lagged) {
-            if (threadIdx.x < R) {
-                // the scored model's argmax: counts -> b.cnt after the CE barrier below
-                const int r = threadIdx.x;
-                if (row0 + r < c.n_rows) {
-                    const float* zr = reinterpret_cast<const float*>(lds + e.logit_off) + r * FL_LOGIT_LD;
-                    int best = 0;
-                    float bv = zr[0];
-                    for (int k = 1; k < C; ++k)
-                        if (zr[k] > bv) { bv = zr[k]; best = k; }
-                    atomicAdd(&cm_s[ylab * C + best], 1);
-                }
-            }
-            lds_barrier();  // every read of the scored image and its logits is done
-            params_store(e, img, pr, lds);
-            lds_barrier();
-        }
-        forward_block_bf16<RT>(d, e, lds, b.dbg);
-    }
-    FL_STAMP(2);
-
-    // softmax cross-entropy: D_L = softmax - onehot, bf16, times the mean's 1/n -- except with
-    // the fp16 slab, whose partials are sums of the unscaled gradient (the 1/n is applied by the
-    // Adam kernel after its fp32 reduction, so small gradients keep fp16's normal range).
-    // Fused evaluation: the same logits score the previous round's model (argmax).
-    const float* z = reinterpret_cast<const float*>(lds + e.logit_off);
-    uint16_t* DL = reinterpret_cast<uint16_t*>(lds + e.dlt_off[L]);
-    const int ldL = e.lda[L];
-    const bool score = cm_s[FL_CM_FLAG] != 0;
-    float lossv = 0.f;
-    if (threadIdx.x < R) {
-        const int r = threadIdx.x, row = row0 + r;
-        const float* zr = z + r * FL_LOGIT_LD;
-        uint16_t* dr = DL + r * ldL;
-        if (row < c.n_rows) {
-            const int y = ylab;
-            float mx = zr[0], bv = zr[0];
-            int best = 0;
-            for (int k = 1; k < C; ++k) {
-                mx = fmaxf(mx, zr[k]);
-                if (zr[k] > bv) { bv = zr[k]; best = k; }  // torch.max(dim=1): first maximum
-            }
-            if (score) atomicAdd(&cm_s[y * C + best], 1);
-            // hardware exp2/log2 (v_exp_f32 / v_log_f32): the deltas are rounded to bf16
-            // right after, far coarser than the fast intrinsics' error; the libm versions
-            // were a ~1 us dependent chain per round (in-kernel stamps)
-            float se = 0.f;
-            for (int k = 0; k < C; ++k) se += __expf(zr[k] - mx);
-            const float inv_se = 1.f / se;
-            const float lse = mx + __logf(se);
-            lossv = (lse - zr[y]) * c.inv_n;
-            for (int k = 0; k < C; ++k) {
-                const float p = __expf(zr[k] - mx) * inv_se;
-                const float dk = p - (k == y ? 1.f : 0.f);
-                dr[k] = (uint16_t)bf16_bits(c.slab_f16 ? dk : dk * c.inv_n);
-            }
-        } else {
-            for (int k = 0; k < C; ++k) dr[k] = 0;
-        }
-    }
-    if (threadIdx.x < 64) {
-        lossv = wave_sum(lossv);
-        if (threadIdx.x == 0) slab[d.P] = lossv;
-    }
-    lds_barrier();
-    if (score || lagged)
-        for (int i = threadIdx.x; i < C * C; i += FL_THREADS)
-            if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
-    FL_STAMP(3);
-
-    // backward, top layer first, one phase per layer (wgrad_l and dgrad_l are independent)
-    for (int l = L - 1; l >= 0; --l) {
-        if (c.slab_f16) wgrad_layer_bf16<RT, true>(d, e, l, lds, slab);
-        else wgrad_layer_bf16<RT, false>(d, e, l, lds, slab);
-        if (l > 0) dgrad_layer_bf16<RT>(d, e, l, lds);
-        lds_barrier();
-        FL_STAMP(4 + (L - 1 - l));
-    }
-    FL_STAMP(15);
-}
-
+// Kernel body shared by the single-engine and trial-batch entry points (fl_train_bf16_body.inc).
 template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                      const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
                      int stage_local, int mode, float* __restrict__ cm_out, int fold_mask) {
-    fl_train_bf16_body<RT>(d, e, c, b, pg, st_in, st_out, local_step, stage_local, mode, cm_out, fold_mask);
+#include "fl_train_bf16_body.inc"
 }
 
 template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
-fl_train_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel pg, FLSel si, FLSel so,
-                           int local_step, int stage_local, int mode, FLSel cm, int fold_mask) {
+fl_train_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel pg_sel, FLSel si_sel,
+                           FLSel so_sel, int local_step, int stage_local, int mode, FLSel cm_sel, int fold_mask) {
     const FLTrialDesc& t = T[blockIdx.y];
-    fl_train_bf16_body<RT>(d, e, t.c, t.b, reinterpret_cast<const float*>(fl_sel(t, pg)),
-                           reinterpret_cast<const FLState*>(fl_sel(t, si)), reinterpret_cast<FLState*>(fl_sel(t, so)),
-                           local_step, stage_local, mode, reinterpret_cast<float*>(fl_sel(t, cm)), fold_mask);
+    const FLConfig c = t.c;
+    const FLBuffers b = t.b;
+    const float* __restrict__ pg = reinterpret_cast<const float*>(fl_sel(t, pg_sel));
+    const FLState* __restrict__ st_in = reinterpret_cast<const FLState*>(fl_sel(t, si_sel));
+    FLState* __restrict__ st_out = reinterpret_cast<FLState*>(fl_sel(t, so_sel));
+    float* __restrict__ cm_out = reinterpret_cast<float*>(fl_sel(t, cm_sel));
+#include "fl_train_bf16_body.inc"
 }
 
 // Local evaluation of one row block (rows [blk*R, blk*R + R)) of the post-step model:

@@ -1,5 +1,6 @@
-"""bench.py contract: one JSON line with the required keys, for the headline [C] config and
-the wide config (BASELINE config 3), on one GPU with a short run."""
+"""bench.py contract: one JSON line with the required keys, for the headline [C] config, the
+wide config (BASELINE config 3) and the packed sweep (BASELINE config 5), on one GPU with a
+short run."""
 import json
 import os
 import subprocess
@@ -46,3 +47,12 @@ def test_bench_wide_contract():
     rec = _run(["--config", "wide", "--steps", "2", "--warmup", "1", "--wide-rows", "2048"])
     assert rec["config"]["model"] == "MLP 14-4096-4096-4096-2"
     assert rec["tflops_per_client"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_sweep_contract():
+    """BASELINE config 5 under the bench contract: 12 packed trials per GPU, a step = one round
+    of every trial (three trial batches: one per hidden shape)."""
+    rec = _run(["--config", "sweep", "--steps", "32", "--warmup", "16"])
+    assert len(rec["config"]["trials"]) == 12 and "3 trial batches" in rec["config"]["parallelism"]
+    assert rec["us_per_trial_round"] > 0 and 0.5 < rec["best_trial"]["train_acc_synthetic"] <= 1.0

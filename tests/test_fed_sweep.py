@@ -102,17 +102,38 @@ def test_group_graph_equals_standalone_engines(dtype, batched):
     alone; early stopping inside the group is per trial."""
     X, y = make_income_like(1500, seed=6)
     trials = grid([(16,), (24, 8)], [0.004, 0.02], [1, 2])
-    base = EngineConfig(max_rounds=60, patience=3, tolerance=3e-3, dtype=dtype, graph_rounds=8)
+    base = EngineConfig(max_rounds=64, patience=3, tolerance=3e-3, dtype=dtype, graph_rounds=8)
     from fedmi.hpo.fed_sweep import FedTrialGroup
     g = FedTrialGroup(X, y, 2, trials, None, base, group_graph_rounds=8, batched=batched)
     g.run(3)     # eager rounds first, then graph replays from an odd start
     g.run(41)
+    g.run(16)    # replays only, behind the previous call's history read-back
     assert g.graph is not None
     for t, e in zip(g.trials, g.engines):
         cfg = replace(base, hidden=t.hidden, lr=t.lr, local_steps=t.local_steps)
         ref = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *t.hidden, 2], 0))
-        ref.run(44)
+        ref.run(60)
         np.testing.assert_array_equal(ref.global_flat(), e.global_flat())
         h = ref.history()
         assert h["rounds_run"] == t.rounds_run and h["stop_round"] == t.history["stop_round"]
         np.testing.assert_array_equal(h["global"], t.history["global"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched", [True, False])
+def test_group_replays_after_history_readback(batched):
+    """A run() of graph replays only, behind a run() that read the histories back: the last
+    round's metrics are still scored (each engine's round bookkeeping is restored to the state
+    the captured rounds leave)."""
+    X, y = make_income_like(2000, seed=3)
+    trials = grid([(16,), (24, 8)], [0.004], [1, 2])
+    base = EngineConfig(max_rounds=40, early_stop=False, dtype="bf16", graph_rounds=8)
+    g = FedTrialGroup(X, y, 2, trials, None, base, group_graph_rounds=8, batched=batched)
+    g.run(16)
+    g.run(16)
+    for t, e in zip(g.trials, g.engines):
+        ref = HipRoundEngine(X, y, 2, replace(base, hidden=t.hidden, lr=t.lr, local_steps=t.local_steps), None,
+                             init_flat([14, *t.hidden, 2], 0))
+        ref.run(32)
+        np.testing.assert_array_equal(ref.history()["global"], t.history["global"])
+        assert t.final["accuracy"] > 0.5
