@@ -818,44 +818,63 @@ class TrialBatch {
         return a.kind == b.kind && std::memcmp(a.i, b.i, sizeof(a.i)) == 0;
     }
 
+    // Record every engine's launches, match them into batched launches (all checks done before
+    // anything is issued: on a mismatch the engines' round bookkeeping is rolled back and
+    // nothing ran), then issue them.
     template <class F>
     void issue(F&& per_engine, hipStream_t s) {
         upload(s);
-        std::vector<std::vector<FLLaunchRec>> recs(K_);
-        for (int k = 0; k < K_; ++k) {
-            engs_[k]->rec_ = &recs[k];
-            try {
-                per_engine(engs_[k]);
-            } catch (...) {
+        std::vector<int> flags0(K_);
+        for (int k = 0; k < K_; ++k) flags0[k] = engs_[k]->flags();
+        auto rollback = [&]() {
+            for (int k = 0; k < K_; ++k) {
                 engs_[k]->rec_ = nullptr;
-                throw;
+                engs_[k]->set_flags(flags0[k]);
             }
-            engs_[k]->rec_ = nullptr;
+        };
+        struct Planned {
+            const FLLaunchRec* m;
+            FLSel sel[5];
+            int cnt;
+        };
+        std::vector<std::vector<FLLaunchRec>> recs(K_);
+        std::vector<Planned> plan;
+        try {
+            for (int k = 0; k < K_; ++k) {
+                engs_[k]->rec_ = &recs[k];
+                per_engine(engs_[k]);
+                engs_[k]->rec_ = nullptr;
+            }
+            std::vector<size_t> pos(K_, 0);
+            for (const FLLaunchRec& m : recs[0]) {
+                // trials whose next recorded launch is this one: a prefix of the table
+                Planned pl;
+                pl.m = &m;
+                pl.cnt = 0;
+                for (int k = 0; k < K_; ++k) {
+                    const bool match = pos[k] < recs[k].size() && same_launch(recs[k][pos[k]], m);
+                    if (match && k != pl.cnt) throw std::runtime_error("TrialBatch: launch sequences do not align");
+                    if (match) ++pl.cnt;
+                }
+                for (int a = 0; a < 5; ++a) {
+                    pl.sel[a] = resolve(0, m.p[a]);
+                    for (int k = 1; k < pl.cnt; ++k) {
+                        const FLSel o = resolve(k, recs[k][pos[k]].p[a]);
+                        if (o.base != pl.sel[a].base || o.off != pl.sel[a].off)
+                            throw std::runtime_error("TrialBatch: trials disagree on a launch argument");
+                    }
+                }
+                for (int k = 0; k < pl.cnt; ++k) ++pos[k];
+                plan.push_back(pl);
+            }
+            for (int k = 0; k < K_; ++k)
+                if (pos[k] != recs[k].size()) throw std::runtime_error("TrialBatch: launch sequences do not align");
+        } catch (...) {
+            rollback();
+            throw;
         }
         const FLEngine& e0 = *engs_[0];
-        std::vector<size_t> pos(K_, 0);
-        for (const FLLaunchRec& m : recs[0]) {
-            // trials whose next recorded launch is this one: a prefix of the table
-            int cnt = 0;
-            for (int k = 0; k < K_; ++k) {
-                const bool match = pos[k] < recs[k].size() && same_launch(recs[k][pos[k]], m);
-                if (match && k != cnt) throw std::runtime_error("TrialBatch: launch sequences do not align");
-                if (match) ++cnt;
-            }
-            FLSel sel[5];
-            for (int a = 0; a < 5; ++a) {
-                sel[a] = resolve(0, m.p[a]);
-                for (int k = 1; k < cnt; ++k) {
-                    const FLSel o = resolve(k, recs[k][pos[k]].p[a]);
-                    if (o.base != sel[a].base || o.off != sel[a].off)
-                        throw std::runtime_error("TrialBatch: trials disagree on a launch argument");
-                }
-            }
-            for (int k = 0; k < cnt; ++k) ++pos[k];
-            launch(e0, m, sel, cnt, s);
-        }
-        for (int k = 0; k < K_; ++k)
-            if (pos[k] != recs[k].size()) throw std::runtime_error("TrialBatch: launch sequences do not align");
+        for (const Planned& pl : plan) launch(e0, *pl.m, pl.sel, pl.cnt, s);
     }
     void launch(const FLEngine& e, const FLLaunchRec& m, const FLSel* sel, int cnt, hipStream_t s) {
         const FLConfig& c = e.c_;
