@@ -22,6 +22,18 @@
 // of each phase; the phases here only hand data to each other through LDS.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Partial barrier through an LDS counter: a wave's LDS stores are complete (lgkmcnt) before
+// its lane 0 counts it in; waiting waves re-read the counter (s_sleep between reads) and may
+// then read what the counted waves stored.  Only waves that arrive are waited for.
+__device__ __forceinline__ void lds_count_arrive(int* cnt) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0) atomicAdd(cnt, 1);
+}
+__device__ __forceinline__ void lds_count_wait(int* cnt, int target) {
+    while (*reinterpret_cast<volatile int*>(cnt) < target) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
 // Gradient-slab stores.  The slab (n_blocks x P fp32, ~11 MB for the reference MLP) is read
 // once, by the next kernel: non-temporal stores stream it past the L2, so the train kernel's
 // end no longer writes back 11 MB of dirty lines (measured: fl_train 19.5 -> 14.8 us per

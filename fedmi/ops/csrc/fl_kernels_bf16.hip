@@ -294,8 +294,12 @@ __device__ __forceinline__ void slab_put(float* slab, int idx, float v) {
     if (F16) slab_store_h(reinterpret_cast<uint16_t*>(slab) + idx, v);
     else slab_store(slab + idx, v);
 }
+// Tiles go to waves [0, nw).  nw < FL_WAVES (waves nw.. run a long dgrad, wgrad_waves_bf16):
+// handed out from wave nw-1 down, so the low waves, which also sum the biases (threads 0..),
+// get the fewest.  nw = FL_WAVES: from wave 0 up (the dgrad items pair with them from the top).
 template <int RT, bool F16>
-__device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, const char* lds, float* __restrict__ slab) {
+__device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, const char* lds, float* __restrict__ slab,
+                                 int nw) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4, lq = lr >> 2, lp = lr & 3;
     const int K = d.dim[l], N = d.dim[l + 1];
@@ -303,7 +307,8 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
     const int ldd = e.lda[l + 1], lda = e.lda[l];
     const char* D = lds + e.dlt_off[l + 1];
     const char* act = lds + e.act_off[l];
-    for (int t = wave; t < otiles * itiles; t += FL_WAVES) {
+    const int t0 = nw == FL_WAVES ? wave : (wave < nw ? nw - 1 - wave : otiles * itiles);
+    for (int t = t0; t < otiles * itiles; t += nw) {
         const int ot = t / itiles, it = t - ot * itiles;
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         if (RT >= 2) {  // 32-row K chunks; k-runs 4lg.. and 16+4lg.. (8 consecutive rows per read)
@@ -339,6 +344,21 @@ __device__ void wgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, con
         }
         slab_put<F16>(slab, d.b_off[l] + o, s0 + s1);
     }
+}
+
+// Waves that take wgrad tiles in the backward phase of layer l.  The dgrad items (one per 16
+// output columns, handed out from the last wave down) are chains of kp[l+1]/32 dependent
+// k-steps; when they are long (the 50 -> 200 layer: 4 items of 7 steps) their waves take no
+// wgrad tiles, which otherwise stack on top of the chain and set the phase's length; with
+// the LDS arrival count that replaces the phase's barrier (fl_train_bf16_body.inc) the
+// (50, 200) layer's backward phase went 3.9 -> 3.1 us and the round 23.8 -> 23.3 us
+// (tools/probes/stamps_fine.py, profiles/ab_backward_waves_r2.log).  Short chains (the head's 1 step)
+// share the waves with the tiles as before.  Only the work-to-wave map changes: every tile
+// and item computes the same values.
+__device__ __forceinline__ int wgrad_waves_bf16(const MLPDescB& e, int l) {
+    const int items = l > 0 ? (e.kp[l] >> 4) : 0;
+    const int steps = e.kp[l + 1] >> 5;
+    return (items > 0 && steps >= 4 && 2 * items <= FL_WAVES) ? FL_WAVES - items : FL_WAVES;
 }
 
 // D_l[r][i] = (sum_o D_{l+1}[r][o] W_l[o][i]) * (act_l[r][i] > 0), all kp[l] columns.
