@@ -276,6 +276,11 @@ hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
                           const MLPDescB* e = nullptr, FLState* st_out = nullptr, int fold = 0,
                           int tail_a = 0, int fold_mask = FL_FOLD_B, const PeerArgs* peer = nullptr, int wx = 0,
                           int afold = 0);
+// (fl_adam_local.hip: the Adam kernel without the in-kernel exchange; fl_launch_adam picks it)
+hipError_t fl_launch_adam_local(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
+                                const float* anchor, float* comm, const FLState* st, int local_step,
+                                const MLPDescB& e, int pack, FLState* st_out, int fold, int tail_a, int fold_mask,
+                                hipStream_t s);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
