@@ -478,7 +478,10 @@ __device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDe
 // Kernels
 // ---------------------------------------------------------------------------------------
 // Kernel body shared by the single-engine and trial-batch entry points (fl_train_bf16_body.inc).
-template <int RT>
+// LAG: the lagged scoring pass (FL_EVAL_LAGGED, several clients) is compiled in; the other
+// modes get an instantiation without it -- its register copy of the round's weights stays out
+// of the forward pass (R = 32: 90 instead of 126 VGPRs; R = 64 spill-free).
+template <int RT, bool LAG>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                      const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
@@ -490,6 +493,7 @@ template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel pg_sel, FLSel si_sel,
                            FLSel so_sel, int local_step, int stage_local, int mode, FLSel cm_sel, int fold_mask) {
+    constexpr bool LAG = false;  // trial batches never run lagged rounds
     const FLTrialDesc& t = T[blockIdx.y];
     const FLConfig c = t.c;
     const FLBuffers b = t.b;
@@ -589,21 +593,17 @@ hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLCon
                                 bool stage_local, int mode, float* cm_out, int fold_mask) {
     if ((mode == FL_EVAL_FUSED || mode == FL_EVAL_LAGGED) && cm_out == nullptr) return hipErrorInvalidValue;
     const size_t lds = (size_t)e.lds_bytes;
+    const bool lag = mode == FL_EVAL_LAGGED;
+#define FLB_TRAIN(RT_, LAG_)                                                                                \
+    hipLaunchKernelGGL((fl_train_bf16_kernel<RT_, LAG_>), dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, \
+                       si, so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask)
     switch (c.R) {
-        case 16:
-            hipLaunchKernelGGL(fl_train_bf16_kernel<1>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
-                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask);
-            break;
-        case 32:
-            hipLaunchKernelGGL(fl_train_bf16_kernel<2>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
-                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask);
-            break;
-        case 64:
-            hipLaunchKernelGGL(fl_train_bf16_kernel<4>, dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, si,
-                               so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask);
-            break;
+        case 16: if (lag) FLB_TRAIN(1, true); else FLB_TRAIN(1, false); break;
+        case 32: if (lag) FLB_TRAIN(2, true); else FLB_TRAIN(2, false); break;
+        case 64: if (lag) FLB_TRAIN(4, true); else FLB_TRAIN(4, false); break;
         default: return hipErrorInvalidValue;
     }
+#undef FLB_TRAIN
     return hipGetLastError();
 }
 
@@ -720,7 +720,10 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
 #define FLB_SET(fn)                                                                                     \
     if (r == hipSuccess)                                                                                \
     r = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, v)
-    FLB_SET(fl_train_bf16_kernel<1>); FLB_SET(fl_train_bf16_kernel<2>); FLB_SET(fl_train_bf16_kernel<4>);
+    FLB_SET((fl_train_bf16_kernel<1, false>)); FLB_SET((fl_train_bf16_kernel<2, false>));
+    FLB_SET((fl_train_bf16_kernel<4, false>));
+    FLB_SET((fl_train_bf16_kernel<1, true>)); FLB_SET((fl_train_bf16_kernel<2, true>));
+    FLB_SET((fl_train_bf16_kernel<4, true>));
     FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>); FLB_SET(fl_eval_bf16_kernel<4>);
     FLB_SET(fl_train_bf16_batch_kernel<1>); FLB_SET(fl_train_bf16_batch_kernel<2>);
     FLB_SET(fl_train_bf16_batch_kernel<4>);
