@@ -130,8 +130,30 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
     const int n16 = e.param_bytes >> 4;
     const int kp = e.kp[0], lda = e.lda[0];
     const int nx = RT * 16 * kp;
-    uint4 pv[STAGE_P_UNROLL];
     float xv[STAGE_X_UNROLL];
+#ifndef FL_STAGE_VGPR
+    // the parameter region goes global -> LDS by DMA (global_load_lds_dwordx4: 1 KB per wave
+    // instruction, no VGPR round trip, no ds_write), the rows' loads issued first; the region's
+    // last partial 1 KB is exec-masked (the head partials follow it in LDS)
+#pragma unroll
+    for (int u = 0; u < STAGE_X_UNROLL; ++u) {
+        const int idx = threadIdx.x + u * FL_THREADS;
+        const int r = idx / kp, k = idx - r * kp;
+        const int row = row0 + r;
+        const bool ok = idx < nx && row < n_rows && k < F;
+        const float v = X[ok ? (size_t)row * F + k : 0];
+        xv[u] = ok ? v : 0.f;
+    }
+    {
+        const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        for (int c0 = wv * 64; c0 < n16; c0 += FL_THREADS)
+            if (c0 + ln < n16)
+                __builtin_amdgcn_global_load_lds(packed + (size_t)(c0 + ln) * 16,
+                                                 (__attribute__((address_space(3))) void*)(lds + e.param_off + c0 * 16),
+                                                 16, 0, 0);
+    }
+#else
+    uint4 pv[STAGE_P_UNROLL];
     // unpredicated loads (clamped indices): a conditionally written register array is
     // demoted to scratch by the compiler
 #pragma unroll
@@ -160,6 +182,7 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
         const int i = threadIdx.x + u * FL_THREADS;
         if (i < n16) dst[i] = pv[u];
     }
+#endif
     uint16_t* a = reinterpret_cast<uint16_t*>(lds + e.act_off[0]);
     uint16_t* alo = reinterpret_cast<uint16_t*>(lds + e.alo_off[0]);
 #pragma unroll
@@ -179,6 +202,9 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
         a[r * lda + k] = (uint16_t)bf16_bits(v);
         alo[r * lda + k] = (uint16_t)lo_bits(v);
     }
+#ifndef FL_STAGE_VGPR
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA has written the region (barrier follows)
+#endif
 }
 
 // Register half of a parameter-region copy (FL_EVAL_LAGGED: the round's own weights are
