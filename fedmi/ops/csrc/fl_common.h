@@ -281,6 +281,11 @@ hipError_t fl_launch_adam_local(const MLPDesc& d, const FLConfig& c, const FLBuf
                                 const float* anchor, float* comm, const FLState* st, int local_step,
                                 const MLPDescB& e, int pack, FLState* st_out, int fold, int tail_a, int fold_mask,
                                 hipStream_t s);
+// (fl_adam_local.hip: the Adam kernel for exchanges on LL chunks)
+hipError_t fl_launch_adam_ll(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
+                             const float* anchor, float* comm, const FLState* st, int local_step, const MLPDescB& e,
+                             int pack, FLState* st_out, int fold, int tail_a, int fold_mask, const PeerArgs& pa,
+                             int xchg, int afold, hipStream_t s);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,

@@ -325,7 +325,9 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
                const FLState* __restrict__ st, int local_step, MLPDescB e, int pack,
                FLState* __restrict__ st_out, int fold, int tail_a, int fold_mask, PeerArgs pa, int xchg,
                int afold) {
+#define ADAM_PA_LL (pa.ll != nullptr)
 #include "fl_adam_body.inc"
+#undef ADAM_PA_LL
 }
 
 // Trial batch (no peer exchange: the trials' FedAvg is one shared collective outside).
@@ -343,7 +345,9 @@ fl_adam_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pin_sel
     FLState* __restrict__ st_out = reinterpret_cast<FLState*>(fl_sel(t, st_out_sel));
     const PeerArgs pa = {};
     const int xchg = 0, afold = 0;
+#define ADAM_PA_LL false
 #include "fl_adam_body.inc"
+#undef ADAM_PA_LL
 }
 
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,
@@ -551,6 +555,9 @@ hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
     if (peer == nullptr && !wx && !afold)
         return fl_launch_adam_local(d, c, b, pin, anchor, comm, st, local_step, ee, e != nullptr ? 1 : 0, st_out, fold,
                                     tail_a, fold_mask, s);
+    if (pa.ll != nullptr)
+        return fl_launch_adam_ll(d, c, b, pin, anchor, comm, st, local_step, ee, e != nullptr ? 1 : 0, st_out, fold,
+                                 tail_a, fold_mask, pa, wx ? 1 : 0, afold ? 1 : 0, s);
 #endif
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
                        local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask, pa, wx ? 1 : 0,
