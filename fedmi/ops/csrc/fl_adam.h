@@ -11,8 +11,12 @@
 // the 16 partials are combined in a fixed order (deterministic), then wave 0 applies Adam
 // and writes the result at the parameter's image position.  Image padding is never
 // written (it stays 0 in every buffer).  The last block writes this rank's metric tail.
+#ifndef ADAM_WAVES
 #define ADAM_WAVES 16
+#endif
+#ifndef ADAM_DEPTH
 #define ADAM_DEPTH 16
+#endif
 // bf16 mode: parameter -> packed LDS-layout image(s).  A weight is stored as its bf16 hi part
 // and, `wlo_delta` bytes further, its lo part bf16(p - hi) (split-bf16 forward, fl_common.h);
 // a bias stays fp32.
