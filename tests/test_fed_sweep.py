@@ -137,3 +137,19 @@ def test_group_replays_after_history_readback(batched):
         ref.run(32)
         np.testing.assert_array_equal(ref.history()["global"], t.history["global"])
         assert t.final["accuracy"] > 0.5
+
+
+@pytest.mark.gpu
+def test_trial_batch_rejects_incompatible_engines():
+    """A native trial batch takes engines of one shape, ordered by local steps (descending)."""
+    from fedmi.ops import native
+    X, y = make_income_like(600, seed=2)
+    mk = lambda h, ls: HipRoundEngine(X, y, 2, EngineConfig(hidden=h, local_steps=ls, max_rounds=4, dtype="bf16",
+                                                            graph_rounds=0), None, init_flat([14, *h, 2], 0))
+    m = native()
+    with pytest.raises(RuntimeError, match="shape"):
+        m.TrialBatch([mk((16,), 1).engine, mk((24,), 1).engine])
+    with pytest.raises(RuntimeError, match="descending"):
+        m.TrialBatch([mk((16,), 1).engine, mk((16,), 2).engine])
+    tb = m.TrialBatch([mk((16,), 2).engine, mk((16,), 1).engine])
+    assert tb.size == 2
