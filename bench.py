@@ -152,7 +152,7 @@ def main(argv=None):
                     help="--config wide: FedAvg bucket dtype on the wire (fp32 master weights either way)")
     a = ap.parse_args(argv)
     from fedmi.parallel.comm import launch_env
-    if a.gpus > 1 and launch_env()[3] is None:
+    if a.gpus > 1 and launch_env()[1] == 1:  # no multi-process launcher around us: start the ranks
         return _self_launch(a, argv)
     if a.config == "wide":
         return main_wide(a)

@@ -23,7 +23,7 @@ working, but the data plane is different:
   - ``gloo``  -- CPU tensors (BASELINE config 1: "2-client FedAvg ... CPU + gloo").
 
 Launch with ``torchrun --nproc-per-node N --master-addr 127.0.0.1 ...`` or, like the reference,
-``mpiexec -n N python ...`` (Open MPI / MPICH / PMIx / Slurm environments are recognised,
+``mpiexec -n N python ...`` (Open MPI / MPICH environments are recognised,
 :func:`launch_env`); the node-local rank selects the device (fixes the reference's
 everyone-on-GPU-0).
 """
@@ -45,14 +45,14 @@ def _env_int(name: str, default: int) -> int:
 
 # Rank / size / node-local rank as set by the launcher that started this process: torchrun, or
 # the MPI launchers the reference is run with (``mpiexec -n k python <script>``, SURVEY §1 L0 --
-# Open MPI's and MPICH/Hydra's environment, Slurm's srun).  mpi4py is not needed: the control
+# Open MPI's and MPICH/Hydra's per-process environment).  mpi4py is not needed: the control
 # plane is gloo over a TCP store, so an MPI launch only has to tell every process who it is.
+# (Allocation-wide variables such as Slurm's SLURM_NTASKS are deliberately not read: they are
+# also set for a process started alone inside the allocation, which would then wait for peers.)
 _LAUNCH_VARS = (
     ("RANK", "WORLD_SIZE", "LOCAL_RANK"),                                              # torchrun
     ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"),    # Open MPI
     ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"),                                       # MPICH / Hydra
-    ("PMIX_RANK", "PMIX_SIZE", "PMIX_LOCAL_RANK"),                                     # PMIx
-    ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"),                                 # srun
 )
 
 
@@ -63,7 +63,7 @@ def launch_env() -> tuple:
     for i, (r, n, lr) in enumerate(_LAUNCH_VARS):
         if os.environ.get(r, "") != "" and os.environ.get(n, "") != "":
             rank, size = _env_int(r, 0), _env_int(n, 1)
-            return rank, size, _env_int(lr, rank), ("torchrun", "openmpi", "mpich", "pmix", "slurm")[i]
+            return rank, size, _env_int(lr, rank), ("torchrun", "openmpi", "mpich")[i]
     return 0, 1, 0, None
 
 

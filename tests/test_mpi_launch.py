@@ -1,6 +1,5 @@
 """Launch like the reference (``mpiexec -n k python <script>``): the processes
-learn rank / size / local rank from the MPI launcher's environment (Open MPI, MPICH/Hydra,
-PMIx, Slurm).  No MPI launcher exists in this image, so the test starts the processes itself
+learn rank / size / local rank from the MPI launcher's environment (Open MPI, MPICH/Hydra).  No MPI launcher exists in this image, so the test starts the processes itself
 with the environment Open MPI's and MPICH's launchers set."""
 import os
 import socket
@@ -41,6 +40,11 @@ def test_launch_env_recognises_launchers(monkeypatch):
     assert launch_env()[3] == "torchrun"      # torchrun's variables win
     monkeypatch.setenv("WORLD_SIZE", "")
     assert launch_env()[3] == "openmpi"       # an empty variable does not count
+    for k in ALL_VARS:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("SLURM_PROCID", "0")
+    monkeypatch.setenv("SLURM_NTASKS", "8")   # allocation-wide: a process started alone stays alone
+    assert launch_env() == (0, 1, 0, None)
 
 
 @pytest.mark.parametrize("flavour", ["openmpi", "mpich"])
