@@ -90,6 +90,8 @@ def main_wide(a, comm):
     res = run_wide_fedavg(comm, dims, a.synthetic_rows, a.rounds, micro_batch=a.micro_batch, dtype=a.dtype,
                           lr=a.lr, eval_every=a.eval_every, seed=a.seed + 7, verbose=not a.quiet,
                           allreduce_dtype=a.wide_allreduce)
+    if comm.rank == 0 and comm.rccl_env:
+        print(f"RCCL pinned: {comm.rccl_env}", flush=True)
     if comm.rank == 0:
         print(f"wide MLP {'-'.join(map(str, dims))}, {comm.size} client(s) x {a.synthetic_rows} rows: "
               f"{res['median_round_s'] * 1e3:.1f} ms/round, {res['tflops_per_client']:.1f} TFLOP/s per client, "
@@ -108,7 +110,9 @@ def main(argv=None):
         raise SystemExit("--participation must be in (0, 1]")
     if a.wide and a.participation < 1.0:
         raise SystemExit("--participation < 1 is not supported with --wide (every wide client trains every round)")
-    comm = get_world(backend=a.backend, device=a.device)
+    # RCCL protocol pinned per workload: LL for the fused engine's small FedAvg images, Simple
+    # for the wide MLP's large buckets (fedmi.parallel.comm.pin_rccl_env)
+    comm = get_world(backend=a.backend, device=a.device, rccl_proto="Simple" if a.wide else "LL")
     if a.wide:
         return main_wide(a, comm)
     rank, size = comm.Get_rank(), comm.Get_size()

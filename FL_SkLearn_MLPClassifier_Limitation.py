@@ -111,6 +111,9 @@ class FederatedMLPLearning:
                                  list(self.local_model.coefs_) + list(self.local_model.intercepts_),
                                  {"hidden": list(self.hidden), "lr": self.lr, "max_iter": self.max_iter,
                                   "warm_start": self.warm_start, "world": self.size, "history": history}, comm)
+        if comm is not None and comm.size > 1 and self.global_weights is not None:
+            from fedmi.parallel.consistency import check_replicas
+            check_replicas(comm, self.global_weights)  # every client holds the same average
         if self.rank == 0 and self.global_weights is not None:
             print("\nFinal Global Weight Statistics:")
             for idx, w in enumerate(self.global_weights):

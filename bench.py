@@ -84,6 +84,10 @@ def _self_launch(a, argv) -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
+    # build (or verify) the extension ONCE here -- compilation never touches the GPU -- so the N
+    # ranks do not all find it missing / stale and compile it at the same time
+    from fedmi.ops import build as _b
+    _b.build()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__),
            *(sys.argv[1:] if argv is None else list(argv))]
@@ -119,6 +123,25 @@ def torch_eager_anchor(X, y, dims, rounds: int = 60, warmup: int = 10) -> float:
     return (time.perf_counter() - t0) / rounds * 1e6
 
 
+def fp32_round_us(X, y, dims, a, rounds: int = 200) -> float:
+    """Untimed companion number at the reference's precision: the same one-client round with
+    the exact-fp32 kernels (v_mfma_f32_16x16x4_f32; reference [C] trains in fp32, C:65-66),
+    graph-replayed, microseconds per round (after the bf16 timed region, one client)."""
+    from fedmi.fl.engine import EngineConfig, HipRoundEngine
+    from fedmi.models.mlp import init_flat
+    g = _pick_graph_rounds(rounds)
+    cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=rounds + 3 * g + 64, early_stop=False,
+                       graph_rounds=g, dtype="fp32")
+    eng = HipRoundEngine(X, y, 2, cfg, None, init_flat(dims, seed=0))
+    eng.run(32, check_every=32)
+    eng.prime_graph(g)
+    eng.stream.synchronize()
+    t0 = time.perf_counter()
+    eng._issue(rounds, close=False)
+    eng.stream.synchronize()
+    return (time.perf_counter() - t0) / rounds * 1e6
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -139,6 +162,7 @@ def main(argv=None):
                     help="MFMA operand type of the fused kernels (fp32 accumulate, fp32 master weights)")
     ap.add_argument("--no-convergence", action="store_true")
     ap.add_argument("--no-anchor", action="store_true", help="skip the same-box eager torch anchor")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the untimed fp32-kernel round (one client)")
     ap.add_argument("--config", default="c", choices=["c", "wide", "sweep"],
                     help="c: the reference [C] workload (default, the headline metric) | wide: BASELINE config 3, "
                          "MLP 14-4096-4096-4096-2 on --wide-rows synthetic rows per client, bf16 NT GEMMs, "
@@ -180,10 +204,12 @@ def main(argv=None):
     dims = [14, *a.hidden, 2]
     g = a.graph_rounds or _pick_graph_rounds(a.steps)
     # (ranks sharing one GPU: with more than two, the Adam kernels' in-kernel chunk exchange can
-    # wait on a peer whose kernel cannot become resident; classic rounds there)
+    # wait on a peer whose kernel cannot become resident; classic rounds there -- the record's
+    # data_plane says so)
+    lag_off_shared = a.share_gpu and N > 2
     cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=a.warmup + a.steps + g + 16, early_stop=False,
                        rows_per_block=a.rows_per_block, graph_rounds=g, dtype=a.dtype,
-                       lagged_eval=not (a.share_gpu and N > 2))
+                       lagged_eval=not lag_off_shared)
     eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank),
                          n_total=a.rows_per_client * N)
 
@@ -212,6 +238,10 @@ def main(argv=None):
     eng.sync_history()
     h = eng.history()
     assert h["rounds_run"] == a.warmup + primed + a.steps + 1, (h["rounds_run"], primed)
+    # every rank must hold the same global model and metric history (raises otherwise: no number
+    # is reported for a run whose FedAvg was not FedAvg)
+    from fedmi.parallel.consistency import check_replicas
+    replicas_ok = check_replicas(comm, [eng.global_flat(), np.asarray(h["global"])])
     samples = a.rows_per_client * N * a.steps
     value = samples / dt
     anchor = None
@@ -219,6 +249,9 @@ def main(argv=None):
         if comm.rank == 0:
             anchor = torch_eager_anchor(X, y, dims)
         barrier()
+    fp32_us = None
+    if N == 1 and a.dtype != "fp32" and not a.no_fp32:
+        fp32_us = fp32_round_us(X, y, dims, a)
     # rounds-to-target is measured with the same kernels (dtype) as the throughput
     rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=cfg.lagged_eval)
     if comm.rank == 0:
@@ -239,13 +272,21 @@ def main(argv=None):
                        "global_batch": a.rows_per_client * N, "seq_len": 1,
                        "parallelism": f"fedavg{N} (1 client/{'shared ' if a.share_gpu else ''}GPU, "
                                       f"{eng.aggregation} all-reduce)",
-                       "data_plane": eng.aggregation,
+                       "data_plane": eng.aggregation + (
+                           " (classic rounds: lagged evaluation disabled for > 2 ranks sharing one GPU)"
+                           if lag_off_shared else ""),
+                       "round_design": ("fused-eval" if N == 1 else
+                                        "lagged-eval+adam-fedavg" if eng.engine.adam_exchange else
+                                        "lagged-eval" if eng.engine.lagged else "classic"),
+                       "rccl_env": comm.rccl_env,
                        "rows_per_client": a.rows_per_client, "optimizer": "Adam(0.004)+StepLR(30,0.5)",
                        "graph_rounds": g, "share_gpu": bool(a.share_gpu)},
             "samples_per_sec_per_client": value / N,
             "us_per_round": dt / a.steps * 1e6,
             "torch_eager_us_per_round_1client": anchor,
+            "fp32_us_per_round": fp32_us if a.dtype != "fp32" else dt / a.steps * 1e6,
             "final_train_acc_synthetic": float(h["global"][-1][0]),
+            "replicas_consistent": replicas_ok,
             "rounds_to_target": rtt,
         }
         print(json.dumps(rec), flush=True)
@@ -262,7 +303,7 @@ def main_wide(a) -> None:
 
     from fedmi.parallel.comm import resolve_backend
     a.backend = resolve_backend(a.backend, "cuda")
-    comm = get_world(backend="rccl" if a.backend == "xgmi" else a.backend, device="cuda")
+    comm = get_world(backend="rccl" if a.backend == "xgmi" else a.backend, device="cuda", rccl_proto="Simple")
     N = comm.size
     if N != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
@@ -295,6 +336,8 @@ def main_wide(a) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     value = a.wide_rows * N * a.steps / dt
+    from fedmi.parallel.consistency import check_replicas
+    replicas_ok = check_replicas(comm, [c.params])
     if comm.rank == 0:
         print(json.dumps({
             "metric": "train samples/s, wide-MLP FedAvg (BASELINE config 3)", "value": value,
@@ -305,9 +348,10 @@ def main_wide(a) -> None:
             "data": f"synthetic income-shaped (device Philox), {a.wide_rows} rows/client; random-init weights",
             "config": {"model": "MLP " + "-".join(map(str, dims)), "global_batch": a.wide_rows * N, "seq_len": 1,
                        "parallelism": f"fedavg{N} (1 client/GPU, per-layer RCCL buckets, "
-                                      f"{a.wide_allreduce} on the wire)"},
+                                      f"{a.wide_allreduce} on the wire)", "rccl_env": comm.rccl_env},
             "tflops_per_client": c.flops_per_round / (dt / a.steps) / 1e12,
             "local_train_acc_synthetic": c.metrics()["accuracy"],
+            "replicas_consistent": replicas_ok,
             "micro_batch": c.mb,
         }), flush=True)
     comm.close()
@@ -356,6 +400,8 @@ def main_sweep(a) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     value = len(trials) * a.steps * N / dt
+    from fedmi.parallel.consistency import check_replicas
+    replicas_ok = check_replicas(comm, [e.global_flat() for e in grp.engines])
     best = grp.best()
     if comm.rank == 0:
         print(json.dumps({
@@ -366,9 +412,10 @@ def main_sweep(a) -> int:
             "data": f"synthetic income-shaped (device Philox), {a.rows_per_client} rows/client; random-init weights",
             "config": {"model": "MLP 14-{hidden}-2 grid", "global_batch": a.rows_per_client * N, "seq_len": 1,
                        "parallelism": f"fedavg{N} x {len(trials)} trials/GPU ({len(grp.batches)} trial batches, "
-                                      f"one all-reduce per round)",
+                                      f"one all-reduce per round)", "rccl_env": comm.rccl_env,
                        "trials": [[list(t.hidden), t.lr, t.local_steps] for t in trials]},
             "us_per_trial_round": dt / (a.steps * len(trials)) * 1e6,
+            "replicas_consistent": replicas_ok,
             "best_trial": {"hidden": list(best.hidden), "lr": best.lr, "local_steps": best.local_steps,
                            "train_acc_synthetic": best.final["accuracy"]},
         }), flush=True)

@@ -587,7 +587,10 @@ class HipRoundEngine(RoundEngineBase):
             return False
         if cfg.grad_slab == "fp16":
             return True
-        return bool(self.X.numel() == 0 or float(self.X.abs().max()) <= FP16_SLAB_MAX_ABS_X)
+        if self.X.numel() == 0:
+            return True
+        lo, hi = torch.aminmax(self.X)  # two scalars, no |X| temporary of the whole shard
+        return bool(max(-float(lo), float(hi)) <= FP16_SLAB_MAX_ABS_X)
 
     def _round_tables(self, client_sizes=None):
         """Host-built device tables (fl_common.h FLBuffers::sched / rtab): per optimizer-step

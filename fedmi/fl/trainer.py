@@ -127,7 +127,16 @@ class FederatedMLPLearning:
             raise
         finally:
             wd.close()
-        self.global_weights = flat_to_dict(eng.global_flat(), eng.dims)
+        gflat = eng.global_flat()
+        self.global_weights = flat_to_dict(gflat, eng.dims)
+        if comm is not None and getattr(comm, "size", 1) > 1:
+            # every client must end the run holding the same global model and metric history
+            # (C:119-120); a data-plane fault raises here instead of passing as a result
+            from ..parallel.consistency import check_replicas
+            eng.sync_history()
+            self.replicas_consistent = check_replicas(comm, [gflat, np.asarray(eng.history()["global"])])
+        else:
+            self.replicas_consistent = True
         return eng.hist.global_metrics_dict()
 
     # ---- extras ----

@@ -124,10 +124,14 @@ class WideClient:
             self.bhp = torch.zeros(256, **f32)
             self.logits_p = torch.empty(mb, 256, **f32)
             self.logits = self.logits_p[:, :dims[-1]]
-        # bf16 FedAvg buckets (allreduce_dtype="bf16"): the scaled weights cross the links as bf16
-        # (half the bytes), summed by RCCL in bf16 and widened back into the fp32 master copy
+        # bf16 FedAvg buckets (allreduce_dtype="bf16"): half the bytes on the links.  What crosses
+        # them is the scaled round DELTA n_i/N * (w_local - w_global_prev) in bf16 (summed by RCCL),
+        # added back to the fp32 previous global model ``gprev``: the master weights stay fp32 and
+        # bf16 rounds only the (small) update, so late-schedule Adam steps are not rounded away
+        # (every rank starts from the same init, so gprev is the same on every rank)
         self.send_bf16 = (torch.empty(flat.numel(), dtype=torch.bfloat16, device=dev)
                           if allreduce_dtype == "bf16" and self.world > 1 else None)
+        self.gprev = flat.clone() if self.send_bf16 is not None else None
         self._quantize()
 
     # ------------------------------------------------------------------
@@ -396,12 +400,14 @@ class WideClient:
                 if self.send_bf16 is None:
                     self.comm.allreduce_(seg, scale=self.agg)
                 else:
-                    # the n_i / N weight is applied by the fp32 -> bf16 pass that fills the bucket
-                    bseg = self.send_bf16[off:end]
-                    self.m.to_bf16(seg.data_ptr(), bseg.data_ptr(), seg.numel(), self.comm_stream.cuda_stream,
-                                   self.agg)
+                    # bf16 delta on the wire, fp32 master kept: one pass fills the bucket with
+                    # bf16(n_i/N * (w - gprev)), one adds the reduced deltas to gprev (and w)
+                    bseg, gseg = self.send_bf16[off:end], self.gprev[off:end]
+                    cs = self.comm_stream.cuda_stream
+                    self.m.fedavg_delta_bf16(seg.data_ptr(), gseg.data_ptr(), bseg.data_ptr(), seg.numel(), self.agg,
+                                             cs)
                     self.comm.allreduce_(bseg)
-                    seg.copy_(bseg)
+                    self.m.fedavg_apply_delta(seg.data_ptr(), gseg.data_ptr(), bseg.data_ptr(), seg.numel(), cs)
             self._quantize_layer(l, self.comm_stream)
             ev = torch.cuda.Event()
             ev.record(self.comm_stream)
@@ -494,7 +500,11 @@ def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int
             print(msg, flush=True)
     steady = times[1:] or times
     dt = float(np.median(steady))
+    c.sync()
+    from ..parallel.consistency import check_replicas
+    replicas_ok = check_replicas(comm, [c.params]) if world > 1 else True
     return {"loss": losses, "accuracy": accs, "round_s": times, "median_round_s": dt,
+            "replicas_consistent": replicas_ok,
             "tflops_per_client": c.flops_per_round / dt / 1e12,
             "samples_per_s_per_client": rows_per_client / dt}
 
@@ -546,6 +556,8 @@ def load_wide(path: str, client: WideClient) -> int:
         client.params.copy_(torch.as_tensor(flat, device=client.dev))
         client.m_.copy_(torch.as_tensor(st["exp_avg"], device=client.dev))
         client.v_.copy_(torch.as_tensor(st["exp_avg_sq"], device=client.dev))
+        if client.gprev is not None:
+            client.gprev.copy_(client.params)
     client._quantize()
     client.stream.synchronize()
     client.round = int(meta["round"])

@@ -3,7 +3,10 @@
 ``native()`` returns the compiled gfx950 extension (``fedmi/ops/_fedmi_hip*.so``: the
 fused FL round kernels, the RCCL communicator, HIP-graph capture).  On a machine with a
 GPU the extension is REQUIRED: every device code path goes through it and there is no
-silent eager fallback -- if it is missing or fails to load, ``native()`` raises.  On a
+silent eager fallback -- if it is missing or fails to load, ``native()`` raises.  A binary
+is only loaded if the source digest compiled into it matches this tree's sources
+(``build.so_digest`` / ``build.build_digest``): a stale ``.so`` is rebuilt (under a file
+lock, so concurrent ranks build once) or, with ``FEDMI_NO_BUILD=1``, refused.  On a
 CPU-only host, ``fedmi.fl.engine.TorchRoundEngine`` implements the same round math with
 eager torch ops (used as the CPU plumbing path and as the numerics oracle in tests).
 """
@@ -30,17 +33,22 @@ def native(build_if_missing: bool = True):
         spec.loader.exec_module(mod)
         _NATIVE = mod
         return _NATIVE
+    from . import build as _b
+    if not _b.is_fresh():
+        have = _b.so_digest(_b.TARGET)
+        why = ("not built" if not os.path.isfile(_b.TARGET) else
+               f"stale (built from sources {have}, tree is {_b.build_digest()})")
+        if not build_if_missing or os.environ.get("FEDMI_NO_BUILD", "0") == "1":
+            raise ImportError(f"fedmi native extension {why}: run `python -m fedmi.ops.build`")
+        import sys
+        print(f"[fedmi] native extension {why}; building", file=sys.stderr, flush=True)
+        _b.build()
     try:
         _NATIVE = importlib.import_module("fedmi.ops._fedmi_hip")
-        return _NATIVE
-    except ImportError as e:  # not built yet
+    except ImportError as e:
         _NATIVE_ERR = e
-    if build_if_missing and os.environ.get("FEDMI_NO_BUILD", "0") != "1":
-        from . import build as _b
-        _b.build()
-        _NATIVE = importlib.import_module("fedmi.ops._fedmi_hip")
-        return _NATIVE
-    raise ImportError(f"fedmi native extension unavailable: {_NATIVE_ERR}")
+        raise ImportError(f"fedmi native extension unavailable: {_NATIVE_ERR}") from e
+    return _NATIVE
 
 
 def native_available() -> bool:

@@ -11,9 +11,12 @@ Usage: ``python -m fedmi.ops.build [--force] [-j N]``.
 from __future__ import annotations
 
 import argparse
+import contextlib
+import fcntl
 import glob
 import hashlib
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -44,21 +47,67 @@ def _sources() -> list:
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _digest(paths) -> str:
+def _headers() -> list:
+    return sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc")))
+
+
+def source_digest() -> str:
+    """Digest of every source and header the extension is built from (+ the target arch).
+    It is compiled INTO the extension (``SRC_DIGEST``, and a marker string found by
+    :func:`so_digest` without loading the library), so a binary can be matched to the tree it
+    runs from wherever it travels -- the ``_build`` stamp does not go to the GPU box."""
     h = hashlib.sha256()
-    for p in sorted(paths):
+    for p in sorted(_sources() + _headers()):
+        h.update(os.path.basename(p).encode())
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(ARCH.encode())
-    h.update(os.environ.get("FEDMI_HIPCC_FLAGS", "").encode())
     return h.hexdigest()[:16]
 
 
-def _compile(src: str) -> str:
+_MARKER = b"FEDMI_SRC_DIGEST:"
+
+
+def so_digest(path: str = TARGET):
+    """The source digest compiled into the extension at ``path`` (``None``: no file, or a
+    binary built before digests were embedded).  Reads the file; never loads it."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    m = re.search(re.escape(_MARKER) + rb"([0-9a-f]{16})", data)
+    return m.group(1).decode() if m else None
+
+
+def build_digest() -> str:
+    """What a build of this tree with the current ``FEDMI_HIPCC_FLAGS`` embeds: the source
+    digest, or (experiment flags set) a digest of it and the flags, so a variant build is
+    never taken for the plain one."""
+    flags = os.environ.get("FEDMI_HIPCC_FLAGS", "").strip()
+    if not flags:
+        return source_digest()
+    return hashlib.sha256((source_digest() + flags).encode()).hexdigest()[:16]
+
+
+@contextlib.contextmanager
+def _build_lock():
+    """Exclusive across processes: N ranks that find the extension missing or stale at once
+    build it one after another (the later ones then see a fresh binary and return)."""
+    os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, "lock"), "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
+
+
+def _compile(src: str, digest: str) -> str:
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
     extra = os.environ.get("FEDMI_HIPCC_FLAGS", "").split()  # experiments, e.g. -DFL_THREADS=1024
     cmd = ["hipcc", "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}", *extra,
-           "-I" + CSRC, *_pybind_includes(), src, "-o", obj]
+           f'-DFEDMI_SRC_DIGEST="{digest}"', "-I" + CSRC, *_pybind_includes(), src, "-o", obj]
     if src.endswith(".cpp"):
         cmd[1:1] = ["-x", "hip"]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -67,26 +116,32 @@ def _compile(src: str) -> str:
     return obj
 
 
+def is_fresh() -> bool:
+    """The in-tree extension exists and was built from the sources in this tree."""
+    return so_digest(TARGET) == build_digest()
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    with _build_lock():
+        return _build_locked(force, jobs, verbose)
+
+
+def _build_locked(force: bool, jobs: int, verbose: bool) -> str:
     srcs = _sources()
-    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc"))
-    stamp = os.path.join(BUILD, "stamp")
-    digest = _digest(srcs + headers)
-    if not force and os.path.isfile(TARGET) and os.path.isfile(stamp):
-        with open(stamp) as f:
-            if f.read().strip() == digest:
-                return TARGET
+    digest = build_digest()
+    if not force and so_digest(TARGET) == digest:
+        return TARGET
     os.makedirs(BUILD, exist_ok=True)
     with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
-        objs = list(ex.map(_compile, srcs))
+        objs = list(ex.map(lambda p: _compile(p, digest), srcs))
     tlib = _torch_lib()
-    link = ["g++", "-shared", "-o", TARGET, *objs, f"-L{tlib}", "-lamdhip64", "-lrccl",
+    tmp = TARGET + f".tmp{os.getpid()}"
+    link = ["g++", "-shared", "-o", tmp, *objs, f"-L{tlib}", "-lamdhip64", "-lrccl",
             f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"]
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout}\n{r.stderr}")
-    with open(stamp, "w") as f:
-        f.write(digest)
+    os.replace(tmp, TARGET)  # atomic: a process mapping the old file keeps its copy
     if verbose:
         print(f"built {TARGET}")
     return TARGET

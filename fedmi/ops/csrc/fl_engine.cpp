@@ -921,6 +921,12 @@ static void synth(uintptr_t X, uintptr_t y, long long n, int F, unsigned long lo
                               as_ptr<const float>(w2), H, as_stream(stream), label_noise));
 }
 
+#ifndef FEDMI_SRC_DIGEST
+#define FEDMI_SRC_DIGEST "unknown"
+#endif
+// found by fedmi/ops/build.py:so_digest in the file bytes (no load needed)
+__attribute__((used)) static const char kSrcDigestMarker[] = "FEDMI_SRC_DIGEST:" FEDMI_SRC_DIGEST;
+
 static py::dict device_info(int dev) {
     hipDeviceProp_t p;
     HIP_CHECK(hipGetDeviceProperties(&p, dev));
@@ -985,6 +991,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
           py::arg("w1"), py::arg("w2"), py::arg("H"), py::arg("stream"), py::arg("label_noise") = 0.f);
     m.def("device_info", &device_info);
     m.attr("STATE_BYTES") = (int)sizeof(FLState);
+    m.attr("SRC_DIGEST") = std::string(kSrcDigestMarker + sizeof("FEDMI_SRC_DIGEST:") - 1);
     register_trainer(m);
     register_peer(m);
 }

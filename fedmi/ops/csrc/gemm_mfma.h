@@ -37,4 +37,6 @@ hipError_t splitk_reduce_launch(const float* slab, size_t stride, int splits, fl
                                 hipStream_t s);
 hipError_t colsum_launch(const float* X, int M, int N, int ld, float* out, float beta, int batch, long long sX,
                          long long sOut, const int* active, hipStream_t s);
+hipError_t fedavg_delta_bf16_launch(const float* w, const float* g, void* d, size_t n, float scale, hipStream_t s);
+hipError_t fedavg_apply_delta_launch(float* w, float* g, const void* d, size_t n, hipStream_t s);
 hipError_t f32_to_bf16_launch(const float* x, void* y, size_t n, hipStream_t s, float scale = 1.f);

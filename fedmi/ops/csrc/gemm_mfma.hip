@@ -264,6 +264,79 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, __hip_bfloat16* 
     if (i < n) y[i] = __float2bfloat16(x[i] * scale);
 }
 
+// bf16 FedAvg buckets that keep the fp32 master (wide client, allreduce_dtype="bf16"): the wire
+// carries the scaled DELTA d = bf16(scale * (w_local - w_global_prev)), whose bf16 rounding is
+// relative to one round's update instead of to the weight, and the reduced sum is added back
+// to the fp32 previous global model: w = g = g + sum_i d_i.  VEC: 4 elements per thread
+// (float4 loads, one 8-byte bf16 store; 16/8-byte aligned operands), else one per thread.
+template <bool VEC>
+__global__ void fedavg_delta_bf16_kernel(const float* __restrict__ w, const float* __restrict__ g,
+                                         __hip_bfloat16* __restrict__ d, size_t n, float scale) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t i = VEC ? t * 4 : t;
+    if (VEC && i + 4 <= n) {
+        const float4 a = *reinterpret_cast<const float4*>(w + i);
+        const float4 b = *reinterpret_cast<const float4*>(g + i);
+        __hip_bfloat16 o[4] = {__float2bfloat16(scale * (a.x - b.x)), __float2bfloat16(scale * (a.y - b.y)),
+                               __float2bfloat16(scale * (a.z - b.z)), __float2bfloat16(scale * (a.w - b.w))};
+        *reinterpret_cast<uint2*>(d + i) = *reinterpret_cast<const uint2*>(o);
+    } else {
+        for (size_t j = i; j < n && j < i + (VEC ? 4 : 1); ++j) d[j] = __float2bfloat16(scale * (w[j] - g[j]));
+    }
+}
+
+template <bool VEC>
+__global__ void fedavg_apply_delta_kernel(float* __restrict__ w, float* __restrict__ g,
+                                          const __hip_bfloat16* __restrict__ d, size_t n) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t i = VEC ? t * 4 : t;
+    if (VEC && i + 4 <= n) {
+        float4 b = *reinterpret_cast<const float4*>(g + i);
+        const uint2 raw = *reinterpret_cast<const uint2*>(d + i);
+        const __hip_bfloat16* q = reinterpret_cast<const __hip_bfloat16*>(&raw);
+        b.x += __bfloat162float(q[0]); b.y += __bfloat162float(q[1]);
+        b.z += __bfloat162float(q[2]); b.w += __bfloat162float(q[3]);
+        *reinterpret_cast<float4*>(g + i) = b;
+        *reinterpret_cast<float4*>(w + i) = b;
+    } else {
+        for (size_t j = i; j < n && j < i + (VEC ? 4 : 1); ++j) {
+            const float v = g[j] + __bfloat162float(d[j]);
+            g[j] = v;
+            w[j] = v;
+        }
+    }
+}
+
+static bool fedavg_vec_ok(const void* w, const void* g, const void* d) {
+    return !((((uintptr_t)w | (uintptr_t)g) & 15) || ((uintptr_t)d & 7));
+}
+
+hipError_t fedavg_delta_bf16_launch(const float* w, const float* g, void* d, size_t n, float scale, hipStream_t s) {
+    auto* o = reinterpret_cast<__hip_bfloat16*>(d);
+    if (fedavg_vec_ok(w, g, d)) {
+        const size_t th = (n + 3) / 4;
+        hipLaunchKernelGGL(fedavg_delta_bf16_kernel<true>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, w, g,
+                           o, n, scale);
+    } else {
+        hipLaunchKernelGGL(fedavg_delta_bf16_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, g,
+                           o, n, scale);
+    }
+    return hipGetLastError();
+}
+
+hipError_t fedavg_apply_delta_launch(float* w, float* g, const void* d, size_t n, hipStream_t s) {
+    auto* q = reinterpret_cast<const __hip_bfloat16*>(d);
+    if (fedavg_vec_ok(w, g, d)) {
+        const size_t th = (n + 3) / 4;
+        hipLaunchKernelGGL(fedavg_apply_delta_kernel<true>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, w, g,
+                           q, n);
+    } else {
+        hipLaunchKernelGGL(fedavg_apply_delta_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, g,
+                           q, n);
+    }
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 template <typename T, bool AK, bool BK_>
 static hipError_t launch_t(const GemmArgs& g, int epi, int splits, int batch, hipStream_t s) {

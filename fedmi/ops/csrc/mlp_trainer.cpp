@@ -340,6 +340,16 @@ static void to_bf16_py(uintptr_t x, uintptr_t y, size_t n, uintptr_t stream, flo
                                 reinterpret_cast<hipStream_t>(stream), scale));
 }
 
+static void fedavg_delta_bf16_py(uintptr_t w, uintptr_t g, uintptr_t d, size_t n, float scale, uintptr_t stream) {
+    TR_CHECK(fedavg_delta_bf16_launch(reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(g),
+                                      reinterpret_cast<void*>(d), n, scale, reinterpret_cast<hipStream_t>(stream)));
+}
+
+static void fedavg_apply_delta_py(uintptr_t w, uintptr_t g, uintptr_t d, size_t n, uintptr_t stream) {
+    TR_CHECK(fedavg_apply_delta_launch(reinterpret_cast<float*>(w), reinterpret_cast<float*>(g),
+                                       reinterpret_cast<const void*>(d), n, reinterpret_cast<hipStream_t>(stream)));
+}
+
 // Single-problem loss head (wide path): softmax CE (mode 0) / sklearn binary (mode 1).
 static void xent_py(uintptr_t z, int ldz, uintptr_t y, int M, int C, int mode, float scale, uintptr_t dz, int lddz,
                     uintptr_t loss_acc, uintptr_t stream) {
@@ -427,6 +437,8 @@ void register_trainer(py::module_& m) {
     m.def("rowsum_bf16", &rowsum_bf16_py);
     m.def("pad_bf16", &pad_bf16_py);
     m.def("xent", &xent_py);
+    m.def("fedavg_delta_bf16", &fedavg_delta_bf16_py);
+    m.def("fedavg_apply_delta", &fedavg_apply_delta_py);
     m.def("adam_flat", &adam_flat_py);
     py::class_<MLPTrainerT<float>>(m, "MLPTrainer")
         .def(py::init<std::vector<int>, int, py::dict, py::dict>())

@@ -97,13 +97,30 @@ def _c_stdout_to_stderr():
         os.dup2(saved, 1)
         os.close(saved)
 
+RCCL_ALGO_DEFAULT = "Ring"
+
+
+def pin_rccl_env(proto: str) -> dict:
+    """Pin RCCL's algorithm and protocol for reproducible collectives and return
+    what this process's communicators will use.  RCCL reads them when a communicator is
+    created, so this runs before ``ncclCommInitRank`` / the nccl process group.  Values the
+    user exported win.  Defaults: Ring (xGMI is point-to-point; every rank on one ring over its
+    direct links) with the protocol of the messages this process sends -- LL for the
+    latency-bound FedAvg images of the fused engine (45 KB - 1 MB), Simple for the wide
+    MLP's bandwidth-bound per-layer buckets (16-67 MB)."""
+    os.environ.setdefault("NCCL_ALGO", RCCL_ALGO_DEFAULT)
+    os.environ.setdefault("NCCL_PROTO", proto)
+    return {"NCCL_ALGO": os.environ["NCCL_ALGO"], "NCCL_PROTO": os.environ["NCCL_PROTO"]}
+
+
 class Comm:
     """``rccl=False`` (with ``backend='xgmi'``) skips the RCCL communicator: device
     all-reduces outside the round engine then go through the host.  That is the setting for
-    several ranks sharing one GPU (tests), which RCCL does not support."""
+    several ranks sharing one GPU (tests), which RCCL does not support.  ``rccl_proto``: the
+    RCCL protocol pinned for this process (:func:`pin_rccl_env`; reported as ``rccl_env``)."""
 
     def __init__(self, backend: str = "auto", device: Optional[str] = None, timeout_s: float = 600.0,
-                 rccl: bool = True):
+                 rccl: bool = True, rccl_proto: str = "LL"):
         self.rank, self.size, self.local_rank, self.launcher = launch_env()
         if device is None or device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
@@ -121,6 +138,7 @@ class Comm:
         self.backend = backend
         self.peer_allreduce = backend == "xgmi"   # round engines use the one-shot xGMI all-reduce
         self.native = None       # RcclComm
+        self.rccl_env = None     # pinned NCCL_ALGO / NCCL_PROTO when an RCCL communicator exists
         self._nccl_group = None
         self._initialized_here = False
         if self.size > 1:
@@ -134,6 +152,8 @@ class Comm:
                     dist.init_process_group("gloo", rank=self.rank, world_size=self.size,
                                             timeout=timedelta(seconds=timeout_s))
                 self._initialized_here = True
+            if backend in ("rccl", "nccl") or (backend == "xgmi" and rccl):
+                self.rccl_env = pin_rccl_env(rccl_proto)
             if backend == "rccl" or (backend == "xgmi" and rccl):
                 from ..ops import native
                 m = native()
@@ -235,11 +255,12 @@ class Comm:
 _WORLD: Optional[Comm] = None
 
 
-def get_world(backend: str = "auto", device: Optional[str] = None, rccl: bool = True) -> Comm:
+def get_world(backend: str = "auto", device: Optional[str] = None, rccl: bool = True,
+              rccl_proto: str = "LL") -> Comm:
     """Process-wide communicator (the analogue of ``MPI.COMM_WORLD``)."""
     global _WORLD
     if _WORLD is None:
-        _WORLD = Comm(backend=backend, device=device, rccl=rccl)
+        _WORLD = Comm(backend=backend, device=device, rccl=rccl, rccl_proto=rccl_proto)
     return _WORLD
 
 

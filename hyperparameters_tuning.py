@@ -151,6 +151,9 @@ def main(argv=None):
     if a.save and rank == 0:
         save_sweep(a.save, results, best, {"world": comm.Get_size(), "max_iter": a.max_iter})
     comm.Barrier()
+    if comm.Get_size() > 1:
+        from fedmi.parallel.consistency import check_replicas
+        check_replicas(comm, [np.asarray(w) for r in results for w in r.weights])  # every trial's average
     if rank == 0:
         print("\n\nBest MEASURED RESULTS")
         print("\nBest Global Hyperparameters:", {"hidden_layer_sizes": best.hidden, "learning_rate": best.lr})
@@ -185,6 +188,9 @@ def federated_main(a):
     best, done = run_fed_sweep(X_local, y_local, 2, comm, trials, rounds=rounds, trials_per_gpu=a.trials_per_gpu,
                                base=base, backend="torch" if a.device == "cpu" else "auto")
     wall = time.time() - t0
+    if size > 1:
+        from fedmi.parallel.consistency import check_replicas
+        check_replicas(comm, [np.asarray(t.history["global"]) for t in done])
     if rank == 0:
         for t in done:
             if not a.quiet:

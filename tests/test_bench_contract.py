@@ -13,8 +13,9 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config"}
 
 
-def _run(args, n=1):
-    r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True, timeout=300)
+def _run(args, n=1, timeout=300):
+    r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -28,7 +29,7 @@ def _run(args, n=1):
 def test_bench_headline_contract():
     rec = _run(["--steps", "50", "--warmup", "10", "--no-convergence"])
     assert rec["steps"] == 50 and rec["warmup"] == 10 and rec["dtype"] == "bf16"
-    assert rec["vs_baseline"] > 0
+    assert rec["vs_baseline"] > 0 and rec["replicas_consistent"] is True
 
 
 @pytest.mark.gpu
@@ -40,6 +41,20 @@ def test_bench_self_launch_shared_gpu():
                 "--no-anchor"], n=2)
     assert rec["config"]["data_plane"] == "xgmi-oneshot+adam", rec["config"]
     assert rec["config"]["share_gpu"] is True
+    assert rec["replicas_consistent"] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_self_launch_eight_ranks_shared_gpu():
+    """--gpus 8 (a whole MI355X node's world) with every rank on cuda:0: 8 self-launched ranks,
+    the peer protocol's start-up self-test at world 8, classic rounds (the record says the lagged
+    design is off for > 2 ranks sharing a GPU), and the replica check on every rank."""
+    rec = _run(["--gpus", "8", "--share-gpu", "--steps", "40", "--warmup", "5", "--no-convergence",
+                "--no-anchor"], n=8, timeout=540)
+    assert rec["config"]["data_plane"].startswith("xgmi-oneshot (classic rounds"), rec["config"]
+    assert rec["config"]["round_design"] == "classic"
+    assert rec["replicas_consistent"] is True
 
 
 @pytest.mark.gpu

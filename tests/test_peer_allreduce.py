@@ -190,19 +190,23 @@ def _worker4(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def test_peer_four_ranks_lagged_adam_exchange():
-    """W = 4 (more ranks than the 2-rank test: the unrolled rank loops and chunk-flag rows):
-    self-tests pass and the lagged engine with FedAvg inside the Adam kernel -- LL weight chunks
-    (value + call index in one 8-byte push) and publish / wait / pull chunks alike -- equals
-    classic rounds over the standalone peer kernel bit for bit, with unequal shard sizes."""
-    world = 4
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [4, 8])
+def test_peer_many_ranks_lagged_adam_exchange(world):
+    """W = 4 and W = 8 = PEER_MAX_WORLD, the world of an MI355X node (every unrolled rank loop,
+    every chunk-flag row and all 8 sources of the LL ring in use): self-tests of all three
+    protocols (standalone pull, publish / wait / pull chunks, LL chunks) pass, and the lagged
+    engine with FedAvg inside the Adam kernel -- LL weight chunks (value + call index in one
+    8-byte push) and publish / wait / pull chunks alike -- equals classic rounds over the
+    standalone peer kernel bit for bit, with unequal shard sizes; every rank ends with the same
+    global model.  All ranks share cuda:0 (the 1-GPU box), so the pulls stay on one device."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker4, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = sorted([q.get(timeout=110) for _ in range(world)], key=lambda t: t[0])
+    out = sorted([q.get(timeout=110 + 30 * world) for _ in range(world)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=30)
     for rank, res, err in out:

@@ -31,7 +31,7 @@ def _data(rank, dev):
     return torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
 
 
-def _worker(rank, port, q, wire):
+def _worker(rank, port, q, wires, rounds, step_size, gamma):
     os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     try:
@@ -40,38 +40,50 @@ def _worker(rank, port, q, wire):
         from fedmi.parallel.comm import Comm
         comm = Comm(backend="xgmi", device="cuda:0", rccl=False)
         X, y = _data(rank, comm.device)
-        c = WideClient(X, y, DIMS, comm=comm, n_total=sum(ROWS), micro_batch=512, dtype="bf16", allreduce_dtype=wire)
-        losses = []
-        for _ in range(ROUNDS):
-            c.run_round()
-            losses.append(c.loss())
-        c.sync()
-        torch.cuda.synchronize()
-        q.put((rank, c.params.cpu().numpy(), losses, None))
-        comm.Barrier()
+        res = {}
+        for wire in wires:
+            c = WideClient(X, y, DIMS, comm=comm, n_total=sum(ROWS), micro_batch=512, dtype="bf16",
+                           allreduce_dtype=wire, step_size=step_size, gamma=gamma)
+            snaps = []
+            for _ in range(rounds):
+                c.run_round()
+                c.loss()
+                c.sync()
+                torch.cuda.synchronize()
+                snaps.append(c.params.cpu().numpy().copy())
+            res[wire] = snaps
+            comm.Barrier()
+        q.put((rank, res, None))
         comm.close()
     except Exception:  # noqa: BLE001
         import traceback
-        q.put((rank, None, None, traceback.format_exc()))
+        q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("wire,tol", [("fp32", 1e-6), ("bf16", 5e-2)])
-def test_wide_fedavg_buckets_match_simulation(wire, tol):
-    """fp32 buckets: the simulation to fp32 rounding; bf16 buckets (scaled weights rounded to
-    bf16 on the wire, fp32 master copy): close to it -- a rounding that flips the sign of a
-    small gradient moves that weight by a whole Adam step (lr 0.004) in the next round."""
+def _run_two(wires, rounds=ROUNDS, step_size=30, gamma=0.5):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q, wire)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, wires, rounds, step_size, gamma)) for r in range(2)]
     for p in procs:
         p.start()
-    out = sorted([q.get(timeout=110) for _ in range(2)], key=lambda t: t[0])
+    out = sorted([q.get(timeout=150) for _ in range(2)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=30)
-    for rank, _, _, err in out:
+    for rank, _, err in out:
         assert err is None, f"rank {rank}:\n{err}"
-    np.testing.assert_array_equal(out[0][1], out[1][1])
+    for w in wires:  # every rank holds the same global model after every round
+        for a, b in zip(out[0][1][w], out[1][1][w]):
+            np.testing.assert_array_equal(a, b)
+    return out[0][1]
+
+
+@pytest.mark.parametrize("wire,tol", [("fp32", 1e-6), ("bf16", 2e-3)])
+def test_wide_fedavg_buckets_match_simulation(wire, tol):
+    """fp32 buckets: the simulation to fp32 rounding; bf16 buckets (the scaled round delta
+    rounded to bf16 on the wire, added to the fp32 previous global model): close to it."""
+    res = _run_two((wire,))
+    out = [(0, [res[wire][-1]])]
 
     # single-process simulation of the same two clients
     import torch
@@ -90,8 +102,24 @@ def test_wide_fedavg_buckets_match_simulation(wire, tol):
             c.stream.synchronize()
             c.round += 1
     ref = cl[0].params.cpu().numpy()
-    err = np.max(np.abs(out[0][1] - ref)) / np.max(np.abs(ref))
+    err = np.max(np.abs(out[0][1][0] - ref)) / np.max(np.abs(ref))
     assert err < tol, err
+
+
+def test_wide_bf16_wire_keeps_fp32_master():
+    """with bf16 buckets the master weights must stay fp32.  StepLR decays the LR
+    20x per round (0.004 -> 2e-4 -> 1e-5 -> 5e-7 -> 2.5e-8): the late Adam steps are far below
+    half a bf16 ulp of the weights, so re-rounding the averaged weights to bf16 (round 2's
+    design) would erase them.  With the delta wire they survive: every round's global update
+    matches the fp32 wire's to a few bf16 ulps OF THE UPDATE."""
+    res = _run_two(("fp32", "bf16"), rounds=5, step_size=1, gamma=0.05)
+    f, b = res["fp32"], res["bf16"]
+    for r in range(1, 5):
+        uf, ub = f[r] - f[r - 1], b[r] - b[r - 1]
+        assert np.max(np.abs(uf)) > 0, r
+        rel = np.linalg.norm(ub - uf) / np.linalg.norm(uf)
+        assert rel < 0.05, (r, rel)
+    assert np.max(np.abs(b[-1] - f[-1])) / np.max(np.abs(f[-1])) < 2e-3
 
 
 def test_wide_local_evaluation_whole_shard():

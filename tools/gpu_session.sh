@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: GPU tests, 1-GPU bench, rocprofv3 kernel stats and PMC counter passes
 # of the flagship round.  Usage (from the repo root, on the GPU box):
-#   tools/gpu_session.sh <tag> [tests bench prof pmc]     (default: all four, in that order)
+#   tools/gpu_session.sh <tag> [tests bench n8 fp32 prof pmc]   (default: tests bench prof pmc, in that order)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -21,6 +21,18 @@ run_tests() {
 run_bench() {
     cd $R && timeout -k 10 400 python -u bench.py $BENCH_ARGS > $out/bench.json 2> $out/bench.err
     local rc=$?; cat $out/bench.json; return $rc
+}
+run_n8() {
+    # a whole node's world (8 ranks) on the box's one GPU: peer self-test at world 8, classic rounds,
+    # replica check (the driver's SCALE run uses 8 real GPUs)
+    cd $R && timeout -k 10 500 python -u bench.py --gpus 8 --share-gpu --steps 400 --warmup 50 --no-anchor \
+        --no-convergence > $out/bench_n8_share.json 2> $out/bench_n8_share.err
+    local rc=$?; cat $out/bench_n8_share.json; return $rc
+}
+run_fp32() {
+    cd $R && timeout -k 10 400 python -u bench.py --dtype fp32 --steps 2000 --warmup 200 --no-anchor \
+        > $out/bench_fp32.json 2> $out/bench_fp32.err
+    local rc=$?; cat $out/bench_fp32.json; return $rc
 }
 run_prof() {
     cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv \
