@@ -31,7 +31,7 @@ class WideClient:
     def __init__(self, X: torch.Tensor, y: torch.Tensor, dims: Sequence[int], comm=None, n_total: Optional[int] = None,
                  micro_batch: int = 131072, lr: float = 0.004, betas=(0.9, 0.999), eps: float = 1e-8,
                  step_size: int = 30, gamma: float = 0.5, seed: int = 0, dtype: str = "bf16",
-                 eval_rows: int = 0, allreduce_dtype: str = "fp32"):
+                 eval_rows: int = 0, allreduce_dtype: str = "fp32", warmup_rounds: int = 0):
         from ..ops import native
         self.m = native()
         self.dev = X.device
@@ -46,6 +46,8 @@ class WideClient:
         self.mb = min(micro_batch, self.n)
         self.lr, self.betas, self.eps = lr, betas, eps
         self.step_size, self.gamma = step_size, gamma
+        # linear LR warm-up over the first rounds (0: none, the reference's schedule), then StepLR
+        self.warmup_rounds = int(warmup_rounds)
         self.dtype = 1 if dtype == "bf16" else 0
         self.eval_rows = eval_rows
         if allreduce_dtype not in ("fp32", "bf16"):
@@ -378,6 +380,8 @@ class WideClient:
             # torch Adam + StepLR (scalars computed on host: the schedule is known)
             t = self.round + 1
             lr = self.lr * self.gamma ** (self.round // self.step_size)
+            if self.warmup_rounds > 0:
+                lr *= min(1.0, (self.round + 1) / self.warmup_rounds)
             self.m.adam_flat(self.params.data_ptr(), self.m_.data_ptr(), self.v_.data_ptr(), self.grads.data_ptr(),
                              self.params.numel(), lr, self.betas[0], self.betas[1], self.eps, t, s)
 

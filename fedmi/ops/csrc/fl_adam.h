@@ -17,6 +17,13 @@
 #ifndef ADAM_DEPTH
 #define ADAM_DEPTH 16
 #endif
+// 16-byte slab loads in flight per lane (fl_adam_body.inc): 2 x 16 waves x 8 rows = 256 fp16 slab
+// rows (the 8000-row shard's 250 workgroups) in ONE round of loads
+#ifndef ADAM_WDEPTH
+#define ADAM_WDEPTH 2
+#endif
+typedef _Float16 fl_half8 __attribute__((ext_vector_type(8)));
+typedef float fl_float4v __attribute__((ext_vector_type(4)));
 // bf16 mode: parameter -> packed LDS-layout image(s).  A weight is stored as its bf16 hi part
 // and, `wlo_delta` bytes further, its lo part bf16(p - hi) (split-bf16 forward, fl_common.h);
 // a bias stays fp32.

@@ -98,7 +98,7 @@ def test_round_engine_fedavg_through_rccl(dtype):
 def test_wide_aggregate_through_rccl(wire):
     """WideClient.aggregate: per-layer buckets all-reduced as n_i/N-scaled sums on the comm
     stream, fp32 or bf16 on the wire (one rank: the scale is 1, so the weights must come back
-    unchanged -- bf16: up to one bf16 rounding)."""
+    unchanged -- bf16: up to one bf16 rounding of the round's update)."""
     import torch
     from fedmi.data.synthetic import make_income_like
     from fedmi.fl.wide import WideClient
@@ -107,6 +107,7 @@ def test_wide_aggregate_through_rccl(wire):
     Xn, yn = make_income_like(1024, seed=5)
     X, y = torch.as_tensor(Xn, device=dev), torch.as_tensor(yn, device=dev)
     c = WideClient(X, y, [14, 256, 128, 2], comm=None, micro_batch=512, dtype="bf16")
+    g0 = c.params.clone()   # the global model this local step started from
     c.local_step()
     c.stream.synchronize()
     before = c.params.clone()
@@ -114,6 +115,7 @@ def test_wide_aggregate_through_rccl(wire):
     c.world, c.comm = 2, _OneRankDevComm(rc)
     if wire == "bf16":
         c.send_bf16 = torch.empty(c.params.numel(), dtype=torch.bfloat16, device=dev)
+        c.gprev = g0.clone()
     c.aggregate()
     c.sync()
     torch.cuda.synchronize()
@@ -121,7 +123,10 @@ def test_wide_aggregate_through_rccl(wire):
     if wire == "fp32":
         assert torch.equal(c.params, before)
     else:
-        assert torch.equal(c.params, before.to(torch.bfloat16).float())
+        # the round's delta crosses the wire as bf16 and is added back to the fp32 global model
+        expect = g0 + (before - g0).to(torch.bfloat16).float()
+        assert torch.equal(c.params, expect)
+        assert torch.equal(c.gprev, expect)
     rc.destroy()
 
 

@@ -1,66 +1,131 @@
-// Kernel-boundary cost probe (gfx950): per-kernel time inside a captured hipGraph for
-//   empty 1-block kernels, 250x512-thread kernels holding ~100 KB LDS, the same writing an
-//   11 MB slab (the fused train kernel's gradient partials), and a persistent kernel that
-//   replaces two boundaries with two grid barriers (agent-scope atomics).
-// Build: hipcc --offload-arch=gfx950 -O3 tools/probes/overhead_probe.hip -o /tmp/overhead_probe
+// Round-structure probe (gfx950): is ONE kernel with a grid barrier cheaper than the fused
+// round's train -> Adam kernel boundary?  Shapes of the [C] round (8000 rows, R = 32: 250
+// workgroups of 1024 threads holding ~100 KB of LDS, one per CU; a 5.7 MB fp16 gradient slab of
+// 250 rows x 11352 partials; 179 reduction blocks of 64 parameters).  Per round, in a captured
+// hipGraph of N rounds:
+//   chain      : k_train (slab rows, non-temporal stores) -> k_reduce (16-byte slab loads, the
+//                production Adam kernel's access pattern)
+//   fused-uc   : one kernel: the same slab rows written into UNCACHED memory (hipExtMallocWithFlags
+//                hipDeviceMallocUncached: stores go to memory, s_waitcnt vmcnt(0) = visible),
+//                arrival counted on an uncached counter, bounded spin, then the same reduction
+//                by the first 179 workgroups -- no cache maintenance at all
+//   fused-nt   : the same with the slab in ordinary memory, non-temporal stores + agent-scope
+//                release / acquire fences around the barrier (the cache-maintenance version)
+// Round 1's probe wrote the slab with CACHEABLE stores and then released at agent scope, i.e.
+// it timed an 11 MB L2 writeback, not a grid barrier (VERDICT r2 "weak" 2).
+// Build: hipcc --offload-arch=gfx950 -O3 tools/probes/overhead_probe.hip -o tools/probes/overhead_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); return 1; } } while (0)
 
-__global__ void k_empty() {}
+constexpr int B = 250, T = 1024, P = 11352, STRIDE = ((P + 1) + 3) & ~3;   // floats per slab row
+constexpr int RB = (P + 63) / 64;                                          // reduction blocks
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
-__global__ void k_lds(float* out) {
+// ~the train kernel's LDS footprint and a little LDS traffic, then one fp16 slab row
+__device__ __forceinline__ void train_part(_Float16* __restrict__ slab, bool nt) {
     extern __shared__ float lds[];
-    lds[threadIdx.x] = threadIdx.x;
+    for (int i = threadIdx.x; i < 25 * 1024; i += blockDim.x) lds[i] = (float)(i ^ blockIdx.x);
     __syncthreads();
-    if (lds[(threadIdx.x + 1) % blockDim.x] < 0.f) out[0] = 1.f;
+    _Float16* row = slab + (size_t)blockIdx.x * STRIDE * 2;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const _Float16 v = (_Float16)(lds[(i * 7) % (25 * 1024)] * 1e-3f);
+        if (nt) __builtin_nontemporal_store(v, &row[i]);
+        else row[i] = v;
+    }
 }
 
-__global__ void k_slab(float* slab, int per_block) {
-    extern __shared__ float lds[];
-    lds[threadIdx.x] = threadIdx.x;
+// 64 parameters per block, 16 waves: lane (q, r) = (lane % 8, lane / 8) sums 8 partials of rows
+// 8w + r + 128k with 16-byte loads, an xor tree folds r, wave 0 folds the 16 waves
+__device__ __forceinline__ void reduce_part(const _Float16* __restrict__ slab, float* __restrict__ out, int blk) {
+    __shared__ float part[16][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane & 7, r = lane >> 3;
+    const int p0 = blk * 64 + q * 8;
+    const _Float16* base = slab + (p0 < P ? p0 : 0);
+    float acc[8] = {};
+    half8 x[2];
+    for (int s0 = wave * 8 + r; s0 < B + r; s0 += 256) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int s = s0 + 128 * u;
+            const half8 v = __builtin_nontemporal_load(reinterpret_cast<const half8*>(base + (size_t)(s < B ? s : 0) * STRIDE * 2));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[u][i] = s < B ? v[i] : (_Float16)0;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] += (float)x[u][i];
+    }
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += __shfl_xor(acc[i], off, 64);
+    if (r == 0)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) part[wave][q * 8 + i] = acc[i];
     __syncthreads();
-    float* s = slab + (size_t)blockIdx.x * per_block;
-    for (int i = threadIdx.x; i < per_block; i += blockDim.x) s[i] = lds[i % blockDim.x];
+    if (wave == 0) {
+        float g = 0.f;
+        for (int w = 0; w < 16; ++w) g += part[w][lane];
+        const int p = blk * 64 + lane;
+        if (p < P) out[p] = g;
+    }
 }
 
-// grid barrier: counter incremented by every block, spin until it reaches target
-__device__ void grid_sync(unsigned* ctr, unsigned target) {
+__global__ void __launch_bounds__(1024) k_train(_Float16* slab) { train_part(slab, true); }
+__global__ void __launch_bounds__(1024) k_reduce(const _Float16* slab, float* out) { reduce_part(slab, out, blockIdx.x); }
+
+// grid barrier on an uncached counter: stores acknowledged -> arrive -> bounded spin
+__device__ __forceinline__ bool grid_arrive_wait(unsigned* ctr, unsigned target, bool fences) {
+    __shared__ int ok;
+    if (!fences) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // bounded spin: a grid that is not fully resident gives up instead of hanging
-        for (int it = 0; it < 2000000 && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it)
+        if (fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        int it = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target && ++it < 4000000)
             __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (fences) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        ok = it < 4000000;
     }
     __syncthreads();
+    return ok;
 }
 
-__global__ void k_persist(float* slab, int per_block, unsigned* ctr, unsigned base) {
-    extern __shared__ float lds[];
-    lds[threadIdx.x] = threadIdx.x;
-    __syncthreads();
-    float* s = slab + (size_t)blockIdx.x * per_block;
-    for (int i = threadIdx.x; i < per_block; i += blockDim.x) s[i] = lds[i % blockDim.x];
-    grid_sync(ctr, base + gridDim.x);
-    grid_sync(ctr, base + 2 * gridDim.x);
+__global__ void __launch_bounds__(1024) k_fused(_Float16* slab, float* out, unsigned* ctr, unsigned base, int fences,
+                                                unsigned* err) {
+    train_part(slab, fences != 0);
+    if (!grid_arrive_wait(ctr, base + gridDim.x, fences != 0)) {
+        if (threadIdx.x == 0) atomicAdd(err, 1u);
+        return;  // every wave of the grid reaches this exit (bounded spin)
+    }
+    if (blockIdx.x < RB) reduce_part(slab, out, blockIdx.x);
 }
 
 int main() {
-    const int B = 250, T = 512, per_block = 11352, N = 200;
+    const int N = 200;
     const size_t lds = 100 * 1024;
-    float *slab, *out;
-    unsigned* ctr;
-    CK(hipMalloc(&slab, (size_t)B * 2 * per_block * 4));
-    CK(hipMalloc(&out, 4));
-    CK(hipMalloc(&ctr, 4));
-    CK(hipFuncSetAttribute((const void*)k_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    CK(hipFuncSetAttribute((const void*)k_slab, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    CK(hipFuncSetAttribute((const void*)k_persist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    _Float16 *slab, *slab_uc;
+    float* out;
+    unsigned *ctr, *err;
+    const size_t slab_bytes = (size_t)B * STRIDE * 4;
+    CK(hipMalloc(&slab, slab_bytes));
+    CK(hipExtMallocWithFlags((void**)&slab_uc, slab_bytes, hipDeviceMallocUncached));
+    CK(hipExtMallocWithFlags((void**)&ctr, 256, hipDeviceMallocUncached));
+    CK(hipMalloc(&out, P * 4));
+    CK(hipMalloc(&err, 4));
+    CK(hipMemset(slab, 0, slab_bytes));
+    CK(hipMemset(slab_uc, 0, slab_bytes));
+    CK(hipMemset(err, 0, 4));
+    CK(hipFuncSetAttribute((const void*)k_train, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFuncSetAttribute((const void*)k_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipDeviceProp_t pr;
+    CK(hipGetDeviceProperties(&pr, 0));
+    if (pr.multiProcessorCount < B) { printf("needs >= %d CUs for a resident grid\n", B); return 1; }
     hipStream_t s;
     CK(hipStreamCreate(&s));
     hipEvent_t e0, e1;
@@ -72,36 +137,45 @@ int main() {
         for (int i = 0; i < N; ++i) body(i);
         CK(hipStreamEndCapture(s, &g));
         CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
-        CK(hipMemsetAsync(ctr, 0, 4, s));
-        CK(hipGraphLaunch(x, s));
-        CK(hipStreamSynchronize(s));
         float best = 1e30f;
-        for (int rep = 0; rep < 5; ++rep) {
+        for (int rep = 0; rep < 6; ++rep) {
             CK(hipMemsetAsync(ctr, 0, 4, s));
             CK(hipEventRecord(e0, s));
             CK(hipGraphLaunch(x, s));
             CK(hipEventRecord(e1, s));
             CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-            best = ms < best ? ms : best;
+            if (rep > 0) best = ms < best ? ms : best;
         }
-        printf("%-44s %8.2f us per launch\n", name, best * 1e3f / N);
+        unsigned e = 0;
+        CK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
+        printf("%-58s %8.2f us per round%s\n", name, best * 1e3f / N, e ? "  (BARRIER TIMEOUTS)" : "");
         CK(hipGraphExecDestroy(x)); CK(hipGraphDestroy(g));
         return 0;
     };
-    time_graph("empty <<<1,64>>>", [&](int) { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s); });
-    time_graph("empty <<<250,512>>>", [&](int) { hipLaunchKernelGGL(k_empty, dim3(B), dim3(T), 0, s); });
-    time_graph("lds 100KB <<<250,512>>>", [&](int) { hipLaunchKernelGGL(k_lds, dim3(B), dim3(T), lds, s, out); });
-    time_graph("lds 100KB <<<500,512>>>", [&](int) { hipLaunchKernelGGL(k_lds, dim3(2 * B), dim3(T), lds / 2, s, out); });
-    time_graph("slab 11MB <<<250,512>>>", [&](int) { hipLaunchKernelGGL(k_slab, dim3(B), dim3(T), lds, s, slab, per_block); });
-    time_graph("slab 1.1MB <<<250,512>>>", [&](int) { hipLaunchKernelGGL(k_slab, dim3(B), dim3(T), lds, s, slab, per_block / 10); });
-    time_graph("3 x slab-kernel chain (per chain)", [&](int) {
-        hipLaunchKernelGGL(k_slab, dim3(B), dim3(T), lds, s, slab, per_block);
-        hipLaunchKernelGGL(k_lds, dim3(B), dim3(T), lds, s, out);
-        hipLaunchKernelGGL(k_lds, dim3(B), dim3(T), lds, s, out);
-    });
-    time_graph("persistent slab + 2 grid barriers", [&](int i) {
-        hipLaunchKernelGGL(k_persist, dim3(B), dim3(T), lds, s, slab, per_block, ctr, (unsigned)(2 * B * i));
-    });
+    // reference results of one round for the correctness check of the fused variants
+    hipLaunchKernelGGL(k_train, dim3(B), dim3(T), lds, s, slab);
+    hipLaunchKernelGGL(k_reduce, dim3(RB), dim3(T), 0, s, slab, out);
+    std::vector<float> ref(P), got(P);
+    CK(hipMemcpyAsync(ref.data(), out, P * 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    if (time_graph("train only (250 x 1024, 100 KB LDS, nt fp16 slab row)", [&](int) {
+            hipLaunchKernelGGL(k_train, dim3(B), dim3(T), lds, s, slab); })) return 1;
+    if (time_graph("reduce only (179 x 1024, 16-byte nt slab loads)", [&](int) {
+            hipLaunchKernelGGL(k_reduce, dim3(RB), dim3(T), 0, s, slab, out); })) return 1;
+    if (time_graph("chain: train -> reduce", [&](int) {
+            hipLaunchKernelGGL(k_train, dim3(B), dim3(T), lds, s, slab);
+            hipLaunchKernelGGL(k_reduce, dim3(RB), dim3(T), 0, s, slab, out); })) return 1;
+    for (int fences = 0; fences < 2; ++fences) {
+        CK(hipMemsetAsync(out, 0, P * 4, s));
+        if (time_graph(fences ? "fused-nt: one kernel, nt slab, agent release/acquire"
+                              : "fused-uc: one kernel, uncached slab + counter, no fences", [&](int i) {
+                hipLaunchKernelGGL(k_fused, dim3(B), dim3(T), lds, s, fences ? slab : slab_uc, out, ctr,
+                                   (unsigned)(B * i), fences, err); })) return 1;
+        CK(hipMemcpy(got.data(), out, P * 4, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (int i = 0; i < P; ++i) bad += got[i] != ref[i];
+        printf("   result vs chain: %zu of %d partial sums differ\n", bad, P);
+    }
     return 0;
 }
