@@ -170,19 +170,30 @@ def sklearn_to_torch_layout(weights):
 def save_sklearn_run(path: str, rank: int, round_done: int, global_weights, local_weights, meta: dict,
                      comm=None) -> None:
     """[S] round checkpoint (collective): rank 0 writes ``global.safetensors`` + ``meta.json``
-    (rounds done, history, run settings), every rank its local model ``client{r}.safetensors``."""
+    (rounds done, history, run settings), every rank its local model ``client{r}.safetensors``.
+    Every file is written to a temporary name and renamed into place, and ``meta.json`` -- the
+    file that says which round the directory holds -- is written LAST, after a barrier: a crash
+    at any point leaves either the previous round's complete set or the new one."""
     os.makedirs(path, exist_ok=True)
-    save_sklearn_weights(os.path.join(path, f"client{rank}.safetensors"), local_weights)
+
+    def _atomic_weights(name, w):
+        tmp = os.path.join(path, f".{name}.tmp{os.getpid()}")
+        save_sklearn_weights(tmp, w)
+        os.replace(tmp, os.path.join(path, name))
+
+    _atomic_weights(f"client{rank}.safetensors", local_weights)
+    if rank == 0 and global_weights is not None:
+        _atomic_weights("global.safetensors", global_weights)
+    if comm is not None and getattr(comm, "size", 1) > 1:
+        comm.Barrier()   # every client file of this round is in place
     if rank == 0:
-        if global_weights is not None:
-            save_sklearn_weights(os.path.join(path, "global.safetensors"), global_weights)
         m = dict(meta, format=SK_FORMAT, rounds=int(round_done))
         tmp = os.path.join(path, "meta.json.tmp")
         with open(tmp, "w") as f:
             json.dump(m, f)
         os.replace(tmp, os.path.join(path, "meta.json"))
     if comm is not None and getattr(comm, "size", 1) > 1:
-        comm.Barrier()
+        comm.Barrier()   # nobody reads / rewrites the directory before meta.json points at it
 
 
 def load_sklearn_run(path: str, rank: int) -> dict:

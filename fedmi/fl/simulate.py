@@ -93,7 +93,10 @@ class ClientGroup:
             e.engine.run_local(r, s)      # train + Adam + eval into its own FedAvg buffer
         with torch.cuda.stream(self.stream):
             bufs = [e.params[(r + 1) & 1] for e in self.clients]
-            tot = bufs[0].clone()
+            tot = getattr(self, "_tot", None)
+            if tot is None or tot.shape != bufs[0].shape:
+                tot = self._tot = torch.empty_like(bufs[0])   # one accumulation buffer for all rounds
+            tot.copy_(bufs[0])
             for b in bufs[1:]:
                 tot += b                  # rank order
             for b in bufs:

@@ -104,32 +104,52 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
     return out
 
 
+def _trial_file(r: TrialResult) -> str:
+    return "trial_h" + "-".join(str(h) for h in r.hidden) + f"_lr{r.lr:g}.safetensors"
+
+
 def save_sweep(path: str, results: Sequence[TrialResult], best: Optional[TrialResult], meta: dict) -> None:
     """[H] checkpoint: every trial's metrics (JSON) + the best trial's averaged weights in the
-    reference's coefs_ + intercepts_ layout (H:119, H:130-132) as ``best.safetensors``."""
+    reference's coefs_ + intercepts_ layout (H:119, H:130-132) as ``best.safetensors``.
+    Incremental: called after every finished trial (hyperparameters_tuning.py), it writes only
+    the weights files it has not written yet (named by the trial's grid key) and then replaces
+    ``sweep.json`` atomically, so a crash part-way leaves a resumable sweep of the trials done."""
     import json
     import os
     from ..ckpt.checkpoint import save_sklearn_weights
     os.makedirs(path, exist_ok=True)
-    if best is not None:
-        save_sklearn_weights(os.path.join(path, "best.safetensors"), best.weights)
-    rows = [{"hidden": list(r.hidden), "lr": r.lr, "local": r.local, "global": r.global_, "n_iter": r.n_iter}
-            for r in results]
-    with open(os.path.join(path, "sweep.json"), "w") as f:
-        json.dump(dict(meta, trials=rows, best={"hidden": list(best.hidden), "lr": best.lr} if best else None), f)
     # every trial's averaged weights, so a resumed sweep can still return any of them as the best
-    for i, r in enumerate(results):
-        save_sklearn_weights(os.path.join(path, f"trial{i}.safetensors"), r.weights)
+    for r in results:
+        fp = os.path.join(path, _trial_file(r))
+        if not os.path.isfile(fp):
+            tmp = fp + ".tmp"
+            save_sklearn_weights(tmp, r.weights)
+            os.replace(tmp, fp)
+    if best is not None:
+        save_sklearn_weights(os.path.join(path, "best.safetensors.tmp"), best.weights)
+        os.replace(os.path.join(path, "best.safetensors.tmp"), os.path.join(path, "best.safetensors"))
+    rows = [{"hidden": list(r.hidden), "lr": r.lr, "local": r.local, "global": r.global_, "n_iter": r.n_iter,
+             "file": _trial_file(r)} for r in results]
+    tmp = os.path.join(path, "sweep.json.tmp")
+    with open(tmp, "w") as f:
+        json.dump(dict(meta, trials=rows, best={"hidden": list(best.hidden), "lr": best.lr} if best else None), f)
+    os.replace(tmp, os.path.join(path, "sweep.json"))
 
 
-def load_sweep(path: str) -> List[TrialResult]:
+def load_sweep(path: str, expect: Optional[dict] = None) -> List[TrialResult]:
+    """Trials of a saved sweep.  ``expect``: run settings (world, max_iter, data digest, ...)
+    that must equal the saved ones -- trials of a different run must not mix into this one's
+    best-trial selection."""
     import json
     import os
     from ..ckpt.checkpoint import load_sklearn_weights
     with open(os.path.join(path, "sweep.json")) as f:
         m = json.load(f)
+    for k, v in (expect or {}).items():
+        if m.get(k) != v:
+            raise ValueError(f"{path}: saved with {k}={m.get(k)!r}, this run has {k}={v!r}; not resuming")
     out = []
     for i, r in enumerate(m["trials"]):
-        w = load_sklearn_weights(os.path.join(path, f"trial{i}.safetensors"))
+        w = load_sklearn_weights(os.path.join(path, r.get("file", f"trial{i}.safetensors")))
         out.append(TrialResult(tuple(r["hidden"]), float(r["lr"]), r["local"], r["global"], int(r["n_iter"]), w))
     return out

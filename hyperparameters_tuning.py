@@ -125,7 +125,19 @@ def main(argv=None):
     if backend == "auto":
         backend = "hip" if comm.device.type == "cuda" else "numpy"
 
+    from fedmi.hpo.sweep import load_sweep, save_sweep
+    from fedmi.parallel.consistency import digest
+    # the run settings a checkpoint must match to be resumed (trials of another run, data or
+    # client count must not mix into this run's best-trial selection)
+    meta = {"world": comm.Get_size(), "max_iter": a.max_iter, "dtype": a.dtype,
+            "data": digest([ds.X_train, ds.y_train])}
+    done = load_sweep(a.resume, expect=meta) if a.resume else []
+    partial = list(done)
+
     def report(res):
+        partial.append(res)
+        if a.save and rank == 0:
+            save_sweep(a.save, partial, None, meta)  # incremental: a crash leaves a resumable sweep
         if a.quiet:
             return
         print("\n\tLOCAL MEASURED RESULTS\n")
@@ -136,8 +148,6 @@ def main(argv=None):
             print(f"\t[Rank {rank}] Global Metrics (Hidden Layers: {res.hidden}, LR: {res.lr}): {res.global_}\n")
             print("-" * 50, flush=True)
 
-    from fedmi.hpo.sweep import load_sweep, save_sweep
-    done = load_sweep(a.resume) if a.resume else []
     if done and rank == 0:
         print(f"Resumed {len(done)} trials from {a.resume}", flush=True)
     t0 = time.time()
@@ -149,7 +159,7 @@ def main(argv=None):
                                   packed=not a.no_pack, on_trial=report, done=done, dtype=a.dtype)
     wall = time.time() - t0
     if a.save and rank == 0:
-        save_sweep(a.save, results, best, {"world": comm.Get_size(), "max_iter": a.max_iter})
+        save_sweep(a.save, results, best, meta)
     comm.Barrier()
     if comm.Get_size() > 1:
         from fedmi.parallel.consistency import check_replicas

@@ -120,6 +120,30 @@ def test_hpo_sweep_save_resume_reuses_trials(tmp_path):
     for u, v in zip(res2[0].weights, res[0].weights):
         np.testing.assert_array_equal(u, v)
     assert os.path.isfile(tmp_path / "best.safetensors")
+    # a checkpoint of another run (different client count) is refused, not mixed in
+    with pytest.raises(ValueError, match="world"):
+        load_sweep(str(tmp_path), expect={"world": 2})
+    assert len(load_sweep(str(tmp_path), expect={"world": 1})) == 2
+
+
+def test_hpo_sweep_incremental_checkpoint(tmp_path):
+    """[H] --save writes after every trial: a sweep interrupted after k trials resumes them."""
+    from fedmi.data.tabular import load_tabular
+    from fedmi.hpo.sweep import load_sweep, run_sweep, save_sweep
+    ds = load_tabular(with_mean=False)
+    X, y = ds.X_train[:400], ds.y_train[:400]
+    partial = []
+
+    def on_trial(r):
+        partial.append(r)
+        save_sweep(str(tmp_path), partial, None, {"world": 1})
+        if len(partial) == 3:
+            raise KeyboardInterrupt  # "crash" after the third trial
+
+    with pytest.raises(KeyboardInterrupt):
+        run_sweep(X, y, None, [(5,), (6,)], [0.01, 0.02], max_iter=5, backend="numpy", on_trial=on_trial)
+    done = load_sweep(str(tmp_path), expect={"world": 1})
+    assert [(r.hidden, r.lr) for r in done] == [((5,), 0.01), ((5,), 0.02), ((6,), 0.01)]
 
 
 @pytest.mark.gpu
