@@ -79,17 +79,23 @@ def parse_args(argv=None):
                     help="rows per micro-batch for --wide (about 112 KiB of activation buffers per row at 4096 wide: 14 GiB of HBM)")
     ap.add_argument("--eval-every", type=int, default=0, help="--wide: local accuracy every N rounds")
     ap.add_argument("--wide-allreduce", default="fp32", choices=["fp32", "bf16"],
-                    help="--wide: FedAvg bucket dtype on the wire (fp32 master weights either way)")
+                    help="--wide: FedAvg bucket dtype on the wire (bf16: the round's delta, fp32 master weights "
+                         "either way)")
+    ap.add_argument("--wide-lr", type=float, default=None,
+                    help="--wide: Adam learning rate (default fedmi.fl.wide.WIDE_LR = 1e-4: the reference's 0.004 "
+                         "makes the 4096-wide model diverge, in torch as on the kernels, profiles/wide_learn_r3.log)")
+    ap.add_argument("--wide-warmup", type=int, default=0, help="--wide: linear LR warm-up rounds")
     return ap.parse_args(argv)
 
 
 def main_wide(a, comm):
     """--wide: federated wide-MLP rounds (fedmi.fl.wide.run_wide_fedavg)."""
-    from fedmi.fl.wide import run_wide_fedavg
+    from fedmi.fl.wide import WIDE_LR, run_wide_fedavg
     dims = [14, *a.hidden, 2]
     res = run_wide_fedavg(comm, dims, a.synthetic_rows, a.rounds, micro_batch=a.micro_batch, dtype=a.dtype,
-                          lr=a.lr, eval_every=a.eval_every, seed=a.seed + 7, verbose=not a.quiet,
-                          allreduce_dtype=a.wide_allreduce)
+                          lr=a.wide_lr if a.wide_lr is not None else WIDE_LR, eval_every=a.eval_every,
+                          seed=a.seed + 7, verbose=not a.quiet, allreduce_dtype=a.wide_allreduce,
+                          warmup_rounds=a.wide_warmup)
     if comm.rank == 0 and comm.rccl_env:
         print(f"RCCL pinned: {comm.rccl_env}", flush=True)
     if comm.rank == 0:

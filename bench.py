@@ -173,7 +173,10 @@ def main(argv=None):
                     help="rows per client (BASELINE config 3 names 1e8-row shards: 12500000 per client at k = 8)")
     ap.add_argument("--micro-batch", type=int, default=131072, help="--config wide: rows per micro-batch")
     ap.add_argument("--wide-allreduce", default="fp32", choices=["fp32", "bf16"],
-                    help="--config wide: FedAvg bucket dtype on the wire (fp32 master weights either way)")
+                    help="--config wide: FedAvg bucket dtype on the wire (bf16: the round's delta; fp32 master "
+                         "weights either way)")
+    ap.add_argument("--wide-lr", type=float, default=None,
+                    help="--config wide: Adam lr (default fedmi.fl.wide.WIDE_LR = 1e-4; 0.004 diverges at width 4096)")
     a = ap.parse_args(argv)
     from fedmi.parallel.comm import launch_env
     if a.gpus > 1 and launch_env()[1] == 1:  # no multi-process launcher around us: start the ranks
@@ -297,7 +300,7 @@ def main(argv=None):
 def main_wide(a) -> None:
     """BASELINE config 3 under the same contract: a step is one federated round of the wide
     client (full-batch local Adam step over the shard + per-layer FedAvg buckets)."""
-    from fedmi.fl.wide import WideClient
+    from fedmi.fl.wide import WIDE_LR, WideClient
     from fedmi.parallel.comm import get_world
     import torch.distributed as dist
 
@@ -309,8 +312,9 @@ def main_wide(a) -> None:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
     dims = [14, 4096, 4096, 4096, 2]
     X, y = synth_shard(a.wide_rows, comm.rank, comm.device)
+    lr = a.wide_lr if a.wide_lr is not None else WIDE_LR
     c = WideClient(X, y, dims, comm=comm if N > 1 else None, n_total=a.wide_rows * N, dtype="bf16", seed=0,
-                   micro_batch=a.micro_batch, allreduce_dtype=a.wide_allreduce)
+                   micro_batch=a.micro_batch, allreduce_dtype=a.wide_allreduce, lr=lr)
 
     def barrier():
         if N > 1:
@@ -318,8 +322,11 @@ def main_wide(a) -> None:
 
     # every round as the reference runs it: local step, local evaluation of the post-step model
     # on the whole shard (device-side confusion counts), FedAvg
-    for _ in range(a.warmup):
+    first_loss = None
+    for i in range(a.warmup):
         c.run_round(evaluate=True)
+        if i == 0:
+            first_loss = c.loss()   # (untimed: warm-up) the loss of round 1's local step
     c.sync()
     torch.cuda.synchronize(comm.device)
     barrier()
@@ -336,6 +343,7 @@ def main_wide(a) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     value = a.wide_rows * N * a.steps / dt
+    last_loss = c.loss()
     from fedmi.parallel.consistency import check_replicas
     replicas_ok = check_replicas(comm, [c.params])
     if comm.rank == 0:
@@ -351,6 +359,8 @@ def main_wide(a) -> None:
                                       f"{a.wide_allreduce} on the wire)", "rccl_env": comm.rccl_env},
             "tflops_per_client": c.flops_per_round / (dt / a.steps) / 1e12,
             "local_train_acc_synthetic": c.metrics()["accuracy"],
+            "lr": lr, "rounds_run": c.round,
+            "loss_first_round": first_loss, "loss_last_round": last_loss,
             "replicas_consistent": replicas_ok,
             "micro_batch": c.mb,
         }), flush=True)
