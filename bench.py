@@ -169,6 +169,9 @@ def main(argv=None):
                          "per-layer FedAvg buckets over RCCL | sweep: BASELINE config 5, --trials FedAvg trials "
                          "({hidden} x {lr} x {local steps} grid) packed per GPU, a step = one round of every trial")
     ap.add_argument("--trials", type=int, default=12, help="--config sweep: trials per GPU (first K of the grid)")
+    ap.add_argument("--trial-rows-per-block", type=int, default=-1,
+                    help="--config sweep: rows per workgroup of the trial batches (-1: the largest that fits LDS, "
+                         "64 first; 0: the single-engine choice, 32)")
     ap.add_argument("--wide-rows", type=int, default=131072,
                     help="rows per client (BASELINE config 3 names 1e8-row shards: 12500000 per client at k = 8)")
     ap.add_argument("--micro-batch", type=int, default=131072, help="--config wide: rows per micro-batch")
@@ -388,6 +391,7 @@ def main_sweep(a) -> int:
     X, y = synth_shard(a.rows_per_client, comm.rank, comm.device)
     g_rounds = 16
     base = EngineConfig(max_rounds=a.warmup + a.steps + 2 * g_rounds + 4, early_stop=False, dtype=a.dtype,
+                        rows_per_block=a.trial_rows_per_block,
                         graph_rounds=g_rounds)
     grp = FedTrialGroup(X, y, 2, trials, comm if N > 1 else None, base, n_total=a.rows_per_client * N,
                         group_graph_rounds=g_rounds)
@@ -423,7 +427,8 @@ def main_sweep(a) -> int:
             "config": {"model": "MLP 14-{hidden}-2 grid", "global_batch": a.rows_per_client * N, "seq_len": 1,
                        "parallelism": f"fedavg{N} x {len(trials)} trials/GPU ({len(grp.batches)} trial batches, "
                                       f"one all-reduce per round)", "rccl_env": comm.rccl_env,
-                       "trials": [[list(t.hidden), t.lr, t.local_steps] for t in trials]},
+                       "trials": [[list(t.hidden), t.lr, t.local_steps] for t in trials],
+                       "rows_per_block": {"x".join(map(str, t.hidden)): e.R for t, e in zip(trials, grp.engines)}},
             "us_per_trial_round": dt / (a.steps * len(trials)) * 1e6,
             "replicas_consistent": replicas_ok,
             "best_trial": {"hidden": list(best.hidden), "lr": best.lr, "local_steps": best.local_steps,

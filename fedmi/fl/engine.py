@@ -50,7 +50,8 @@ class EngineConfig:
     rtol: float = 1e-5
     max_rounds: int = 300
     metric_mode: str = "mean"       # 'mean' (C:169) | 'pooled' (S:130)
-    rows_per_block: int = 0         # R rows per workgroup of the fused kernels (16 | 32 | 64 (bf16); 0 = auto)
+    rows_per_block: int = 0         # R rows per workgroup of the fused kernels (16 | 32 | 64 (bf16); 0 = auto:
+                                    # 32 if it fits LDS, else 16; -1 = the largest that fits, 64 first (bf16))
     graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
     seed: int = 0
     # partial participation (client sampling): each round max(1, round(participation * world))
@@ -480,8 +481,11 @@ class HipRoundEngine(RoundEngineBase):
         f32 = dict(dtype=torch.float32, device=dev)
         self.X = (X if isinstance(X, torch.Tensor) else torch.as_tensor(np.ascontiguousarray(X, np.float32))).to(**f32).contiguous()
         self.y = (y if isinstance(y, torch.Tensor) else torch.as_tensor(np.asarray(y))).to(dtype=torch.int32, device=dev).contiguous()
-        # rows per workgroup: 0 = auto (32 when the model's LDS image fits, else 16)
-        R_try = [32, 16] if int(cfg.rows_per_block) == 0 else [int(cfg.rows_per_block)]
+        # rows per workgroup: 0 = auto (32 when the model's LDS image fits, else 16); -1 = the
+        # largest that fits, 64 first (bf16: half the workgroups and gradient-slab rows -- what
+        # packed trial batches want, whose throughput is workgroup-slots x workgroup latency)
+        rpb = int(cfg.rows_per_block)
+        R_try = [32, 16] if rpb == 0 else ([64, 32, 16] if cfg.dtype == "bf16" else [32, 16]) if rpb == -1 else [rpb]
         R = R_try[0]
         slab_stride = ((self.P + 1) + 3) & ~3
         # device parameter buffers use the padded image layout (fl_common.h)

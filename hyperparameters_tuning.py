@@ -193,7 +193,9 @@ def federated_main(a):
     trials = grid(hidden, tuple(a.lrs) if a.lrs else DEFAULT_LRS,
                   tuple(a.local_steps) if a.local_steps else DEFAULT_LOCAL_STEPS)
     rounds = a.rounds if a.rounds > 1 else 50
-    base = EngineConfig(max_rounds=rounds, dtype=a.dtype, graph_rounds=0)
+    # rows_per_block -1: trial batches take 64 rows per workgroup where LDS allows (bf16): half the
+    # workgroups, and a packed group round is bound by workgroup slots x workgroup latency
+    base = EngineConfig(max_rounds=rounds, dtype=a.dtype, graph_rounds=0, rows_per_block=-1)
     t0 = time.time()
     best, done = run_fed_sweep(X_local, y_local, 2, comm, trials, rounds=rounds, trials_per_gpu=a.trials_per_gpu,
                                base=base, backend="torch" if a.device == "cpu" else "auto")
