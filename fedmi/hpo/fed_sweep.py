@@ -181,11 +181,26 @@ class FedTrialGroup:
                 e.stream.wait_stream(self.stream)
                 e.sync_history()
 
+    def _issue_rounds_unjoined(self, r0: int, n: int) -> None:
+        """One client (no shared all-reduce): rounds of different trial batches do not depend on
+        each other, so each batch runs its ``n`` rounds back to back on its own stream and the
+        streams join once at the end -- no per-round join that holds every batch to the slowest
+        one.  Every batch issues exactly the launches of ``n`` group rounds, in the same order."""
+        for tb, _, st in self.batches:
+            st.wait_stream(self.stream)
+            for r in range(r0, r0 + n):
+                tb.run(r, 1, st.cuda_stream, close=False)   # fused evaluation rounds
+        for _, _, st in self.batches:
+            self.stream.wait_stream(st)
+
     def _capture(self) -> None:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
-            for r in range(self.graph_rounds):   # parities 0, 1, ...: replayed from even rounds
-                self._issue_group_round(r)
+            if self.world == 1 and self.batches:
+                self._issue_rounds_unjoined(0, self.graph_rounds)
+            else:
+                for r in range(self.graph_rounds):   # parities 0, 1, ...: replayed from even rounds
+                    self._issue_group_round(r)
         self.graph = g
         self._graph_flags = [e.engine.flags() for e in self.engines]
 

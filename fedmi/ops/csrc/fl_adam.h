@@ -14,6 +14,10 @@
 #ifndef ADAM_WAVES
 #define ADAM_WAVES 16
 #endif
+// the canonical wave count of the reduction order (fl_adam_body.inc): blocks of ADAM_WAVES < 16
+// waves emulate 16 / ADAM_WAVES canonical waves each and give bit-identical sums
+#define ADAM_CANON 16
+static_assert(ADAM_CANON % ADAM_WAVES == 0, "ADAM_WAVES must divide 16");
 #ifndef ADAM_DEPTH
 #define ADAM_DEPTH 16
 #endif
@@ -52,7 +56,7 @@ __device__ __forceinline__ float adam_update(const FLConfig& c, const FLBuffers&
     if (scale != 0.f) {
         float g = 0.f;
 #pragma unroll
-        for (int w = 0; w < ADAM_WAVES; ++w) g += part[w][lane];
+        for (int w = 0; w < ADAM_CANON; ++w) g += part[w][lane];
         if (c.slab_f16) g *= c.inv_n;  // fp16 slab: partial sums of the unscaled gradient
         if (c.weight_decay != 0.f) g += c.weight_decay * p;
         if (c.prox_mu != 0.f) g += c.prox_mu * (p - anc);

@@ -330,25 +330,7 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
 #undef ADAM_PA_LL
 }
 
-// Trial batch (no peer exchange: the trials' FedAvg is one shared collective outside).
-__global__ void __launch_bounds__(ADAM_WAVES * 64)
-fl_adam_batch_kernel(MLPDesc d, const FLTrialDesc* __restrict__ T, FLSel pin_sel, FLSel anchor_sel, FLSel comm_sel,
-                     FLSel st_sel, int local_step, MLPDescB e, int pack, FLSel st_out_sel, int fold, int tail_a,
-                     int fold_mask) {
-    const FLTrialDesc& t = T[blockIdx.y];
-    const FLConfig c = t.c;
-    const FLBuffers b = t.b;
-    const float* __restrict__ pin = reinterpret_cast<const float*>(fl_sel(t, pin_sel));
-    const float* __restrict__ anchor = reinterpret_cast<const float*>(fl_sel(t, anchor_sel));
-    float* __restrict__ comm = reinterpret_cast<float*>(fl_sel(t, comm_sel));
-    const FLState* __restrict__ st = reinterpret_cast<const FLState*>(fl_sel(t, st_sel));
-    FLState* __restrict__ st_out = reinterpret_cast<FLState*>(fl_sel(t, st_out_sel));
-    const PeerArgs pa = {};
-    const int xchg = 0, afold = 0;
-#define ADAM_PA_LL false
-#include "fl_adam_body.inc"
-#undef ADAM_PA_LL
-}
+// (the trial-batch Adam kernel lives in fl_adam_batch.hip: 4-wave blocks, same canonical sums)
 
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,
 // argmax, confusion counts into this rank's tail (exact: integer-valued fp32 < 2^24).
@@ -625,18 +607,6 @@ hipError_t fl_launch_train_batch(const MLPDesc& d, int R, int n_slabs, const FLT
             break;
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
-}
-
-hipError_t fl_launch_adam_batch(const MLPDesc& d, const MLPDescB* e, const FLTrialDesc* T, int K, FLSel pin,
-                                FLSel anchor, FLSel comm, FLSel st, int local_step, FLSel st_out, int fold, int tail_a,
-                                int fold_mask, hipStream_t s) {
-    if (K < 1 || (fold && st_out.base < 0)) return hipErrorInvalidValue;
-    const int blocks = (d.P + 63) / 64 + 1;
-    MLPDescB ee = {};
-    if (e != nullptr) ee = *e;
-    hipLaunchKernelGGL(fl_adam_batch_kernel, dim3(blocks, K), dim3(ADAM_WAVES * 64), 0, s, d, T, pin, anchor, comm,
-                       st, local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask);
     return hipGetLastError();
 }
 
