@@ -525,6 +525,10 @@ class HipRoundEngine(RoundEngineBase):
         self.h_global = torch.zeros(mr * 4, dtype=torch.float64, device=dev)
         self.h_rank = torch.zeros(mr * self.world * 4, dtype=torch.float64, device=dev)
         self.h_loss = torch.zeros(mr, dtype=torch.float32, device=dev)
+        # fp16 gradient slab guard: the Adam kernel sets it when a partial it reads is saturated at
+        # +-65504 (slab_store_h's clamp) or not finite; read_history() reports it
+        self.sat = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.slab_saturated = False
         ecfg = {
             "R": R, "n_rows": self.n_local, "world": self.world, "rank": self.rank, "agg_scale": self.agg_scale,
             "local_steps": int(cfg.local_steps), "lr": float(cfg.lr), "gamma": float(cfg.gamma),
@@ -545,6 +549,7 @@ class HipRoundEngine(RoundEngineBase):
             "local": self.local.data_ptr(), "m": self.mom.data_ptr(), "v": self.vel.data_ptr(),
             "hist_global": self.h_global.data_ptr(), "hist_rank": self.h_rank.data_ptr(),
             "hist_loss": self.h_loss.data_ptr(), "sched": self.sched.data_ptr(), "rtab": self.rtab.data_ptr(),
+            "sat": self.sat.data_ptr(),
             "params0": self.params[0].data_ptr(),
             "params1": self.params[1].data_ptr(), "state0": self.state[0].data_ptr(),
             "state1": self.state[1].data_ptr(),
@@ -848,6 +853,14 @@ class HipRoundEngine(RoundEngineBase):
             self.hist.stop_round = int(st["stop_round"])
             self.hist.stop_trigger = int(st["stop_round"]) - 1
             self._stopped_seen = True
+        if self.slab_f16 and not self.slab_saturated and int(self.sat.item()):
+            self.slab_saturated = True
+            msg = ("fp16 gradient slab saturated (a per-workgroup partial reached +-65504 or is not finite): the "
+                   "gradients of those rounds are clipped; rerun with EngineConfig(grad_slab='fp32')")
+            if self.cfg.debug:
+                raise FloatingPointError(msg)
+            import warnings
+            warnings.warn(msg, RuntimeWarning, stacklevel=2)
 
     def global_flat(self) -> np.ndarray:
         self.stream.synchronize()

@@ -203,6 +203,8 @@ struct FLBuffers {
     const float* rtab;
     float* cnt;         // FL_EVAL_LAGGED: confusion counts of the previous round's local model
     float* lbuf;        // FL_EVAL_LAGGED: the previous round's loss, published one round later
+    int* sat;           // optional: set to 1 by the Adam kernel when an fp16 slab partial it reads is
+                        // saturated (|x| = 65504, slab_store_h's clamp) or not finite
 };
 
 // Evaluation placement of a round (`mode` of the train kernels).

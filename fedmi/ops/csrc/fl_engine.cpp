@@ -223,6 +223,7 @@ class FLEngine {
         // host-built device tables owned by the caller
         b_.sched = as_ptr<const float>(bufs["sched"].cast<uintptr_t>());
         b_.rtab = as_ptr<const float>(bufs["rtab"].cast<uintptr_t>());
+        b_.sat = bufs.contains("sat") ? as_ptr<int>(bufs["sat"].cast<uintptr_t>()) : nullptr;
         {
             // FL_EVAL_LAGGED: previous round's counts + loss (zero)
             const size_t nlag = FL_MAX_CLASSES * FL_MAX_CLASSES + 4;

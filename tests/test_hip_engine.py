@@ -572,6 +572,29 @@ def test_bf16_grad_slab_auto_and_formats_agree():
     ha, hf = auto.history(), f32.history()
     assert abs(ha["global"][-1, 0] - hf["global"][-1, 0]) < 0.01
     assert abs(ha["loss"][-1] - hf["loss"][-1]) < 0.01
+    assert not auto.slab_saturated and int(auto.sat.item()) == 0
+
+
+def test_bf16_fp16_slab_saturation_is_reported():
+    """The fp16 slab clamps partials at +-65504 (slab_store_h); the Adam kernel flags any clamped
+    or non-finite partial it reads, and the engine warns (debug mode: raises) at the next history
+    read instead of training on silently clipped gradients."""
+    import warnings
+    X, y = make_income_like(3000, seed=5)
+    big = (X * 1e5).astype(np.float32)      # partials of 32 rows x |x| ~ 1e5 >> 65504
+    flat = init_flat(DIMS, 3)
+    e = HipRoundEngine(big, y, 2, EngineConfig(max_rounds=8, early_stop=False, dtype="bf16", grad_slab="fp16",
+                                               graph_rounds=0), None, flat)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        e.run(2)
+        e.sync_history()
+    assert e.slab_saturated and any("saturated" in str(x.message) for x in w)
+    d = HipRoundEngine(big, y, 2, EngineConfig(max_rounds=8, early_stop=False, dtype="bf16", grad_slab="fp16",
+                                               graph_rounds=0, debug=True), None, flat)
+    with pytest.raises(FloatingPointError, match="saturated"):
+        d.run(2)
+        d.sync_history()
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
