@@ -42,7 +42,15 @@ def parse_args(argv=None):
     ap.add_argument("--lr", type=float, default=0.004)
     ap.add_argument("--step-size", type=int, default=30)
     ap.add_argument("--gamma", type=float, default=0.5)
-    ap.add_argument("--local-steps", type=int, default=1)
+    ap.add_argument("--local-steps", "--local-epochs", dest="local_steps", type=int, default=1,
+                    help="local full-batch Adam steps per round (= local epochs: one step is one pass over the "
+                         "shard, C:63-73)")
+    ap.add_argument("--clients", type=int, default=0,
+                    help="simulate K clients in THIS process (fedmi.fl.simulate.ClientGroup: K engines, FedAvg as an "
+                         "in-process rank-order sum) instead of one client per process; 0 = one per process")
+    ap.add_argument("--synthetic", action="store_true",
+                    help="train on --synthetic-rows income-shaped rows per client (device Philox generator, 15 %% "
+                         "label noise) instead of the CSV")
     ap.add_argument("--fedprox-mu", type=float, default=0.0)
     ap.add_argument("--participation", type=float, default=1.0,
                     help="fraction of clients sampled per round (both engines; 1.0 = all, the reference)")
@@ -110,6 +118,57 @@ def main_wide(a, comm):
     return res
 
 
+def _dataset(a, comm):
+    """--synthetic: this client's shard of income-shaped rows, generated where it trains (on the
+    GPU by the Philox kernel, rows [rank n, (rank + 1) n) of one stream; numpy on CPU), plus a
+    held-out slice of the same distribution for --mode correct."""
+    from types import SimpleNamespace
+    n = int(a.synthetic_rows)
+    if comm.device.type == "cuda":
+        from fedmi.data.synthetic import device_shard
+        X, y = device_shard(n, comm.rank, comm.device, seed=a.seed + 7)
+        Xt, yt = device_shard(max(n // 4, 1), comm.size + comm.rank, comm.device, seed=a.seed + 7)
+        Xt, yt = Xt.cpu().numpy(), yt.cpu().numpy().astype(np.int64)
+    else:
+        from fedmi.data.synthetic import make_income_like
+        X, y = make_income_like(n, seed=a.seed * 1000 + comm.rank)
+        Xt, yt = make_income_like(max(n // 4, 1), seed=a.seed * 1000 + 999)
+    return SimpleNamespace(X_train=X, y_train=y, X_test=Xt, y_test=yt)
+
+
+def main_clients(a, comm):
+    """--clients K: K clients of one federation in this process (reference semantics client for
+    client: own shard, local step, local evaluation, sample-weighted FedAvg, early stop on the
+    mean of the clients' metrics), reference console output."""
+    from fedmi.fl.simulate import ClientGroup
+    from fedmi.obs.console import print_history
+    if comm.Get_size() > 1:
+        raise SystemExit("--clients simulates a federation in one process; launch it without torchrun / mpiexec")
+    if a.save or a.resume or a.participation < 1.0:
+        raise SystemExit("--clients does not combine with --save / --resume / --participation")
+    ds = load_tabular(a.data, label=a.label, with_mean=True)
+    cfg = EngineConfig(hidden=tuple(a.hidden), lr=a.lr, step_size=a.step_size, gamma=a.gamma,
+                       local_steps=a.local_steps, prox_mu=a.fedprox_mu, early_stop=not a.no_early_stop,
+                       patience=a.patience, tolerance=a.tolerance, max_rounds=a.rounds, seed=a.seed, dtype=a.dtype)
+    backend = a.engine if a.engine != "auto" else ("hip" if comm.device.type == "cuda" else "torch")
+    shard = a.partition or ("compat" if a.mode == "compat" else "iid")
+    g = ClientGroup(ds.X_train, ds.y_train, a.clients, cfg, backend=backend, shard_mode=shard, seed=a.seed,
+                    alpha=a.alpha, device=comm.device if backend == "hip" else None)
+    t0 = time.perf_counter()
+    g.run(a.rounds)
+    wall = time.perf_counter() - t0
+    h = g.history()
+    if not a.quiet:
+        print_history(h, a.patience)
+    print(f"{a.clients} simulated clients ({backend}): {h['rounds_run']} rounds in {wall:.2f} s", flush=True)
+    if a.jsonl:
+        w = JsonlWriter(a.jsonl)
+        w.history(h, clients=a.clients, script="C-clients", aggregation="in-process", wall_s=wall)
+        w.close()
+    comm.close()
+    return h
+
+
 def main(argv=None):
     a = parse_args(argv)
     if not 0.0 < a.participation <= 1.0:
@@ -122,9 +181,11 @@ def main(argv=None):
     if a.wide:
         return main_wide(a, comm)
     rank, size = comm.Get_rank(), comm.Get_size()
+    if a.clients:
+        return main_clients(a, comm)
 
     # every rank derives the same split locally: no broadcast of the table (C:243-246)
-    ds = load_tabular(a.data, label=a.label, with_mean=True)
+    ds = _dataset(a, comm) if a.synthetic else load_tabular(a.data, label=a.label, with_mean=True)
     cfg = EngineConfig(hidden=tuple(a.hidden), lr=a.lr, step_size=a.step_size, gamma=a.gamma,
                        local_steps=a.local_steps, prox_mu=a.fedprox_mu, participation=a.participation, early_stop=not a.no_early_stop,
                        patience=a.patience, tolerance=a.tolerance, max_rounds=a.rounds,
@@ -132,7 +193,9 @@ def main(argv=None):
                        debug=a.debug, dtype=a.dtype)
     trainer = FederatedMLPLearning(ds.X_train, ds.y_train, rank, size, comm=comm, hidden_sizes=a.hidden,
                                    mode=a.mode, backend=a.engine, seed=a.seed, config=cfg,
-                                   shard_mode=a.partition, alpha=a.alpha)
+                                   shard_mode=a.partition, alpha=a.alpha, presharded=a.synthetic,
+                                   output_size=2 if a.synthetic else None,
+                                   n_total=a.synthetic_rows * size if a.synthetic else None)
     if a.resume:
         done = resume(a.resume, trainer)
         if rank == 0:

@@ -101,12 +101,28 @@ def main(argv=None):
     ap.add_argument("--resume", default=None, help="reuse the trials of a sweep saved with --save")
     ap.add_argument("--federated", action="store_true",
                     help="round-engine sweep over hidden x lr x local steps (BASELINE config 5)")
-    ap.add_argument("--local-steps", type=int, nargs="+", default=None, help="--federated: local steps grid")
+    ap.add_argument("--local-steps", "--local-epochs", dest="local_steps", type=int, nargs="+", default=None,
+                    help="--federated: local steps grid (one full-batch step = one local epoch)")
+    ap.add_argument("--hpo-grid", default=None,
+                    help='the whole grid as JSON, e.g. \'{"hidden": [[50, 200], [100]], "lr": [0.002, 0.004], '
+                         '"local_steps": [1, 2]}\' (keys optional; overrides --hidden / --lrs / --local-steps)')
     ap.add_argument("--trials-per-gpu", type=int, default=6, help="--federated: concurrent trials per GPU")
     ap.add_argument("--dtype", choices=["fp64", "fp32", "bf16"], default=None,
                     help="sklearn sweep: estimator precision fp64 (default, sklearn's float64) | fp32; "
                          "--federated: engine MFMA dtype fp32 (default) | bf16")
     a = ap.parse_args(argv)
+    if a.hpo_grid:
+        grid_spec = json.loads(a.hpo_grid)
+        unknown = set(grid_spec) - {"hidden", "lr", "local_steps"}
+        if unknown:
+            ap.error(f"--hpo-grid: unknown keys {sorted(unknown)}")
+        if "hidden" in grid_spec:
+            a.hidden = repr([tuple(int(x) for x in (h if isinstance(h, (list, tuple)) else [h]))
+                             for h in grid_spec["hidden"]])
+        if "lr" in grid_spec:
+            a.lrs = [float(x) for x in grid_spec["lr"]]
+        if "local_steps" in grid_spec:
+            a.local_steps = [int(x) for x in grid_spec["local_steps"]]
     if a.federated:
         if a.dtype == "fp64":
             ap.error("--federated engines run fp32 or bf16")
