@@ -591,216 +591,7 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
 #undef NT_STAMP
 }
 
-// ---------------------------------------------------------------------------------------------
-// 256x256 register-staged variant (variant 5): variant 3's phases, waves, LDS images, slot
-// schedule and k order (bit-identical output), with every operand piece staged global -> VGPR ->
-// LDS instead of by LDS-DMA.  The r1 timing experiment put ~20 % of the main loop in the LDS-DMA
-// issue (no DMA at all: 1870 vs 1345-1377 TF/s, profiles/nt_ksweep_r1_experiments.log), and
-// hipBLASLt's kernel for these shapes does not stage by DMA (profiles/hipblaslt_kernels_r3.txt).
-// A piece that variant 3 DMAs in phase g (into a slot free by then) is loaded into registers in
-// phase g - 3 (16 B per lane, the same per-lane source address) and written with one
-// ds_write_b128 (LDS-linear, lane * 16: the same placement) in phase g's memory section; the
-// write retires at that phase's lgkmcnt(0), before its first barrier's successors read.  A ring
-// of 4 register pairs (the phase index mod 4) holds the loads in flight; the wait before phase g's
-// writes counts the loads issued after them exactly (6, or fewer near the end of K).
-// ASM (variant 6): the piece loads as inline-asm global_load_dwordx4, invisible to hipcc's waitcnt
-// bookkeeping, which otherwise drains vmcnt to 0 before every piece load (its loop-carried
-// register scores cannot see that a ring slot's previous load was consumed three phases ago) --
-// the waits are this kernel's own counted vmcnt, in a statement that names the consumed pair
-// (guide section 5.7, form (ii)).
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void gload16_asm(u32x4& d, const char* p) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void vm_wait_pair(u32x4& a, u32x4& b) {
-    asm volatile("s_waitcnt vmcnt(%c2)" : "+v"(a), "+v"(b) : "i"(N) : "memory");
-}
-
-template <int F, bool ASM>
-__global__ void __launch_bounds__(NT2_THREADS)
-gemm_nt_bf16_rs_kernel(NTArgs g) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
-    const int mt = g.M / NT2_BM, nt = g.N / NT2_BM;
-    const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
-    constexpr int GM = 8;  // grouped tile order (variant 2)
-    const int grp = bid / (GM * nt), first_m = grp * GM;
-    const int gsz = min(mt - first_m, GM);
-    const int in_grp = bid - grp * GM * nt;
-    const int m0 = (first_m + in_grp % gsz) * NT2_BM, n0 = (in_grp / gsz) * NT2_BM;
-    const __hip_bfloat16* A = reinterpret_cast<const __hip_bfloat16*>(g.A);
-    const __hip_bfloat16* B = reinterpret_cast<const __hip_bfloat16*>(g.B);
-    const int t = threadIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63;
-    const int wr = w >> 2, wc = w & 3;
-    const int lr = l & 15, lg = l >> 4;
-
-    uint32_t voA[2], voB[2];
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-        const int c = (l & 7) ^ ((4 * par + (l >> 4)) & 7);
-        voA[par] = (uint32_t)(((l >> 3) * g.lda + c * 8) * 2);
-        voB[par] = (uint32_t)(((l >> 3) * g.ldb + c * 8) * 2);
-    }
-    const int rm0 = (w < 4) ? 16 * w : 128 + 16 * (w - 4);
-    const char* sbB = reinterpret_cast<const char*>(B + (size_t)(n0 + 32 * w) * g.ldb);
-    const char* sbA0 = reinterpret_cast<const char*>(A + (size_t)(m0 + rm0) * g.lda);
-    const char* sbA1 = reinterpret_cast<const char*>(A + (size_t)(m0 + rm0 + 64) * g.lda);
-    const size_t rowB8 = (size_t)8 * g.ldb * 2, rowA8 = (size_t)8 * g.lda * 2;
-    const int KT = g.K / 64;
-    // piece j (0, 1) of the pair variant 3 DMAs in global phase q = 4 kt + r:
-    //   r = 0: B(kt+1, 2+j) | 1: A(kt+1, m0 half, j) | 2: A(kt+1, m1 half, j) | 3: B(kt+2, j)
-    // (K >= 192 here, launch check: the prologue's pieces all exist and the main loop runs at
-    // least once, so no register holding an in-flight load is ever defined on one path only)
-    auto ptile = [](int q) { return (q >> 2) + ((q & 3) == 3 ? 2 : 1); };
-    auto psrc = [&](int q, int j) -> const char* {
-        const int r = q & 3, tile = ptile(q);
-        if (r == 0) return sbB + (2 + j) * rowB8 + tile * 128 + voB[j & 1];
-        if (r == 3) return sbB + j * rowB8 + tile * 128 + voB[j & 1];
-        return (r == 2 ? sbA1 : sbA0) + j * rowA8 + tile * 128 + voA[j & 1];
-    };
-    auto pdst = [&](int q, int j) -> char* {
-        const int r = q & 3, tile = ptile(q);
-        char* base = smem + (tile & 1) * 65536;
-        if (r == 0) return base + 32768 + (32 * w + 8 * (2 + j)) * 128;
-        if (r == 3) return base + 32768 + (32 * w + 8 * j) * 128;
-        return base + (rm0 + (r == 2 ? 64 : 0) + 8 * j) * 128;
-    };
-    auto ld16 = [&](u32x4& d, const char* p) {
-        if (ASM) gload16_asm(d, p);
-        else d = *reinterpret_cast<const u32x4*>(p);
-    };
-    auto st16 = [&](char* p, const u32x4& v) { *reinterpret_cast<u32x4*>(p + l * 16) = v; };
-
-    const int f = (lr >> 1) & 7;
-    const int fo0 = lr * 128 + ((lg ^ f) << 4), fo1 = lr * 128 + (((4 + lg) ^ f) << 4);
-    const int aoff = wr * 128 * 128, boff = 32768 + wc * 64 * 128;
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 af[4], bfr[4], bfr1[4];
-    u32x4 st[4][2];  // loads in flight: ring slot = global phase mod 4
-
-    // prologue: tile 0 (all 8 pieces) and tile 1's B01 -- what variant 3 DMAs before phase 0 --
-    // through registers, while the pairs of phases 0..2 are already loading (16 loads)
-    {
-        u32x4 pv[10];
-        const int t1 = 128;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ld16(pv[i], sbB + i * rowB8 + voB[i & 1]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            ld16(pv[4 + i], sbA0 + i * rowA8 + voA[i & 1]);
-            ld16(pv[6 + i], sbA1 + i * rowA8 + voA[i & 1]);
-        }
-        ld16(pv[8], sbB + t1 + voB[0]);
-        ld16(pv[9], sbB + rowB8 + t1 + voB[1]);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            ld16(st[q][0], psrc(q, 0));
-            ld16(st[q][1], psrc(q, 1));
-        }
-        if (ASM) {
-#pragma unroll
-            for (int i = 0; i < 10; i += 2) vm_wait_pair<6>(pv[i], pv[i + 1]);
-        } else {
-            vm_wait<6>();
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st16(smem + 32768 + (32 * w + 8 * i) * 128, pv[i]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            st16(smem + (rm0 + 8 * i) * 128, pv[4 + i]);
-            st16(smem + (rm0 + 64 + 8 * i) * 128, pv[6 + i]);
-        }
-        st16(smem + 65536 + 32768 + (32 * w) * 128, pv[8]);
-        st16(smem + 65536 + 32768 + (32 * w + 8) * 128, pv[9]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();
-
-    // tp = -1: a main-loop K-tile (every piece it loads or writes exists); tp = 0 / 1: the last
-    // two K-tiles, whose piece validity is then a compile-time function of (tp, r): a piece past
-    // the end is neither loaded nor written, and the wait before the writes is one counted vmcnt
-    // -- never a runtime branch (branches made hipcc copy registers still in flight ahead of the
-    // wait), and no load whose destination hipcc would consider dead and reuse before it lands
-    auto phase = [&](int kt, int r, int tp) {
-        const int q = 4 * kt + r;
-        const char* buf = smem + (kt & 1) * 65536;
-        const int mh = (r == 1 || r == 2) ? 1 : 0;
-        const int fo = (r >= 2) ? fo1 : fo0;
-        // tile of phase q + k relative to this tile: (r + k) / 4 + (r' == 3 ? 2 : 1); valid iff it
-        // is at most the last K-tile (tp - 1 = this tile relative to the last one)
-        auto rel = [&](int k) { return (r + k) / 4 + (((r + k) & 3) == 3 ? 2 : 1); };
-        auto valid = [&](int k) { return tp < 0 || (tp - 1) + rel(k) <= 0; };
-        if (valid(3)) {
-            ld16(st[(r + 3) & 3][0], psrc(q + 3, 0));
-            ld16(st[(r + 3) & 3][1], psrc(q + 3, 1));
-        }
-        if (valid(0)) {
-            const int nv = (valid(1) ? 2 : 0) + (valid(2) ? 2 : 0) + (valid(3) ? 2 : 0);  // issued after it
-            if (nv == 6) {
-                if (ASM) vm_wait_pair<6>(st[r][0], st[r][1]); else vm_wait<6>();
-            } else if (nv == 4) {
-                if (ASM) vm_wait_pair<4>(st[r][0], st[r][1]); else vm_wait<4>();
-            } else if (nv == 2) {
-                if (ASM) vm_wait_pair<2>(st[r][0], st[r][1]); else vm_wait<2>();
-            } else {
-                if (ASM) vm_wait_pair<0>(st[r][0], st[r][1]); else vm_wait<0>();
-            }
-            st16(pdst(q, 0), st[r][0]);
-            st16(pdst(q, 1), st[r][1]);
-        }
-        if (r == 0) {
-#pragma unroll
-            for (int y = 0; y < 4; ++y) bfr[y] = *reinterpret_cast<const bf16x8*>(buf + boff + y * 16 * 128 + fo0);
-        } else if (r == 1) {
-#pragma unroll
-            for (int y = 0; y < 4; ++y) bfr1[y] = *reinterpret_cast<const bf16x8*>(buf + boff + y * 16 * 128 + fo1);
-        }
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-            af[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + (mh * 64 + x * 16) * 128 + fo);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_setprio(1);
-        if (r <= 1) {
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y)
-                    acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr[y], acc[mh * 4 + x][y], 0, 0, 0);
-        } else {
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y)
-                    acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr1[y], acc[mh * 4 + x][y], 0, 0, 0);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
-    };
-
-    int kt = 0;
-    for (; kt + 2 < KT; ++kt) {
-        phase(kt, 0, -1);
-        phase(kt, 1, -1);
-        phase(kt, 2, -1);
-        phase(kt, 3, -1);
-    }
-    phase(kt, 0, 0); phase(kt, 1, 0); phase(kt, 2, 0); phase(kt, 3, 0);
-    ++kt;
-    phase(kt, 0, 1); phase(kt, 1, 1); phase(kt, 2, 1); phase(kt, 3, 1);
-    if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
-    pp_epilogue<F>(g, smem, acc, m0, n0, w, l);
-}
-
-static int g_nt_variant = 3;  // 3: full-line 256x256 loop (default), 5/6: register-staged (6: asm loads),
-                               // 2: half-line, 1/0: 128x128
+static int g_nt_variant = 3;  // 3: full-line 256x256 loop (default), 2: half-line, 1/0: 128x128
 void gemm_nt_set_variant(int v) { g_nt_variant = v; }
 static unsigned long long* g_nt_dbg = nullptr;
 void gemm_nt_set_debug(unsigned long long* dbg) { g_nt_dbg = dbg; }
@@ -815,38 +606,6 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
         (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
         hipLaunchKernelGGL(gemm_nt_bf16_pp_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
-        return hipGetLastError();
-    }
-    if ((g_nt_variant == 5 || g_nt_variant == 6) && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 && g.K >= 192 &&
-        (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&
-        (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
-        (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
-        const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
-        switch (nt_epi_flags(g)) {
-#define NT_RS_CASE(F)                                                                                     \
-    case F:                                                                                               \
-        if (g_nt_variant == 6)                                                                            \
-            hipLaunchKernelGGL((gemm_nt_bf16_rs_kernel<F, true>), dim3(blocks), dim3(NT2_THREADS), 0, s, g); \
-        else                                                                                              \
-            hipLaunchKernelGGL((gemm_nt_bf16_rs_kernel<F, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g); \
-        break;
-            NT_RS_CASE(NT_EPI_CB)
-            NT_RS_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_BIAS | NT_EPI_RELU)
-            NT_RS_CASE(NT_EPI_CB | NT_EPI_BIAS | NT_EPI_RELU)
-            NT_RS_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK)
-            NT_RS_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK | NT_EPI_CSUM)
-            NT_RS_CASE(NT_EPI_CB | NT_EPI_MASK)
-            NT_RS_CASE(NT_EPI_C)
-            NT_RS_CASE(NT_EPI_C | NT_EPI_BETA)
-            NT_RS_CASE(NT_EPI_C | NT_EPI_BIAS)
-#undef NT_RS_CASE
-            default:
-                if (g_nt_variant == 6)
-                    hipLaunchKernelGGL((gemm_nt_bf16_rs_kernel<-1, true>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);
-                else
-                    hipLaunchKernelGGL((gemm_nt_bf16_rs_kernel<-1, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);
-                break;
-        }
         return hipGetLastError();
     }
     if (g_nt_variant == 3 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
