@@ -211,14 +211,10 @@ static inline int nt_epi_flags(const NTArgs& g) {
            (g.C != nullptr && g.beta != 0.f ? NT_EPI_BETA : 0) | (g.csum != nullptr ? NT_EPI_CSUM : 0);
 }
 
-// NW = 8 waves as 2 x 4 (128 x 64 outputs per wave, acc[8][4]) or NW = 4 waves as 2 x 2 (128 x 128,
-// acc[8][8]).
-template <int F, int NW = 8>
-__device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (&acc)[8][32 / NW], int m0, int n0,
-                                            int w, int l) {
-    constexpr int YT = 32 / NW, WN = 16 * YT;  // 16-column tiles per wave, columns per wave
-    constexpr int RI = 256 / (2 * NW);          // row-pair iterations of the block-wide loops
-    const int wr = w / (NW / 2), wc = w % (NW / 2);
+template <int F>
+__device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (&acc)[8][4], int m0, int n0, int w,
+                                            int l) {
+    const int wr = w >> 2, wc = w & 3;
     const int lr = l & 15, lg = l >> 4;
     const bool hC = F < 0 ? g.C != nullptr : (F & NT_EPI_C) != 0;
     const bool hCb = F < 0 ? g.Cbf16 != nullptr : (F & NT_EPI_CB) != 0;
@@ -244,8 +240,8 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     if (hMask) {
         const __hip_bfloat16* Mk = reinterpret_cast<const __hip_bfloat16*>(g.mask);
 #pragma unroll
-        for (int i = 0; i < RI; ++i) {
-            const int row = i * 2 * NW + w * 2, rr = row + (l >> 5);
+        for (int i = 0; i < 16; ++i) {
+            const int row = i * 16 + w * 2, rr = row + (l >> 5);
             glds16(Mk + (size_t)(m0 + rr) * g.ldmask + n0 + (((l & 31) ^ sw(rr)) << 3), smem + row * 512);
         }
         vm_wait<0>();
@@ -253,8 +249,8 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     }
 
 #pragma unroll
-    for (int y = 0; y < YT; ++y) {
-        const int cl = wc * WN + 16 * y + lr, n = n0 + cl;
+    for (int y = 0; y < 4; ++y) {
+        const int cl = wc * 64 + 16 * y + lr, n = n0 + cl;
         const float bv = hBias ? g.bias[n] : 0.f;
         float cs = 0.f;  // column n's sum over the lane's 32 rows of the bf16 output (hCsum)
 #pragma unroll
@@ -294,8 +290,8 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     if (hCb) {
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < RI; ++i) {
-            const int rr = i * 2 * NW + w * 2 + (l >> 5), p = l & 31;
+        for (int i = 0; i < 16; ++i) {
+            const int rr = i * 16 + w * 2 + (l >> 5), p = l & 31;
             const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * 512 + p * 16);
             *reinterpret_cast<uint4*>(Cb + (size_t)(m0 + rr) * g.ldcb + n0 + ((p ^ sw(rr)) << 3)) = d;
         }
@@ -595,213 +591,6 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
 #undef NT_STAMP
 }
 
-// ---------------------------------------------------------------------------------------------
-// 256x256 four-wave variant (variant 7): 4 waves as 2 x 2, 128 x 128 outputs per wave (8 x 8 tiles of
-// v_mfma_f32_16x16x32_bf16, 256 fp32 accumulators per lane -- the AGPR half of the register file),
-// one wave per SIMD.  Same LDS image as variant 3 (two 64 KiB K-tile buffers of full 128-byte lines,
-// chunk c ^ ((r >> 1) & 7)), same fragment offsets and per-element k order, so the output is
-// bit-identical to variants 2/3.  Each fragment feeds 8 MFMAs instead of 4 (A) / 8 (B), so a K-tile
-// costs 128 KiB of ds_read traffic instead of 192 KiB.
-//
-// Stages are the MFMA k-steps (two per K-tile).  Fragments are double-buffered in registers: stage
-// s's 64 MFMAs run on fragments read during stage s-1, and the stage's one barrier, after its first
-// 16 MFMAs, makes stage s+1's data visible:
-//     16 MFMAs | lgkmcnt(0) [+ vmcnt(0) on a K-tile's second k-step: K-tile t+1 landed] | s_barrier |
-//     48 MFMAs interleaved with stage s+1's 16 fragment reads [+ K-tile t+2's 16 LDS-DMAs into the
-//     buffer K-tile t just vacated, on the second k-step]
-// Every wave's reads of K-tile t retire (lgkmcnt(0)) before the second k-step's barrier, after which
-// its buffer is restaged; a K-tile's DMAs fly for one K-tile of MFMAs (128 per wave) before the
-// vmcnt(0) that retires them.  DMA pieces: wave w fills A rows 64w + 8i and B rows 64w + 8i.
-#ifndef NTQ_R1
-#define NTQ_R1 16  // MFMAs of a stage before its barrier (16, 32 or 48)
-#endif
-static_assert(NTQ_R1 == 16 || NTQ_R1 == 32 || NTQ_R1 == 48, "NTQ_R1");
-template <int F, int ABL = 0, int STG = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-gemm_nt_bf16_q_kernel(NTArgs g) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + 4 * 1024];
-    const int mt = g.M / NT2_BM, nt = g.N / NT2_BM;
-    const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
-    constexpr int GM = 8;  // grouped tile order (variant 2)
-    const int grp = bid / (GM * nt), first_m = grp * GM;
-    const int gsz = min(mt - first_m, GM);
-    const int in_grp = bid - grp * GM * nt;
-    const int m0 = (first_m + in_grp % gsz) * NT2_BM, n0 = (in_grp / gsz) * NT2_BM;
-    const __hip_bfloat16* A = reinterpret_cast<const __hip_bfloat16*>(g.A);
-    const __hip_bfloat16* B = reinterpret_cast<const __hip_bfloat16*>(g.B);
-    const int t = threadIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63;
-    const int wr = w >> 1, wc = w & 1;
-    const int lr = l & 15, lg = l >> 4;
-
-    uint32_t voA[2], voB[2];  // lane offsets of a piece by piece parity (variant 3)
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-        const int c = (l & 7) ^ ((4 * par + (l >> 4)) & 7);
-        voA[par] = (uint32_t)(((l >> 3) * g.lda + c * 8) * 2);
-        voB[par] = (uint32_t)(((l >> 3) * g.ldb + c * 8) * 2);
-    }
-    const char* sbA = reinterpret_cast<const char*>(A + (size_t)(m0 + 64 * w) * g.lda);
-    const char* sbB = reinterpret_cast<const char*>(B + (size_t)(n0 + 64 * w) * g.ldb);
-    const size_t rowA8 = (size_t)8 * g.lda * 2, rowB8 = (size_t)8 * g.ldb * 2;
-    char* dump = smem + 2 * 65536 + w * 1024;  // target of the DMAs issued past the last K-tile
-    auto dma = [&](int tile, int i) {  // piece i: 0..7 A rows 64w + 8i, 8..15 B rows 64w + 8(i - 8)
-        char* base = smem + (tile & 1) * 65536;
-        if (i < 8) glds16(sbA + i * rowA8 + tile * 128 + voA[i & 1], base + (64 * w + 8 * i) * 128);
-        else glds16(sbB + (i - 8) * rowB8 + tile * 128 + voB[i & 1], base + 32768 + (64 * w + 8 * (i - 8)) * 128);
-    };
-    const int f = (lr >> 1) & 7;
-    const int fo0 = lr * 128 + ((lg ^ f) << 4), fo1 = lr * 128 + (((4 + lg) ^ f) << 4);
-    const int aoff = wr * 128 * 128, boff = 32768 + wc * 128 * 128;
-    uint32_t vpo[16];  // lane offset of DMA piece i from the operand's (tile-advanced) wave base
-#pragma unroll
-    for (int i = 0; i < 16; ++i) vpo[i] = i < 8 ? voA[i & 1] + (uint32_t)(i * rowA8) : voB[i & 1] + (uint32_t)((i - 8) * rowB8);
-
-    f32x4 acc[8][8];
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-#pragma unroll
-        for (int y = 0; y < 8; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
-
-    const int KT = g.K / 64;
-    // STG (register staging, variant 8): K-tile kt+2 sits in 64 VGPRs (S) from the second k-step of
-    // K-tile kt-1, is written to LDS on the second k-step of K-tile kt (after the barrier that frees
-    // tile kt's buffer), and S is refilled with K-tile kt+3 right behind each write: two stages of
-    // latency for every global load, and no LDS-DMA issue cost in the main loop.
-    uint4 S[16];
-    auto load_piece = [&](int tile, int i) -> uint4 {
-        uint32_t vo;
-        asm volatile("" : "=v"(vo) : "0"(i < 8 ? voA[i & 1] : voB[i & 1]));
-        const char* src = (i < 8 ? sbA + i * rowA8 : sbB + (i - 8) * rowB8) + tile * 128 + vo;
-        return *reinterpret_cast<const uint4*>(src);
-    };
-    // prologue: K-tiles 0 and 1 in flight, tile 0 retired, stage (0, 0)'s fragments read
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dma(0, i);
-    if (STG) {
-        // branch-free: a second copy of tile 0 (KT = 1) / of tile KT-1 (KT = 2) is harmless
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dma(KT > 1 ? 1 : 0, i);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) S[i] = load_piece(min(2, KT - 1), i);
-        vm_wait<32>();
-    } else if (KT > 1) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dma(1, i);
-        vm_wait<16>();
-    } else {
-        vm_wait<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int y = 0; y < 8; ++y) fb0[y] = *reinterpret_cast<const bf16x8*>(smem + boff + y * 16 * 128 + fo0);
-#pragma unroll
-    for (int x = 0; x < 8; ++x) fa0[x] = *reinterpret_cast<const bf16x8*>(smem + aoff + x * 16 * 128 + fo0);
-
-    // one stage: MFMAs on (ca, cb); the next stage's fragments into (na, nb).  No branches inside a
-    // stage, so the scheduler can interleave its memory instructions with the MFMAs: past the last
-    // K-tile the reads fetch unused LDS and the DMAs re-fetch K-tile KT-1 into a per-wave dump slot
-    // past the two buffers (their vmcnt is retired like any other).
-    auto stage = [&](int kt, int ks, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int x = 0; x < NTQ_R1 / 8; ++x)
-#pragma unroll
-            for (int y = 0; y < 8; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[x], cb[y], acc[x][y], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // K-tile kt+1 landed (every wave's, after the barrier); STG: only the prologue's DMAs of
-        // tile 1 count here -- the 16 loads of S may fly
-        if (ks == 1) {
-            if (STG) vm_wait<16>();
-            else vm_wait<0>();
-        }
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        // the rest: 16 groups of {next-stage fragment read, [DMA,] 3 MFMAs}, each group its own
-        // scheduling region so the matrix pipe never idles while the wave issues its memory
-        // instructions.  Reads: B first, then A (the next stage's first 16 MFMAs read all of B
-        // and A 0-1).
-        const int rtile = ks ? kt + 1 : kt;
-        const char* rbuf = smem + (rtile & 1) * 65536;
-        const int fo = ks ? fo0 : fo1;
-        const int dt = kt + 2;
-        const bool live = dt < KT;
-        const int st = live ? dt : KT - 1;
-        char* dA = live ? smem + (dt & 1) * 65536 + 64 * w * 128 : dump;
-        char* dB = live ? smem + (dt & 1) * 65536 + 32768 + 64 * w * 128 : dump;
-        const int step = live ? 1024 : 0;
-        // uniform 64-bit base + opaque 32-bit lane offset: keeps the saddr form (no per-lane 64-bit
-        // pointers hoisted out of the loop)
-        const char* bA = sbA + st * 128;
-        const char* bB = sbB + st * 128;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            // two fragment reads per group in the first 8 groups: the last one retires long before
-            // the next stage's first MFMA waits for it
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int r = 2 * i + h;
-                if (!(ABL & 2) && r < 16) {
-                    if (r < 8) nb[r] = *reinterpret_cast<const bf16x8*>(rbuf + boff + r * 16 * 128 + fo);
-                    else na[r - 8] = *reinterpret_cast<const bf16x8*>(rbuf + aoff + (r - 8) * 16 * 128 + fo);
-                }
-            }
-            if (ks == 1 && STG) {
-                char* wb = smem + (kt & 1) * 65536 + 64 * w * 128 + l * 16;
-                *reinterpret_cast<uint4*>(wb + (i < 8 ? 8 * i * 128 : 32768 + 8 * (i - 8) * 128)) = S[i];
-                S[i] = load_piece(min(kt + 3, KT - 1), i);
-            }
-            if (ks == 1 && !STG && !(ABL & 1)) {
-                // per-piece 32-bit lane offsets (row block folded in), re-marked opaque in place each
-                // stage so no 64-bit per-lane pointer is hoisted: one M0 write + the DMA per piece
-                asm volatile("" : "+v"(vpo[i]));
-                if (i < 8) glds16(bA + vpo[i], dA + i * step);
-                else glds16(bB + vpo[i], dB + (i - 8) * step);
-            }
-#pragma unroll
-            for (int j = 0; j < (64 - NTQ_R1) / 16; ++j) {
-                const int q = NTQ_R1 + (64 - NTQ_R1) / 16 * i + j, x = q >> 3, y = q & 7;
-                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[x], cb[y], acc[x][y], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    for (int kt = 0; kt < KT; ++kt) {
-        stage(kt, 0, fa0, fb0, fa1, fb1);
-        stage(kt, 1, fa1, fb1, fa0, fb0);
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's LDS reads (and dump DMAs) retired: the epilogue reuses the LDS
-    asm volatile("" ::: "memory");
-    pp_epilogue<F, 4>(g, smem, acc, m0, n0, w, l);
-}
-
-// the output configurations of the wide client's GEMMs get their own instantiation
-template <int STG>
-static void launch_q(const NTArgs& g, int blocks, hipStream_t s) {
-    switch (nt_epi_flags(g)) {
-#define NT_Q_CASE(F) \
-    case F: hipLaunchKernelGGL((gemm_nt_bf16_q_kernel<F, 0, STG>), dim3(blocks), dim3(256), 0, s, g); break;
-        NT_Q_CASE(NT_EPI_CB)
-        NT_Q_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_BIAS | NT_EPI_RELU)
-        NT_Q_CASE(NT_EPI_CB | NT_EPI_BIAS | NT_EPI_RELU)
-        NT_Q_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK)
-        NT_Q_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_MASK | NT_EPI_CSUM)
-        NT_Q_CASE(NT_EPI_CB | NT_EPI_MASK)
-        NT_Q_CASE(NT_EPI_C)
-        NT_Q_CASE(NT_EPI_C | NT_EPI_BETA)
-        NT_Q_CASE(NT_EPI_C | NT_EPI_BIAS)
-#undef NT_Q_CASE
-        default: hipLaunchKernelGGL((gemm_nt_bf16_q_kernel<-1, 0, STG>), dim3(blocks), dim3(256), 0, s, g); break;
-    }
-}
-
 static int g_nt_variant = 3;  // 3: full-line 256x256 loop (default), 2: half-line, 1/0: 128x128
 void gemm_nt_set_variant(int v) { g_nt_variant = v; }
 static unsigned long long* g_nt_dbg = nullptr;
@@ -840,23 +629,6 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
 #undef NT_FL_CASE
             default: hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel<-1>, dim3(blocks), dim3(NT2_THREADS), 0, s, g); break;
         }
-        return hipGetLastError();
-    }
-    if ((g_nt_variant == 7 || g_nt_variant == 8) && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
-        (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&
-        (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
-        (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
-        const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
-        if (g_nt_variant == 7) launch_q<0>(g, blocks, s);
-        else launch_q<1>(g, blocks, s);
-        return hipGetLastError();
-    }
-    if (g_nt_variant >= 71 && g_nt_variant <= 73 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0) {
-        // timing ablations of variant 7 (wrong results): 71 no main-loop DMAs, 72 no fragment reads, 73 neither
-        const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
-        if (g_nt_variant == 71) hipLaunchKernelGGL((gemm_nt_bf16_q_kernel<-1, 1>), dim3(blocks), dim3(256), 0, s, g);
-        if (g_nt_variant == 72) hipLaunchKernelGGL((gemm_nt_bf16_q_kernel<-1, 2>), dim3(blocks), dim3(256), 0, s, g);
-        if (g_nt_variant == 73) hipLaunchKernelGGL((gemm_nt_bf16_q_kernel<-1, 3>), dim3(blocks), dim3(256), 0, s, g);
         return hipGetLastError();
     }
     if (g.csum != nullptr) return hipErrorInvalidValue;  // column sums: 256x256 loops only

@@ -285,10 +285,10 @@ def test_skinny_wgrad_bf16(C, trans, rows, splits):
 @pytest.mark.parametrize("M,N,K,pad", [(256, 512, 64, 0), (256, 256, 128, 0), (512, 768, 192, 64), (768, 512, 1024, 0),
                                        (2048, 1024, 4096, 8)])
 def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
-    """The 256x256 main loops (variant 2: half-line DMA pieces, variant 3: whole-line pieces and
-    128-byte LDS rows, variant 7: four waves of 128x128) against the 128x128 loop (variant 1):
-    same per-element k order, so bit-identical, and against an fp32 torch reference; row strides
-    wider than K exercise the DMA source addressing."""
+    """The 256x256 ping-pong main loops (variant 2: half-line DMA pieces, variant 3: whole-line
+    pieces and 128-byte LDS rows) against the 128x128 loop (variant 1): same per-element k
+    order, so bit-identical, and against an fp32 torch reference; row strides wider than K
+    exercise the DMA source addressing."""
     m = native()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
@@ -298,7 +298,7 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     bias = torch.randn(N, device=dev)
     outs = []
     try:
-        for v in (1, 2, 3, 7):
+        for v in (1, 2, 3):
             m.gemm_nt_set_variant(v)
             Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             CbT = torch.empty(N, M, dtype=torch.bfloat16, device=dev)
@@ -314,7 +314,7 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     mask = torch.randn(M, N + 8, device=dev).to(torch.bfloat16)
     mouts = []
     try:
-        for v in (1, 2, 3, 7):
+        for v in (1, 2, 3):
             m.gemm_nt_set_variant(v)
             Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             m.gemm_nt(M, N, K, A.data_ptr(), K + pad, B.data_ptr(), K + pad, 0, 0, Cb.data_ptr(), N, 0, 0, 0,
@@ -323,11 +323,11 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
             mouts.append(Cb)
     finally:
         m.gemm_nt_set_variant(3)
-    assert all(torch.equal(mouts[0], o) for o in mouts[1:])
+    assert torch.equal(mouts[0], mouts[1]) and torch.equal(mouts[0], mouts[2])
     mref = torch.where(mask[:, :N].float() > 0, A[:, :K].float() @ B[:, :K].float().t(), torch.zeros(M, N, device=dev))
     assert ((mouts[1].float() - mref).abs().max() / mref.abs().max()).item() < 1e-2
     ref = (A[:, :K].float() @ B[:, :K].float().t() + bias).clamp_min(0)
-    for v in (1, 2, 3):
+    for v in (1, 2):
         assert torch.equal(outs[0][0], outs[v][0])
         assert torch.equal(outs[0][1], outs[v][1])
     assert ((outs[1][0] - ref).abs().max() / ref.abs().max()).item() < 1e-5
@@ -336,9 +336,8 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
 @pytest.mark.parametrize("cfg", ["Cb", "Cb+CbT+bias+relu", "Cb+bias+relu", "Cb+CbT+mask", "Cb+mask", "C", "C+beta",
                                  "C+bias"])
 def test_gemm_nt_bf16_epilogue_configs(cfg):
-    """Every output configuration the full-line loops (variants 3 and 7) compile separately (wide
-    forward, dgrad, wgrad, logits, plain) is bit-identical to the 128x128 loop's
-    runtime-configured epilogue."""
+    """Every output configuration the full-line loop compiles separately (wide forward, dgrad,
+    wgrad, logits, plain) is bit-identical to the 128x128 loop's runtime-configured epilogue."""
     m = native()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
@@ -351,7 +350,7 @@ def test_gemm_nt_bf16_epilogue_configs(cfg):
     C0 = torch.randn(M, N, device=dev)
     outs = []
     try:
-        for v in (1, 3, 7):
+        for v in (1, 3):
             m.gemm_nt_set_variant(v)
             C = C0.clone()
             Cb = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
@@ -365,13 +364,11 @@ def test_gemm_nt_bf16_epilogue_configs(cfg):
             outs.append((C, Cb, CbT))
     finally:
         m.gemm_nt_set_variant(3)
-    for o in outs[1:]:
-        for a, b in zip(outs[0], o):
-            assert torch.equal(a, b)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [3, 7])
-def test_gemm_nt_bf16_dgrad_column_sums(variant):
+def test_gemm_nt_bf16_dgrad_column_sums():
     """NT_EPI_CSUM: the dgrad epilogue's per-128-row column sums of its bf16 output (bias
     gradient) fold to torch's column sums of the same output; the other outputs are unchanged,
     and the 128x128 loop refuses the option."""
@@ -384,18 +381,14 @@ def test_gemm_nt_bf16_dgrad_column_sums(variant):
     B = torch.randn(N, K, device=dev).to(torch.bfloat16)
     mask = torch.randn(M, N, device=dev).to(torch.bfloat16)
     outs = []
-    try:
-        m.gemm_nt_set_variant(variant)
-        for csum in (False, True):
-            Cb = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
-            CbT = torch.zeros(N, M, dtype=torch.bfloat16, device=dev)
-            cs = torch.full((M // 128, N), float("nan"), device=dev)
-            m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, CbT.data_ptr(), M, 0,
-                      mask.data_ptr(), N, 0, 1.0, 0.0, s, cs.data_ptr() if csum else 0, N)
-            torch.cuda.synchronize()
-            outs.append((Cb, CbT, cs))
-    finally:
-        m.gemm_nt_set_variant(3)
+    for csum in (False, True):
+        Cb = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        CbT = torch.zeros(N, M, dtype=torch.bfloat16, device=dev)
+        cs = torch.full((M // 128, N), float("nan"), device=dev)
+        m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb.data_ptr(), N, CbT.data_ptr(), M, 0,
+                  mask.data_ptr(), N, 0, 1.0, 0.0, s, cs.data_ptr() if csum else 0, N)
+        torch.cuda.synchronize()
+        outs.append((Cb, CbT, cs))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     cs = outs[1][2]
     ref = outs[1][0].float().view(M // 128, 128, N).sum(1)
