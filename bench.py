@@ -361,6 +361,9 @@ def main_wide(a) -> None:
                        "parallelism": f"fedavg{N} (1 client/GPU, per-layer RCCL buckets, "
                                       f"{a.wide_allreduce} on the wire)", "rccl_env": comm.rccl_env},
             "tflops_per_client": c.flops_per_round / (dt / a.steps) / 1e12,
+            # one client: round r's local evaluation is scored from round r+1's training forward
+            # (same weights, rows and kernels: bit-identical counts), so tflops counts executed work
+            "round_design": "fused-eval" if c.fused_eval else "separate-eval",
             "local_train_acc_synthetic": c.metrics()["accuracy"],
             "lr": lr, "rounds_run": c.round,
             "loss_first_round": first_loss, "loss_last_round": last_loss,

@@ -41,7 +41,8 @@ class WideClient:
     def __init__(self, X: torch.Tensor, y: torch.Tensor, dims: Sequence[int], comm=None, n_total: Optional[int] = None,
                  micro_batch: int = 131072, lr: float = 0.004, betas=(0.9, 0.999), eps: float = 1e-8,
                  step_size: int = 30, gamma: float = 0.5, seed: int = 0, dtype: str = "bf16",
-                 eval_rows: int = 0, allreduce_dtype: str = "fp32", warmup_rounds: int = 0):
+                 eval_rows: int = 0, allreduce_dtype: str = "fp32", warmup_rounds: int = 0,
+                 fused_eval: Optional[bool] = None):
         from ..ops import native
         self.m = native()
         self.dev = X.device
@@ -114,6 +115,15 @@ class WideClient:
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         self.cm = torch.zeros(dims[-1] * dims[-1], dtype=torch.float32, device=dev)  # local confusion counts
         self.evaluated = False
+        # Fused evaluation (one client: FedAvg is the identity, so the post-step local model IS the
+        # next round's model): the local evaluation of round r is scored from round r+1's training
+        # forward -- the same kernels on the same weights and rows, so bit-identical logits, one
+        # forward pass fewer per round.  metrics() flushes a pending evaluation with its own
+        # forward pass when it is asked for before the next round runs.
+        self.fused_eval = (comm is None or self.world == 1) if fused_eval is None else bool(fused_eval)
+        if self.fused_eval and self.world > 1:
+            raise ValueError("fused_eval needs one client (with FedAvg the next forward sees the global model)")
+        self._eval_pending = False
         self.round = 0
         self.stream = torch.cuda.Stream(device=dev)
         self.comm_stream = torch.cuda.Stream(device=dev)
@@ -377,11 +387,18 @@ class WideClient:
         self._local_quantized = False
         C = self.dims[-1]
         s = self._s()
+        fuse = self._eval_pending  # this forward also scores the previous round's evaluation
+        self._eval_pending = False
         with torch.cuda.stream(self.stream):
             self.loss_acc.zero_()
+            if fuse:
+                self.cm.zero_()
             for r0 in range(0, self.n, self.mb):
                 rows = min(self.mb, self.n - r0)
                 self._forward(r0, rows)
+                if fuse:
+                    self.m.logits_confusion(self.logits.data_ptr(), self.logits.stride(0), self.y[r0:].data_ptr(),
+                                            rows, C, self.cm.data_ptr(), s)
                 # loss head: softmax CE, dZ = (p - onehot) / n (full-batch mean)
                 self.m.xent(self.logits.data_ptr(), self.logits.stride(0), self.y[r0:].data_ptr(), rows, C, 0,
                             1.0 / self.n,
@@ -435,7 +452,16 @@ class WideClient:
     def evaluate_shard(self) -> None:
         """Local evaluation of the post-step local model on the WHOLE shard (C:148, C:75-91):
         micro-batched forward passes, argmax + confusion counts on the device into
-        ``self.cm`` (no host synchronisation; :meth:`metrics` reads them)."""
+        ``self.cm`` (no host synchronisation; :meth:`metrics` reads them).  With fused evaluation
+        the counts come from the next round's training forward (or :meth:`metrics`' flush)."""
+        if self.fused_eval:
+            self._eval_pending = True
+            self.evaluated = True
+            return
+        self._evaluate_now()
+
+    def _evaluate_now(self) -> None:
+        self._eval_pending = False
         C = self.dims[-1]
         self._quantize()   # the GEMM operand copies of the post-step local weights
         self._local_quantized = True
@@ -451,6 +477,8 @@ class WideClient:
     def metrics(self) -> dict:
         """Accuracy / weighted precision, recall, F1 of the last :meth:`evaluate_shard`."""
         from .metrics import metrics_from_confusion
+        if self._eval_pending:  # nobody has run the forward that would score it: run it now
+            self._evaluate_now()
         self.stream.synchronize()
         C = self.dims[-1]
         return metrics_from_confusion(self.cm.cpu().numpy().reshape(C, C).astype(np.int64))
@@ -475,9 +503,10 @@ class WideClient:
 
     @property
     def flops_per_round(self) -> float:
-        """Training (forward + backward, 6 n MACs) plus the local evaluation forward (2 n MACs)."""
+        """FLOPs a round executes: training (forward + backward, 6 n MACs) plus the local
+        evaluation forward (2 n MACs) unless it is fused into the next round's training forward."""
         macs = sum(a * b for a, b in zip(self.dims[:-1], self.dims[1:]))
-        return (6.0 + (2.0 if self.evaluated else 0.0)) * self.n * macs
+        return (6.0 + (2.0 if self.evaluated and not self.fused_eval else 0.0)) * self.n * macs
 
 
 def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int, micro_batch: int = 131072,
@@ -573,6 +602,7 @@ def load_wide(path: str, client: WideClient) -> int:
         client.v_.copy_(torch.as_tensor(st["exp_avg_sq"], device=client.dev))
         if client.gprev is not None:
             client.gprev.copy_(client.params)
+    client._eval_pending = False  # (an evaluation of the replaced weights)
     client._quantize()
     client.stream.synchronize()
     client.round = int(meta["round"])

@@ -152,6 +152,31 @@ def test_wide_local_evaluation_whole_shard():
     assert abs(m["accuracy"] - acc) < 0.01, (m["accuracy"], acc)
 
 
+def test_wide_fused_evaluation_matches_separate_pass():
+    """One client: round r's evaluation scored from round r+1's training forward (fused_eval) gives
+    the very confusion counts of a separate evaluation pass after round r, and the training itself
+    is unchanged (bitwise); metrics() flushes the last round's pending evaluation."""
+    import torch
+    from fedmi.fl.wide import WideClient
+    dev = torch.device("cuda", 0)
+    X, y = _data(0, dev)
+    sep = WideClient(X, y, DIMS, micro_batch=512, dtype="bf16", fused_eval=False)
+    fus = WideClient(X, y, DIMS, micro_batch=512, dtype="bf16")
+    assert fus.fused_eval and not sep.fused_eval
+    cms = []
+    for r in range(4):
+        sep.run_round(evaluate=True)
+        sep.stream.synchronize()
+        cms.append(sep.cm.clone())
+        fus.run_round(evaluate=True)
+        fus.stream.synchronize()
+        assert torch.equal(fus.params, sep.params), r
+        if r > 0:  # round r's forward scored round r-1's post-step model
+            assert torch.equal(fus.cm, cms[r - 1]), r
+    assert fus.metrics() == sep.metrics()
+    assert torch.equal(fus.cm, cms[-1])
+
+
 @pytest.mark.parametrize("lr,tol", [(1e-4, 2e-3), (0.004, 3e-2)])
 def test_wide_full_width_matches_torch(lr, tol):
     """BASELINE config 3 at FULL width (14-4096-4096-4096-2, 2048 device-generated rows): three
