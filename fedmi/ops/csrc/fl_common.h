@@ -24,6 +24,16 @@
 // Dynamic LDS a fused-kernel workgroup may request: the CU's 160 KiB minus room for the
 // kernels' small static __shared__ objects (round state, counters).
 #define FL_LDS_DYNAMIC_MAX (160 * 1024 - 2048)
+// Threads of a fused-kernel workgroup (overridable for variant builds: -DFL_THREADS=...).
+#ifndef FL_THREADS
+#define FL_THREADS 1024
+#endif
+#define FL_WAVES (FL_THREADS / 64)
+// Lagged rounds scored in registers (fl_layout.h fl_lag_reg_ok): two waves per 16-row group
+// split the last hidden layer; the upper one hands at most FL_LAG_PARTS logits partials (C <= 4
+// classes) to the lower one through LDS.
+#define FL_LAG_PARTS 4
+#define FL_LAG_MAX_C 4
 
 // ldw = roundup16(K) + 4 (4 mod 8 floats): 16-byte aligned rows, and the 16 rows of a
 // 16-lane ds_read_b128 group land on 16 distinct 16-byte bank slots.
@@ -102,6 +112,7 @@ struct MLPDescB {
     int param_off;                    // start of the parameter region (all W_l hi, all b_l, all W_l lo):
     int param_bytes;                  // it is stored pre-packed in global memory and staged by a copy
     int lds_bytes;
+    int lag_reg;                      // 1: lagged rounds score in registers (fl_layout.h fl_lag_reg_ok)
 };
 
 // Packed bf16 W images (see the bank notes above): byte offset of row n (fl_wrow(kp rows) =

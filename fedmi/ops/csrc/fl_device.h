@@ -5,10 +5,6 @@
 #include "fl_common.h"
 #include <math.h>
 
-#ifndef FL_THREADS
-#define FL_THREADS 1024
-#endif
-#define FL_WAVES (FL_THREADS / 64)
 
 // In-kernel phase stamps (100 MHz s_memrealtime) for profiling; off unless b.dbg is set.
 #define FL_STAMP(i)                                                                            \

@@ -14,6 +14,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -151,6 +152,9 @@ class FLEngine {
             HIP_CHECK(fl_set_lds_limit((size_t)lds * 4));
         } else {
             fl_build_bf16_layout(d_, c_.R, &e_, &ev_);
+            // FEDMI_LAG_REG=0: lagged rounds score before the training pass instead of beside it (A/B)
+            const char* lreg_env = std::getenv("FEDMI_LAG_REG");
+            if (lreg_env != nullptr && lreg_env[0] == '0') e_.lag_reg = ev_.lag_reg = 0;
             const size_t need = (size_t)std::max(e_.lds_bytes, ev_.lds_bytes);
             if (need > FL_LDS_DYNAMIC_MAX)
                 throw std::runtime_error("FLEngine(bf16): model exceeds LDS; use a smaller R or the layered path");
@@ -503,6 +507,7 @@ class FLEngine {
         o["lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : e_.lds_bytes;
         o["bank_level"] = dtype_ == 0 ? -1 : e_.level;
         o["eval_lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : ev_.lds_bytes;
+        o["lag_reg"] = dtype_ == 1 && e_.lag_reg != 0;  // lagged rounds score in registers (fl_layout.h)
         o["eval_fedavg"] = peer_ != nullptr && !fused_ && eval_fedavg_fits();
         o["dtype"] = dtype_;
         o["slab_stride"] = c_.slab_stride;

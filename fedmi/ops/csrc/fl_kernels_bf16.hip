@@ -43,6 +43,13 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) { return bf16_
 __device__ __forceinline__ uint32_t lo_bits(float x) { return bf16_bits(x - bf16_to_f32((uint16_t)bf16_bits(x))); }
 __device__ __forceinline__ uint32_t pack_lo_bf16x2(float a, float b) { return lo_bits(a) | (lo_bits(b) << 16); }
 
+// two fp32 -> packed bf16 pair (a low, b high), round to nearest even: v_cvt_pk_bf16_f32
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+    const bf16x2_t v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
 __device__ __forceinline__ bf16x8 ld128(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group passes &M[r0+q][c0+4p]; lane i of the
@@ -121,7 +128,9 @@ __global__ void fl_pack_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDe
 // split: act_0 = bf16(x), alo_0 = bf16(x - bf16(x)).
 #define STAGE_P_UNROLL 8
 #define STAGE_X_UNROLL 2
-template <int RT>
+// NT: the staging threads (threads [0, NT); lagged rounds scored in registers leave the scoring
+// waves out, fwd_sync).
+template <int RT, int NT = FL_THREADS>
 __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const char* __restrict__ packed,
                                                        const float* __restrict__ X, int n_rows, int F, int row0,
                                                        char* lds) {
@@ -137,22 +146,23 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
     // last partial 1 KB is exec-masked (the head partials follow it in LDS)
 #pragma unroll
     for (int u = 0; u < STAGE_X_UNROLL; ++u) {
-        const int idx = threadIdx.x + u * FL_THREADS;
+        const int idx = threadIdx.x + u * NT;
         const int r = idx / kp, k = idx - r * kp;
         const int row = row0 + r;
-        const bool ok = idx < nx && row < n_rows && k < F;
+        const bool ok = idx < nx && row < n_rows && k < F && (NT == FL_THREADS || (int)threadIdx.x < NT);
         const float v = X[ok ? (size_t)row * F + k : 0];
         xv[u] = ok ? v : 0.f;
     }
     {
         const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-        for (int c0 = wv * 64; c0 < n16; c0 += FL_THREADS)
+        for (int c0 = wv * 64; c0 < n16 && (NT == FL_THREADS || wv < NT / 64); c0 += NT)
             if (c0 + ln < n16)
                 __builtin_amdgcn_global_load_lds(packed + (size_t)(c0 + ln) * 16,
                                                  (__attribute__((address_space(3))) void*)(lds + e.param_off + c0 * 16),
                                                  16, 0, 0);
     }
 #else
+    static_assert(NT == FL_THREADS, "FL_STAGE_VGPR stages with every thread");
     uint4 pv[STAGE_P_UNROLL];
     // unpredicated loads (clamped indices): a conditionally written register array is
     // demoted to scratch by the compiler
@@ -163,10 +173,10 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
     }
 #pragma unroll
     for (int u = 0; u < STAGE_X_UNROLL; ++u) {
-        const int idx = threadIdx.x + u * FL_THREADS;
+        const int idx = threadIdx.x + u * NT;
         const int r = idx / kp, k = idx - r * kp;
         const int row = row0 + r;
-        const bool ok = idx < nx && row < n_rows && k < F;
+        const bool ok = idx < nx && row < n_rows && k < F && (NT == FL_THREADS || (int)threadIdx.x < NT);
         const float v = X[ok ? (size_t)row * F + k : 0];
         xv[u] = ok ? v : 0.f;
     }
@@ -187,14 +197,15 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
     uint16_t* alo = reinterpret_cast<uint16_t*>(lds + e.alo_off[0]);
 #pragma unroll
     for (int u = 0; u < STAGE_X_UNROLL; ++u) {
-        const int idx = threadIdx.x + u * FL_THREADS;
-        if (idx < nx) {
+        const int idx = threadIdx.x + u * NT;
+        if (idx < nx && (NT == FL_THREADS || (int)threadIdx.x < NT)) {
             const int r = idx / kp, k = idx - r * kp;
             a[r * lda + k] = (uint16_t)bf16_bits(xv[u]);
             alo[r * lda + k] = (uint16_t)lo_bits(xv[u]);
         }
     }
-    for (int idx = threadIdx.x + STAGE_X_UNROLL * FL_THREADS; idx < nx; idx += FL_THREADS) {
+    for (int idx = threadIdx.x + STAGE_X_UNROLL * NT; idx < nx && (NT == FL_THREADS || (int)threadIdx.x < NT);
+         idx += NT) {
         const int r = idx / kp, k = idx - r * kp;
         const int row = row0 + r;
         const bool ok = row < n_rows && k < F;
@@ -243,7 +254,9 @@ __device__ __forceinline__ void params_store(const MLPDescB& e, const char* __re
 // z = act_l . W_l^T + b_l in split bf16 (fl_common.h): hi.hi in `acc`, the two cross terms in
 // `acl` (independent accumulation chains), z = acc + acl.  Hidden layers: ReLU -> act_{l+1}
 // hi / lo parts (all kp[l+1] columns, the padding comes out 0); last layer: fp32 logits [R][16].
-template <int RT>
+// NWV: waves that take the tiles (FL_WAVES; lagged rounds scored in registers: the first
+// FL_WAVES - 2 RT, fwd_sync).
+template <int RT, int NWV = FL_WAVES>
 __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
@@ -257,7 +270,8 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
     const float* bias = reinterpret_cast<const float*>(lds + e.bias_off[l]);
     const int wc = fl_fwd_col(lr);  // this lane's W row / output column within the tile
     const int wlane = 16 * (lg ^ fl_wswz(wc, e.wxor));  // its chunk of each k-step (swizzled)
-    for (int nt = wave; nt < ntiles; nt += FL_WAVES) {
+    for (int nt = wave; nt < ntiles; nt += NWV) {
+        if (NWV < FL_WAVES && wave >= NWV) break;
         const char* wrow = W + fl_wrow(nt * 16 + wc, e.ldw[l], e.wgap) + wlane;
         const int aoff = (lr * lda + 8 * lg) * 2;
         f32x4 acc[RT], acl[RT];
@@ -435,8 +449,23 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
 // product over k-steps [w*kper, (w+1)*kper) of the single 16-column tile and drops its C useful
 // columns into part[w][row][c]; after a barrier, thread (row, c) sums the G partials in order
 // and adds the bias.  (One wave's chain of kp/32 dependent steps was the longest forward phase.)
-template <int RT>
-__device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPDescB& e, char* lds) {
+// Forward-phase barrier.  PART (lagged rounds scored in registers): only the first
+// FL_WAVES - 2 RT waves run the forward pass, so they meet through an LDS arrival count (`tgt`
+// grows by their number per phase) while the last 2 RT waves score (score_rows_regs).
+template <int RT, bool PART>
+__device__ __forceinline__ void fwd_sync(int* cnt, int& tgt) {
+    if constexpr (PART) {
+        tgt += FL_WAVES - 2 * RT;
+        lds_count_arrive(cnt);
+        lds_count_wait(cnt, tgt);
+    } else {
+        lds_barrier();
+    }
+}
+
+template <int RT, bool PART = false>
+__device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, int* cnt,
+                                                    int& tgt) {
     const int l = d.L - 1, C = d.dim[d.L], G = e.head_split;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
@@ -479,7 +508,7 @@ __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPD
                 for (int j = 0; j < 4; ++j) part[(wave * RT * 16 + rt * 16 + 4 * lg + j) * C + wc] = acc[rt][j] + acl[rt][j];
         }
     }
-    lds_barrier();
+    fwd_sync<RT, PART>(cnt, tgt);
     const float* bias = reinterpret_cast<const float*>(lds + e.bias_off[l]);
     float* z = reinterpret_cast<float*>(lds + e.logit_off);
     for (int i = threadIdx.x; i < RT * 16 * C; i += FL_THREADS) {
@@ -490,24 +519,324 @@ __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPD
     }
 }
 
-template <int RT>
-__device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg) {
+template <int RT, bool PART = false>
+__device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg,
+                                                   int* cnt = nullptr) {
+    int tgt = 0;
     for (int l = 0; l < d.L; ++l) {
+#ifndef FL_LAG_STAMPS
         if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
-        if (l + 1 == d.L && e.head_split > 1) fwd_head_split_bf16<RT>(d, e, lds);
-        else fwd_layer_bf16<RT>(d, e, l, lds);
-        lds_barrier();
+#endif
+        if (l + 1 == d.L && e.head_split > 1) fwd_head_split_bf16<RT, PART>(d, e, lds, cnt, tgt);
+        else fwd_layer_bf16<RT, PART ? FL_WAVES - 2 * RT : FL_WAVES>(d, e, l, lds);
+        fwd_sync<RT, PART>(cnt, tgt);
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// Register-resident scoring pass (FL_EVAL_LAGGED, several clients; fl_layout.h fl_lag_reg_ok)
+// ---------------------------------------------------------------------------------------
+// One wave scores 16 rows with the previous round's local model read straight from its packed
+// global image (b.pk_local, L2-resident: every workgroup reads the same ~105 KB), so the LDS
+// parameter region keeps the round's own weights and the scoring runs on the waves the
+// training forward pass leaves idle, beside it instead of before it.  The product is computed
+// transposed, Z^T = W . H^T: A = 16 W rows (global), B = the rows' activations, and the
+// accumulator of a 16-feature tile -- lane (r, g) holds features 4g..4g+3 of row r -- becomes
+// the next layer's B operand (lane (r, g): features 8g..8g+7 of a 32-deep k-block) after two
+// lane swaps per tile pair (pair_to_b).  Every product sits at the same k position of the same
+// v_mfma_f32_16x16x32_bf16 as in fwd_layer_bf16 / fwd_head_split_bf16 (only the roles of the
+// A and B operands are exchanged), the split-bf16 chains and the bias / ReLU / hi-lo rounding
+// are the same, and the logits' K-split partials are summed in the same order: the logits,
+// hence the argmax counts, equal the evaluation kernel's (tests/test_peer_allreduce.py compares
+// lagged rounds with classic ones bitwise).
+// Profiling builds only (-DFL_LAG_STAMPS, tools/stamps.py): a stamp of the last scoring wave
+// taken once `dep` (a value of the stage being timed) is available.
+__device__ __forceinline__ void lag_stamp(const FLBuffers& b, int slot, uint32_t dep, bool on) {
+#ifdef FL_LAG_STAMPS
+    const uint32_t sdep = __builtin_amdgcn_readfirstlane(dep);
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "s"(sdep));
+    if (on && b.dbg != nullptr && (threadIdx.x & 63) == 0) b.dbg[blockIdx.x * 16 + slot] = t;
+#endif
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// timing experiments only (-DFL_LAG_EXP=1: every hidden tile re-reads tile 0's weights, an L1-hot
+// address -- wrong logits, for stamps)
+#if defined(FL_LAG_EXP) && FL_LAG_EXP == 1
+#define LAG_EXP_T(t) 0
+#else
+#define LAG_EXP_T(t) (t)
+#endif
+struct TileBits {  // one transposed tile after bias + ReLU: hi / lo bf16 pairs of features 4g..4g+3
+    uint32_t h0, h1, l0, l1;
+};
+
+// W_l rows nt*16 + m, k-block ks (A operand of the transposed product), hi and lo images.
+__device__ __forceinline__ void score_ldw(const MLPDescB& e, const char* __restrict__ pk, int l, int nt, int ks, int m,
+                                          int g, bf16x8& wh, bf16x8& wl) {
+    const int n = nt * 16 + m;
+    const char* p = pk + (e.w_off[l] - e.param_off) + fl_wrow(n, e.ldw[l], e.wgap) + 16 * (g ^ fl_wswz(n, e.wxor)) +
+                    ks * 64;
+    wh = *reinterpret_cast<const bf16x8*>(p);
+    wl = *reinterpret_cast<const bf16x8*>(p + e.wlo_delta);
+}
+__device__ __forceinline__ f32x4 score_ldb(const MLPDescB& e, const char* __restrict__ pk, int l, int nt, int g) {
+    return *reinterpret_cast<const f32x4*>(pk + (e.bias_off[l] - e.param_off) + (nt * 16 + 4 * g) * 4);
+}
+
+// One hidden-layer tile: split-bf16 chains in fwd_layer_bf16's order, z + b, ReLU, hi / lo.
+template <int KB>
+__device__ __forceinline__ TileBits score_tile(const bf16x8 (&wh)[KB], const bf16x8 (&wl)[KB], const bf16x8 (&bh)[KB],
+                                               const bf16x8 (&bl)[KB], int nkb, f32x4 bias) {
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f}, acl = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {  // nkb == KB (callers instantiate the exact count)
+        acc = mfma32(wh[kb], bh[kb], acc);
+        acl = mfma32(wh[kb], bl[kb], acl);
+        acl = mfma32(wl[kb], bh[kb], acl);
+    }
+    float v[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = fmaxf((acc[t] + acl[t]) + bias[t], 0.f);
+    // hi / lo parts with the hardware round-to-nearest-even conversion (v_cvt_pk_bf16_f32: the
+    // bits of bf16_bits / lo_bits for finite values, a quarter of their VALU work)
+    const uint32_t h01 = cvt_pk_bf16(v[0], v[1]), h23 = cvt_pk_bf16(v[2], v[3]);
+    return TileBits{h01, h23, cvt_pk_bf16(v[0] - __uint_as_float(h01 << 16), v[1] - __uint_as_float(h01 & 0xffff0000u)),
+                    cvt_pk_bf16(v[2] - __uint_as_float(h23 << 16), v[3] - __uint_as_float(h23 & 0xffff0000u))};
+}
+
+// Tiles 2kb, 2kb+1 (lane groups a_g, b_g) -> B operand of k-block kb.  Lane group g needs
+// features 8g..8g+7 of the block: a_{2g}, a_{2g+1} for g < 2, b_{2g-4}, b_{2g-3} after.
+// permlane32_swap(x, y) swaps x's upper half with y's lower half: x = [a0 a1 b0 b1],
+// y = [a2 a3 b2 b3]; permlane16_swap then swaps x's odd rows with y's even rows:
+// x = [a0 a2 b0 b2] (first 4 features of each group's 8), y = [a1 a3 b1 b3] (last 4).
+__device__ __forceinline__ void pair_to_b(const TileBits& a, const TileBits& b, bf16x8& bh, bf16x8& bl) {
+    const uint32_t xa[4] = {a.h0, a.h1, a.l0, a.l1}, xb[4] = {b.h0, b.h1, b.l0, b.l1};
+    uint32_t f[4], s[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const auto r1 = __builtin_amdgcn_permlane32_swap(xa[i], xb[i], false, false);
+        const auto r2 = __builtin_amdgcn_permlane16_swap(r1[0], r1[1], false, false);
+        f[i] = r2[0];
+        s[i] = r2[1];
+    }
+    bh = __builtin_bit_cast(bf16x8, (u32x4){f[0], f[1], s[0], s[1]});
+    bl = __builtin_bit_cast(bf16x8, (u32x4){f[2], f[3], s[2], s[3]});
+}
+
+// The last hidden layer l (input B operand bh/bl, nkb k-blocks) streamed into the logits
+// layer: each tile pair is one k-block of the logits' product, accumulated in the K-split
+// parts of fwd_head_split_bf16 (part w = k-blocks [w*kper, (w+1)*kper), z = ((p_0 + p_1) + ...)
+// + b; head_split 1 = fwd_layer_bf16's single chain).  Two waves share a 16-row group: `half` 0
+// takes parts [0, wA) (wA = ceil(G/2)) and their k-blocks, half 1 the rest; half 1 stores its
+// parts in `parts` (LDS, lane group 0 = classes 0..3) and counts itself in `ready`, half 0 adds
+// them to its own running sum in part order -- the same additions in the same order as one
+// wave (or fwd_head_split_bf16's partial sum) -- and returns the logits of lane (r, g): classes
+// 4g..4g+3 of row r (half 1 returns nothing useful).  W tiles and biases are prefetched one
+// tile ahead.
+template <int KB>
+__device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDescB& e, const char* __restrict__ pk,
+                                                   int l, const bf16x8 (&bh)[KB], const bf16x8 (&bl)[KB], int nkb,
+                                                   int m, int g, int half, f32x4* parts, int* ready,
+                                                   const FLBuffers& b, bool last) {
+    const int lh = d.L - 1;
+    const int ntiles = e.kp[l + 1] >> 4, ksteps = ntiles >> 1;
+    const int G = e.head_split, kper = (ksteps + G - 1) / G;
+    const int wA = (G + 1) >> 1, KA = min(ksteps, kper * wA);
+    const int ks0 = half ? KA : 0, ks1 = half ? ksteps : KA;
+    // buffer loads: the per-lane part of every address (W row m of a tile, its swizzled chunk g,
+    // the bias entries of lane group g) is fixed, the tile / k-block part scalar -- no address
+    // arithmetic per load
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pk), (short)0,
+                                                                      e.param_bytes, 0x00020000);
+    const int vw = m * e.ldw[l] * 2 + (m >> 3) * e.wgap + 16 * (g ^ fl_wswz(m, e.wxor));
+    const int vh = m * e.ldw[lh] * 2 + (m >> 3) * e.wgap + 16 * (g ^ fl_wswz(m, e.wxor));
+    const int vb = 16 * g;
+    const int sw0 = e.w_off[l] - e.param_off, tstride = 32 * e.ldw[l] + 2 * e.wgap;
+    const int sh0 = e.w_off[lh] - e.param_off, sb0 = e.bias_off[l] - e.param_off;
+    auto ldw_t = [&](int nt, int kb, bf16x8& wh, bf16x8& wl) {
+        const int so = sw0 + nt * tstride + kb * 64;
+        wh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, vw, so, 0));
+        wl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, vw, so + e.wlo_delta, 0));
+    };
+    auto ldb_t = [&](int nt) {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vb, sb0 + nt * 64, 0));
+    };
+    auto ldh = [&](int ks, bf16x8& wh, bf16x8& wl) {
+        wh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, vh, sh0 + ks * 64, 0));
+        wl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, vh, sh0 + ks * 64 + e.wlo_delta, 0));
+    };
+    // two register sets, tile 2p from A while tile 2p+1 loads into B and the reverse: no
+    // register copy of an in-flight load (a copy makes the compiler drain every load first)
+    bf16x8 ah[KB], al[KB], bh2[KB], bl2[KB];
+    const int tA = min(2 * ks0, ntiles - 1);
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) ldw_t(tA, kb, ah[kb], al[kb]);
+    f32x4 abias = ldb_t(tA), bbias;
+    bf16x8 hh, hl;
+    ldh(min(ks0, ksteps - 1), hh, hl);
+    const f32x4 hb = score_ldb(e, pk, lh, 0, g);
+    const f32x4 zero = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = zero, acl = zero, s = zero;
+    int w = half ? wA : 0, kend = min(ksteps, (w + 1) * kper);
+    for (int ks = ks0; ks < ks1; ++ks) {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) ldw_t(LAG_EXP_T(2 * ks + 1), kb, bh2[kb], bl2[kb]);
+        bbias = ldb_t(LAG_EXP_T(2 * ks + 1));
+        const TileBits t0 = score_tile<KB>(ah, al, bh, bl, nkb, abias);
+        int nx = min(2 * ks + 2, ntiles - 1);
+        // set A reloads after tile 2ks consumed all of it (no register copy)
+        asm volatile("" : "+s"(nx) : "v"(t0.h0), "v"(t0.h1), "v"(t0.l0), "v"(t0.l1));
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) ldw_t(LAG_EXP_T(nx), kb, ah[kb], al[kb]);
+        abias = ldb_t(LAG_EXP_T(nx));
+        const TileBits t1 = score_tile<KB>(bh2, bl2, bh, bl, nkb, bbias);
+#ifdef FL_LAG_STAMPS
+        if (ks == 1) lag_stamp(b, 12, t1.h0, last);
+#endif
+        bf16x8 xh, xl;
+        pair_to_b(t0, t1, xh, xl);
+        acc = mfma32(hh, xh, acc);
+        acl = mfma32(hh, xl, acl);
+        acl = mfma32(hl, xh, acl);
+        if (ks + 1 < ks1) ldh(ks + 1, hh, hl);
+        if (ks + 1 == kend) {  // part w complete
+            const f32x4 p = acc + acl;
+            if (half == 0) s = (w == 0) ? p : s + p;
+            else if (g == 0) parts[(w - wA) * 16 + m] = p;
+            acc = zero;
+            acl = zero;
+            ++w;
+            kend = min(ksteps, (w + 1) * kper);
+        }
+    }
+    // empty trailing parts (0 + 0), as fwd_head_split_bf16 sums them
+    if (half == 0) {
+        for (; w < wA; ++w) s = s + (acc + acl);
+        lds_count_wait(ready, 1);
+        for (w = wA; w < G; ++w) s = s + parts[(w - wA) * 16 + m];
+    } else {
+        for (; w < G; ++w)
+            if (g == 0) parts[(w - wA) * 16 + m] = acc + acl;
+        lds_count_arrive(ready);
+    }
+    return s + hb;
+}
+
+// Input side of a scoring wave `sw` (2 per 16-row group; rows row0 + 16 (sw / 2) + (0..15)),
+// run while the other waves stage the round's weights: the rows straight from global memory
+// (the staging's bf16 hi / lo conversion: the B operand of the transposed product), and with two
+// hidden layers the first one (<= 4 tiles, every load issued first; both waves of the group)
+// -> `in` = the B operand of the last hidden layer (nkb k-blocks).
+struct ScoreIn {
+    bf16x8 h[2], l[2];
+};
+template <int RT>
+__device__ __forceinline__ void score_in(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
+                                         int sw, int row0, ScoreIn& in) {
+    const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+    const int swu = __builtin_amdgcn_readfirstlane(sw);
+    const char* __restrict__ pk = b.pk_local;
+    const int F = d.dim[0], row = row0 + 16 * (swu >> 1) + r;
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        const bool ok = row < c.n_rows && k < F;
+        const float v = b.X[ok ? (size_t)row * F + k : 0];
+        xv[j] = ok ? v : 0.f;
+    }
+    const bool last = swu == 0;
+    if (d.L == 2) {
+        uint32_t hv[4], lv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            hv[j] = cvt_pk_bf16(xv[2 * j], xv[2 * j + 1]);
+            lv[j] = cvt_pk_bf16(xv[2 * j] - __uint_as_float(hv[j] << 16), xv[2 * j + 1] - __uint_as_float(hv[j] & 0xffff0000u));
+        }
+        in.h[0] = __builtin_bit_cast(bf16x8, (u32x4){hv[0], hv[1], hv[2], hv[3]});
+        in.l[0] = __builtin_bit_cast(bf16x8, (u32x4){lv[0], lv[1], lv[2], lv[3]});
+        return;
+    }
+    const int nt0 = e.kp[1] >> 4;
+    bf16x8 w0h[4][1], w0l[4][1];
+    f32x4 b0[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int t = nt < nt0 ? nt : 0;
+        score_ldw(e, pk, 0, t, 0, r, g, w0h[nt][0], w0l[nt][0]);
+        b0[nt] = score_ldb(e, pk, 0, t, g);
+    }
+    bf16x8 xh[1], xl[1];
+    {
+        uint32_t hv[4], lv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            hv[j] = cvt_pk_bf16(xv[2 * j], xv[2 * j + 1]);
+            lv[j] = cvt_pk_bf16(xv[2 * j] - __uint_as_float(hv[j] << 16), xv[2 * j + 1] - __uint_as_float(hv[j] & 0xffff0000u));
+        }
+        xh[0] = __builtin_bit_cast(bf16x8, (u32x4){hv[0], hv[1], hv[2], hv[3]});
+        xl[0] = __builtin_bit_cast(bf16x8, (u32x4){lv[0], lv[1], lv[2], lv[3]});
+    }
+    lag_stamp(b, 7, (uint32_t)xh[0][0], last);
+    lag_stamp(b, 10, (uint32_t)w0h[0][0][0], last);
+    TileBits t0[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+        if (nt < nt0) t0[nt] = score_tile<1>(w0h[nt], w0l[nt], xh, xl, 1, b0[nt]);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+        if (2 * kb < nt0) pair_to_b(t0[2 * kb], t0[2 * kb + 1], in.h[kb], in.l[kb]);
+    lag_stamp(b, 11, t0[0].h0, last);
+}
+
+// Output side, after the staging barrier: the last hidden layer + logits (score_hidden_head,
+// the group's two waves splitting it), argmax -> cm_s (LDS ints) by the group's half-0 wave;
+// ysc = the label of row r (lane r + 16 g).
+template <int RT>
+__device__ void score_out(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b, int* cm_s,
+                          int sw, int row0, int ysc, const ScoreIn& in, f32x4* parts, int* ready) {
+    const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+    const int swu = __builtin_amdgcn_readfirstlane(sw);  // wave-uniform: scalar tile indices
+    const int half = swu & 1;
+    const char* __restrict__ pk = b.pk_local;
+    const int C = d.dim[d.L];
+    const int row = row0 + 16 * (swu >> 1) + r;
+    const bool last = swu == 0;
+    if (b.dbg != nullptr && lane == 0 && last) b.dbg[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    f32x4 z;
+    if (d.L == 2) {
+        const bf16x8 xh[1] = {in.h[0]}, xl[1] = {in.l[0]};
+        z = score_hidden_head<1>(d, e, pk, 0, xh, xl, 1, r, g, half, parts, ready, b, last);
+    } else {
+        if ((e.kp[1] >> 5) == 2) {
+            z = score_hidden_head<2>(d, e, pk, 1, in.h, in.l, 2, r, g, half, parts, ready, b, last);
+        } else {
+            const bf16x8 xh[1] = {in.h[0]}, xl[1] = {in.l[0]};
+            z = score_hidden_head<1>(d, e, pk, 1, xh, xl, 1, r, g, half, parts, ready, b, last);
+        }
+    }
+    // stamps (tools/stamps.py): 13 = the first scoring wave past the staging barrier, 14 = its logits done
+    if (b.dbg != nullptr && lane == 0 && last) b.dbg[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+    // argmax over the C <= 4 classes of row r (torch.max: first maximum): lane group 0
+    int best = 0;
+    float bv = z[0];
+#pragma unroll
+    for (int k = 1; k < FL_LAG_MAX_C; ++k)
+        if (k < C && z[k] > bv) { bv = z[k]; best = k; }
+    if (half == 0 && g == 0 && row < c.n_rows) atomicAdd(&cm_s[ysc * C + best], 1);
 }
 
 // ---------------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------------
 // Kernel body shared by the single-engine and trial-batch entry points (fl_train_bf16_body.inc).
-// LAG: the lagged scoring pass (FL_EVAL_LAGGED, several clients) is compiled in; the other
-// modes get an instantiation without it -- its register copy of the round's weights stays out
-// of the forward pass (R = 32: 90 instead of 126 VGPRs; R = 64 spill-free).
-template <int RT, bool LAG>
+// LAG: the lagged scoring pass (FL_EVAL_LAGGED, several clients) is compiled in -- 1: before
+// the training pass (its register copy of the round's weights: R = 32 126 VGPRs), 2: in
+// registers on the last 2 RT waves (score_rows_regs, shapes of fl_lag_reg_ok); the other modes get
+// an instantiation without it (R = 32: 90 VGPRs; R = 64 spill-free).
+template <int RT, int LAG>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                      const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
@@ -519,7 +848,7 @@ template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel pg_sel, FLSel si_sel,
                            FLSel so_sel, int local_step, int stage_local, int mode, FLSel cm_sel, int fold_mask) {
-    constexpr bool LAG = false;  // trial batches never run lagged rounds
+    constexpr int LAG = 0;  // trial batches never run lagged rounds
     const FLTrialDesc& t = T[blockIdx.y];
     const FLConfig c = t.c;
     const FLBuffers b = t.b;
@@ -623,10 +952,11 @@ hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLCon
 #define FLB_TRAIN(RT_, LAG_)                                                                                \
     hipLaunchKernelGGL((fl_train_bf16_kernel<RT_, LAG_>), dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, \
                        si, so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask)
+    const bool lreg = lag && e.lag_reg;
     switch (c.R) {
-        case 16: if (lag) FLB_TRAIN(1, true); else FLB_TRAIN(1, false); break;
-        case 32: if (lag) FLB_TRAIN(2, true); else FLB_TRAIN(2, false); break;
-        case 64: if (lag) FLB_TRAIN(4, true); else FLB_TRAIN(4, false); break;
+        case 16: if (lreg) FLB_TRAIN(1, 2); else if (lag) FLB_TRAIN(1, 1); else FLB_TRAIN(1, 0); break;
+        case 32: if (lreg) FLB_TRAIN(2, 2); else if (lag) FLB_TRAIN(2, 1); else FLB_TRAIN(2, 0); break;
+        case 64: if (lag) FLB_TRAIN(4, 1); else FLB_TRAIN(4, 0); break;
         default: return hipErrorInvalidValue;
     }
 #undef FLB_TRAIN
@@ -746,10 +1076,11 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
 #define FLB_SET(fn)                                                                                     \
     if (r == hipSuccess)                                                                                \
     r = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, v)
-    FLB_SET((fl_train_bf16_kernel<1, false>)); FLB_SET((fl_train_bf16_kernel<2, false>));
-    FLB_SET((fl_train_bf16_kernel<4, false>));
-    FLB_SET((fl_train_bf16_kernel<1, true>)); FLB_SET((fl_train_bf16_kernel<2, true>));
-    FLB_SET((fl_train_bf16_kernel<4, true>));
+    FLB_SET((fl_train_bf16_kernel<1, 0>)); FLB_SET((fl_train_bf16_kernel<2, 0>));
+    FLB_SET((fl_train_bf16_kernel<4, 0>));
+    FLB_SET((fl_train_bf16_kernel<1, 1>)); FLB_SET((fl_train_bf16_kernel<2, 1>));
+    FLB_SET((fl_train_bf16_kernel<4, 1>));
+    FLB_SET((fl_train_bf16_kernel<1, 2>)); FLB_SET((fl_train_bf16_kernel<2, 2>));
     FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>); FLB_SET(fl_eval_bf16_kernel<4>);
     FLB_SET(fl_train_bf16_batch_kernel<1>); FLB_SET(fl_train_bf16_batch_kernel<2>);
     FLB_SET(fl_train_bf16_batch_kernel<4>);

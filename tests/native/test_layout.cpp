@@ -378,12 +378,43 @@ static void check_fp32(const MLPDesc& d, int R) {
     CHECK(d.act_off[L] + R * d.ld[L] <= d.cm_off, "activations overlap the counters");
 }
 
+// Register-resident scoring (fl_kernels_bf16.hip score_rows_regs): every forward phase of the
+// training waves stays on waves [0, nw), and every global read of the scoring waves lies inside
+// the packed parameter image (W rows < kp[l+1], k-blocks < kp[l] / 32, logits rows < 16,
+// bias entries < kp[l+1]) and inside their register arrays (layer-0 input 1 k-block, the stored
+// first hidden layer <= 2 k-blocks, <= 4 tiles).
+static void check_lag_reg(const MLPDesc& d, const MLPDescB& e, int R) {
+    const int L = d.L, C = d.dim[L], nw = FL_WAVES - 2 * (R / 16);
+    for (int l = 0; l + 1 < L; ++l)  // fwd_layer_bf16<RT, nw>: tile nt on wave nt % nw
+        for (int nt = 0; nt < (e.kp[l + 1] >> 4); ++nt) CHECK(nt % nw < nw, "lag_reg: layer %d tile %d on a scoring wave", l, nt);
+    CHECK(e.head_split <= nw && R * C <= nw * 64 && ((C + 15) >> 4) <= nw, "lag_reg: logits phase on a scoring wave");
+    const int G = e.head_split;
+    CHECK(C <= FL_LAG_MAX_C && G - (G + 1) / 2 <= FL_LAG_PARTS, "lag_reg: C %d, logits split %d", C, G);
+    CHECK(e.lds_bytes + fl_lag_reg_static_bytes(R) + 256 <= 160 * 1024, "lag_reg: LDS %d", e.lds_bytes);
+    CHECK(L == 2 || L == 3, "lag_reg: %d layers", L);
+    CHECK(e.kp[0] / 32 == 1, "lag_reg: input k-blocks %d", e.kp[0] / 32);
+    if (L == 3) CHECK((e.kp[1] >> 4) <= 4 && (e.kp[1] >> 5) <= 2, "lag_reg: stored hidden layer %d", e.kp[1]);
+    const int image = e.param_bytes;
+    for (int l = 0; l < L; ++l) {
+        const int rows = (l + 1 == L) ? 16 : e.kp[l + 1];
+        CHECK(rows <= e.kp[l + 1], "lag_reg: layer %d rows", l);
+        for (int n = 0; n < rows; ++n)
+            for (int ks = 0; ks < (e.kp[l] >> 5); ++ks)
+                for (int g = 0; g < 4; ++g) {
+                    const int off = e.w_off[l] - e.param_off + fl_wrow(n, e.ldw[l], e.wgap) + 16 * (g ^ fl_wswz(n, e.wxor)) + ks * 64;
+                    CHECK(off >= 0 && off + 16 + e.wlo_delta <= image && off % 16 == 0, "lag_reg: W%d read %d", l, off);
+                }
+        const int bend = e.bias_off[l] - e.param_off + ((rows + 15) & ~15) * 4;
+        CHECK(bend <= image && (e.bias_off[l] - e.param_off) % 16 == 0, "lag_reg: bias %d", l);
+    }
+}
+
 int main() {
     const std::vector<std::vector<int>> hidden = {{7}, {50, 200}, {33, 17, 9}, {100, 50}, {64, 64, 64}, {24, 12}};
     const int feats[] = {5, 14, 31, 33};
     const int classes[] = {2, 3, 10, 16};
     const int Rs[] = {16, 32, 64};
-    int checked = 0, skipped = 0, levels[3] = {0, 0, 0};
+    int checked = 0, skipped = 0, lagreg = 0, levels[3] = {0, 0, 0};
     for (const auto& h : hidden)
         for (int F : feats)
             for (int C : classes)
@@ -403,6 +434,7 @@ int main() {
                     check_bf16(d, ev, R, false);
                     check_packing(d, e);
                     CHECK(e.head_split == ev.head_split, "train / eval logits split differ");
+                    if (e.lag_reg) { check_lag_reg(d, e, R); ++lagreg; }
                     // operand reads: conflict free at level 2; level 1 leaves dgrad's transposed W
                     // reads 2-way (fl_common.h)
                     const BankStats bs = bank_conflicts_bf16(d, e, R);
@@ -415,8 +447,8 @@ int main() {
                     ++levels[e.level];
                     ++checked;
                 }
-    std::printf("layouts checked: %d (bank levels 0/1/2: %d/%d/%d; skipped as too large for LDS: %d), failures: %d\n",
-                checked, levels[0], levels[1], levels[2], skipped, g_fail);
+    std::printf("layouts checked: %d (bank levels 0/1/2: %d/%d/%d; skipped as too large for LDS: %d; register scoring: "
+                "%d), failures: %d\n", checked, levels[0], levels[1], levels[2], skipped, lagreg, g_fail);
     // the flagship (BASELINE config 2) shape at R = 32
     {
         const int dims[] = {14, 50, 200, 2};
@@ -428,6 +460,7 @@ int main() {
         std::printf("14-50-200-2 R 32: level %d, lds %d / %d bytes, head split %d, extra LDS cycles act %ld W fwd %ld "
                     "W dgrad %ld stores %ld\n", e.level, e.lds_bytes, ev.lds_bytes, e.head_split, bs.act, bs.wfwd, bs.wdgrad, bs.st);
         CHECK(e.level >= 1 && std::max(e.lds_bytes, ev.lds_bytes) <= (int)FL_LDS_DYNAMIC_MAX, "flagship layout");
+        CHECK(e.lag_reg == 1, "flagship layout: lagged rounds score in registers");
     }
     return g_fail ? 1 : 0;
 }

@@ -40,6 +40,18 @@ for which, name in kinds:
         cyc = st[:, 14] - st[:, 13]
         real = (st[:, 2] - st[:, 0]) * 10e-9
         print(f"   effective shader clock over start..forward: {np.median(cyc / real) / 1e9:.2f} GHz")
+    if which == 3 and (st[:, 14] > 0).all():  # register scoring (score_in / score_out)
+        fine = ((7, "scoring: rows loaded"), (10, "scoring: first W tile in"), (11, "scoring: first hidden layer"))
+        for c, what in fine:
+            if (st[:, c] > 0).all():
+                d = (st[:, c] - st[:, 0]) * 10 / 1000
+                print(f"   {what:28s} 0->{c}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
+        for c, what in ((13, "scoring: past staging"), (12, "scoring: 2 tile pairs"), (14, "scoring: logits")):
+            if (st[:, c] > 0).all():
+                d = (st[:, c] - st[:, 1]) * 10 / 1000
+                print(f"   {what:28s} 1->{c}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
+        d = (st[:, 2] - st[:, 1]) * 10 / 1000
+        print(f"   {'training forward':28s} 1->2: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
     cols = [i for i in order if (st[:, i] > 0).all()]
     prev = cols[0]
     for c in cols[1:]:
