@@ -724,39 +724,30 @@ __device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDe
     return s + hb;
 }
 
-// Input side of a scoring wave `sw` (2 per 16-row group; rows row0 + 16 (sw / 2) + (0..15)),
-// run while the other waves stage the round's weights: the rows straight from global memory
-// (the staging's bf16 hi / lo conversion: the B operand of the transposed product), and with two
-// hidden layers the first one (<= 4 tiles, every load issued first; both waves of the group)
-// -> `in` = the B operand of the last hidden layer (nkb k-blocks).
 struct ScoreIn {
     bf16x8 h[2], l[2];
 };
+
+// Input side of a scoring wave `sw` (2 per 16-row group; rows row0 + 16 (sw / 2) + (0..15)), after
+// the staging barrier: the staged rows (act_0 / alo_0, the B operand of the transposed product),
+// and with two hidden layers the first one (<= 4 tiles, every load issued first; both waves of
+// the group) -> `in` = the B operand of the last hidden layer.  (Tried: the rows from global
+// memory and the first layer before the staging barrier, with or without a first touch of every
+// line of the local image -- the loads queue behind the staging's and delay the barrier;
+// profiles/lag_reg_ab_r3.log.)
 template <int RT>
-__device__ __forceinline__ void score_in(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
-                                         int sw, int row0, ScoreIn& in) {
+__device__ __forceinline__ void score_in_lds(const MLPDesc& d, const MLPDescB& e, const FLBuffers& b, const char* lds,
+                                             int sw, ScoreIn& in) {
     const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
     const int swu = __builtin_amdgcn_readfirstlane(sw);
     const char* __restrict__ pk = b.pk_local;
-    const int F = d.dim[0], row = row0 + 16 * (swu >> 1) + r;
-    float xv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j;
-        const bool ok = row < c.n_rows && k < F;
-        const float v = b.X[ok ? (size_t)row * F + k : 0];
-        xv[j] = ok ? v : 0.f;
-    }
-    const bool last = swu == 0;
+    const int xo = ((16 * (swu >> 1) + r) * e.lda[0] + 8 * g) * 2;
+    bf16x8 xh[1], xl[1];
+    xh[0] = ld128(lds + e.act_off[0] + xo);
+    xl[0] = ld128(lds + e.alo_off[0] + xo);
     if (d.L == 2) {
-        uint32_t hv[4], lv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            hv[j] = cvt_pk_bf16(xv[2 * j], xv[2 * j + 1]);
-            lv[j] = cvt_pk_bf16(xv[2 * j] - __uint_as_float(hv[j] << 16), xv[2 * j + 1] - __uint_as_float(hv[j] & 0xffff0000u));
-        }
-        in.h[0] = __builtin_bit_cast(bf16x8, (u32x4){hv[0], hv[1], hv[2], hv[3]});
-        in.l[0] = __builtin_bit_cast(bf16x8, (u32x4){lv[0], lv[1], lv[2], lv[3]});
+        in.h[0] = xh[0];
+        in.l[0] = xl[0];
         return;
     }
     const int nt0 = e.kp[1] >> 4;
@@ -768,19 +759,6 @@ __device__ __forceinline__ void score_in(const MLPDesc& d, const MLPDescB& e, co
         score_ldw(e, pk, 0, t, 0, r, g, w0h[nt][0], w0l[nt][0]);
         b0[nt] = score_ldb(e, pk, 0, t, g);
     }
-    bf16x8 xh[1], xl[1];
-    {
-        uint32_t hv[4], lv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            hv[j] = cvt_pk_bf16(xv[2 * j], xv[2 * j + 1]);
-            lv[j] = cvt_pk_bf16(xv[2 * j] - __uint_as_float(hv[j] << 16), xv[2 * j + 1] - __uint_as_float(hv[j] & 0xffff0000u));
-        }
-        xh[0] = __builtin_bit_cast(bf16x8, (u32x4){hv[0], hv[1], hv[2], hv[3]});
-        xl[0] = __builtin_bit_cast(bf16x8, (u32x4){lv[0], lv[1], lv[2], lv[3]});
-    }
-    lag_stamp(b, 7, (uint32_t)xh[0][0], last);
-    lag_stamp(b, 10, (uint32_t)w0h[0][0][0], last);
     TileBits t0[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
@@ -788,7 +766,7 @@ __device__ __forceinline__ void score_in(const MLPDesc& d, const MLPDescB& e, co
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
         if (2 * kb < nt0) pair_to_b(t0[2 * kb], t0[2 * kb + 1], in.h[kb], in.l[kb]);
-    lag_stamp(b, 11, t0[0].h0, last);
+    lag_stamp(b, 11, t0[0].h0, swu == 0);
 }
 
 // Output side, after the staging barrier: the last hidden layer + logits (score_hidden_head,
