@@ -147,6 +147,9 @@ struct FLConfig {
     int tail_stride;    // C*C confusion counts + 1 loss slot
     int tail_len;       // world * tail_stride
     int lag_off;        // > 0: start of the lag region A (tail_len floats, FL_EVAL_LAGGED)
+    int plain_fwd;      // bf16, several clients, register scoring: the TRAINING forward pass is plain
+                        // bf16 (a_hi.W_hi) and stages only the hi images -- every scoring pass is a
+                        // separate split-bf16 forward there (fl_kernels_bf16.hip)
     int local_steps;    // optimizer steps per round (reference: 1 full-batch step, C:63-73)
     // optimizer (torch.optim.Adam + StepLR, C:44-46); scalars kept in double like torch
     double lr0;
@@ -332,7 +335,7 @@ hipError_t fl_launch_train_batch(const MLPDesc& d, int R, int n_slabs, const FLT
                                  FLSel si, FLSel so, int ls, int mode, FLSel cm, int fold_mask, hipStream_t s);
 hipError_t fl_launch_train_bf16_batch(const MLPDesc& d, const MLPDescB& e, int R, int n_slabs, const FLTrialDesc* T,
                                       int K, FLSel pg, FLSel si, FLSel so, int ls, int stage_local, int mode, FLSel cm,
-                                      int fold_mask, hipStream_t s);
+                                      int fold_mask, hipStream_t s, int plain = 0);
 hipError_t fl_launch_adam_batch(const MLPDesc& d, const MLPDescB* e, const FLTrialDesc* T, int K, FLSel pin,
                                 FLSel anchor, FLSel comm, FLSel st, int local_step, FLSel st_out, int fold, int tail_a,
                                 int fold_mask, hipStream_t s);

@@ -209,6 +209,14 @@ class FLEngine {
         // kernel, which then also exchanges and folds the metrics in time: see lagged())
         // (the lagged train kernel scores the previous local model in the train layout itself)
         lag_ok_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !fused_;
+        // several clients + register scoring: the training forward pass is plain bf16 (no round
+        // scores from it), in every round kind of the engine alike (lagged, classic, step API);
+        // FEDMI_PLAIN_FWD=0 keeps the split forward (A/B)
+        {
+            const char* pf = std::getenv("FEDMI_PLAIN_FWD");
+            c_.plain_fwd = (dtype_ == 1 && (c_.world > 1 || emulate) && e_.lag_reg && !fused_ &&
+                            !(pf != nullptr && pf[0] == '0')) ? 1 : 0;
+        }
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
@@ -508,6 +516,7 @@ class FLEngine {
         o["bank_level"] = dtype_ == 0 ? -1 : e_.level;
         o["eval_lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : ev_.lds_bytes;
         o["lag_reg"] = dtype_ == 1 && e_.lag_reg != 0;  // lagged rounds score in registers (fl_layout.h)
+        o["plain_fwd"] = c_.plain_fwd != 0;              // plain-bf16 training forward (several clients)
         o["eval_fedavg"] = peer_ != nullptr && !fused_ && eval_fedavg_fits();
         o["dtype"] = dtype_;
         o["slab_stride"] = c_.slab_stride;
@@ -735,6 +744,7 @@ class TrialBatch {
                                    std::memcmp(&e.ev_, &a.ev_, sizeof(MLPDescB)) != 0)))
                 throw std::runtime_error("TrialBatch: engines differ in shape or dtype");
             if (e.c_.R != a.c_.R || e.c_.n_rows != a.c_.n_rows || e.c_.world != a.c_.world ||
+                e.c_.plain_fwd != a.c_.plain_fwd ||
                 e.c_.rank != a.c_.rank || e.c_.slab_f16 != a.c_.slab_f16 || e.c_.lag_off != a.c_.lag_off ||
                 e.fused_ != a.fused_ || e.lagged() != a.lagged() || e.emulate_ != a.emulate_)
                 throw std::runtime_error("TrialBatch: engines differ in rows, clients or round kind");
@@ -894,7 +904,7 @@ class TrialBatch {
                                                     m.i[2], sel[3], m.i[3], s));
                 else
                     HIP_CHECK(fl_launch_train_bf16_batch(e.d_, e.e_, c.R, c.n_slabs, dT_, cnt, sel[0], sel[1], sel[2],
-                                                         m.i[0], m.i[1], m.i[2], sel[3], m.i[3], s));
+                                                         m.i[0], m.i[1], m.i[2], sel[3], m.i[3], s, c.plain_fwd));
                 break;
             case FLLaunchRec::ADAM:
                 HIP_CHECK(fl_launch_adam_batch(e.d_, e.dtype_ == 1 ? &e.e_ : nullptr, dT_, cnt, sel[0], sel[1], sel[2],

@@ -130,13 +130,15 @@ __global__ void fl_pack_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDe
 #define STAGE_X_UNROLL 2
 // NT: the staging threads (threads [0, NT); lagged rounds scored in registers leave the scoring
 // waves out, fwd_sync).
-template <int RT, int NT = FL_THREADS>
+// PLAIN (plain-bf16 training forward, FLConfig::plain_fwd): only the hi images and the biases
+// (the region's first w_off[0] + wlo_delta bytes) are staged -- half the bytes.
+template <int RT, int NT = FL_THREADS, bool PLAIN = false>
 __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const char* __restrict__ packed,
                                                        const float* __restrict__ X, int n_rows, int F, int row0,
                                                        char* lds) {
     const uint4* src = reinterpret_cast<const uint4*>(packed);
     uint4* dst = reinterpret_cast<uint4*>(lds + e.param_off);
-    const int n16 = e.param_bytes >> 4;
+    const int n16 = (PLAIN ? e.w_off[0] - e.param_off + e.wlo_delta : e.param_bytes) >> 4;
     const int kp = e.kp[0], lda = e.lda[0];
     const int nx = RT * 16 * kp;
     float xv[STAGE_X_UNROLL];
@@ -162,7 +164,7 @@ __device__ __forceinline__ void stage_params_rows_bf16(const MLPDescB& e, const 
                                                  16, 0, 0);
     }
 #else
-    static_assert(NT == FL_THREADS, "FL_STAGE_VGPR stages with every thread");
+    static_assert(NT == FL_THREADS && !PLAIN, "FL_STAGE_VGPR stages the whole region with every thread");
     uint4 pv[STAGE_P_UNROLL];
     // unpredicated loads (clamped indices): a conditionally written register array is
     // demoted to scratch by the compiler
@@ -256,7 +258,9 @@ __device__ __forceinline__ void params_store(const MLPDescB& e, const char* __re
 // hi / lo parts (all kp[l+1] columns, the padding comes out 0); last layer: fp32 logits [R][16].
 // NWV: waves that take the tiles (FL_WAVES; lagged rounds scored in registers: the first
 // FL_WAVES - 2 RT, fwd_sync).
-template <int RT, int NWV = FL_WAVES>
+// PLAIN: a_hi.W_hi only (the training forward of several clients, FLConfig::plain_fwd): no lo
+// operands, no lo parts of the outputs.
+template <int RT, int NWV = FL_WAVES, bool PLAIN = false>
 __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, char* lds) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
@@ -282,6 +286,11 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
         }
         for (int ks = 0; ks < ksteps; ++ks) {
             const bf16x8 bv = ld128(wrow + ks * 64);
+            if constexpr (PLAIN) {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ld128(act + aoff + rt * 16 * lda * 2 + ks * 64), bv, acc[rt]);
+                continue;
+            }
             const bf16x8 bl = ld128(wrow + e.wlo_delta + ks * 64);
             bf16x8 av[RT], al[RT];
 #pragma unroll
@@ -316,7 +325,7 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int t = 0; t < 4; t += 2) {
-                    if constexpr (NWV == FL_WAVES) {  // the one-client kernel: software rounding
+                    if constexpr (NWV == FL_WAVES && !PLAIN) {  // the one-client kernel: software rounding
                         // (the same bits; the hardware form below measured +1.3 us on its round)
 #pragma unroll
                         for (int q = 0; q < 2; ++q) {
@@ -338,12 +347,15 @@ __device__ __forceinline__ void fwd_layer_bf16(const MLPDesc& d, const MLPDescB&
                         v[q] = fmaxf(z + b, 0.f);
                     }
                     const uint32_t h = cvt_pk_bf16(v[0], v[1]);
-                    const uint32_t lo = cvt_pk_bf16(v[0] - __uint_as_float(h << 16), v[1] - __uint_as_float(h & 0xffff0000u));
                     const int o0 = (rt * 16 + fl_out_row(lg, t)) * ldo + n, o1 = (rt * 16 + fl_out_row(lg, t + 1)) * ldo + n;
                     out[o0] = (uint16_t)h;
-                    olo[o0] = (uint16_t)lo;
                     out[o1] = (uint16_t)(h >> 16);
-                    olo[o1] = (uint16_t)(lo >> 16);
+                    if constexpr (!PLAIN) {
+                        const uint32_t lo =
+                            cvt_pk_bf16(v[0] - __uint_as_float(h << 16), v[1] - __uint_as_float(h & 0xffff0000u));
+                        olo[o0] = (uint16_t)lo;
+                        olo[o1] = (uint16_t)(lo >> 16);
+                    }
                 }
         }
     }
@@ -499,7 +511,7 @@ __device__ __forceinline__ void fwd_sync(int* cnt, int& tgt) {
     }
 }
 
-template <int RT, bool PART = false>
+template <int RT, bool PART = false, bool PLAIN = false>
 __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, int* cnt,
                                                     int& tgt) {
     const int l = d.L - 1, C = d.dim[d.L], G = e.head_split;
@@ -523,6 +535,11 @@ __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPD
         const int k0 = wave * kper, k1 = min(ksteps, k0 + kper);
         for (int ks = k0; ks < k1; ++ks) {
             const bf16x8 bv = ld128(wrow + ks * 64);
+            if constexpr (PLAIN) {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ld128(act + aoff + rt * 16 * lda * 2 + ks * 64), bv, acc[rt]);
+                continue;
+            }
             const bf16x8 bl = ld128(wrow + e.wlo_delta + ks * 64);
             bf16x8 av[RT], al[RT];
 #pragma unroll
@@ -555,7 +572,7 @@ __device__ __forceinline__ void fwd_head_split_bf16(const MLPDesc& d, const MLPD
     }
 }
 
-template <int RT, bool PART = false>
+template <int RT, bool PART = false, bool PLAIN = false>
 __device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDescB& e, char* lds, unsigned long long* dbg,
                                                    int* cnt = nullptr) {
     int tgt = 0;
@@ -563,8 +580,8 @@ __device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDe
 #ifndef FL_LAG_STAMPS
         if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (l + 1 == d.L && e.head_split > 1) fwd_head_split_bf16<RT, PART>(d, e, lds, cnt, tgt);
-        else fwd_layer_bf16<RT, PART ? FL_WAVES - 2 * RT : FL_WAVES>(d, e, l, lds);
+        if (l + 1 == d.L && e.head_split > 1) fwd_head_split_bf16<RT, PART, PLAIN>(d, e, lds, cnt, tgt);
+        else fwd_layer_bf16<RT, PART ? FL_WAVES - 2 * RT : FL_WAVES, PLAIN>(d, e, l, lds);
         fwd_sync<RT, PART>(cnt, tgt);
     }
 }
@@ -850,7 +867,7 @@ __device__ void score_out(const MLPDesc& d, const MLPDescB& e, const FLConfig& c
 // the training pass (its register copy of the round's weights: R = 32 126 VGPRs), 2: in
 // registers on the last 2 RT waves (score_rows_regs, shapes of fl_lag_reg_ok); the other modes get
 // an instantiation without it (R = 32: 90 VGPRs; R = 64 spill-free).
-template <int RT, int LAG>
+template <int RT, int LAG, bool PLAIN>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float* __restrict__ pg,
                      const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int local_step,
@@ -858,7 +875,7 @@ fl_train_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float
 #include "fl_train_bf16_body.inc"
 }
 
-template <int RT>
+template <int RT, bool PLAIN>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_train_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel pg_sel, FLSel si_sel,
                            FLSel so_sel, int local_step, int stage_local, int mode, FLSel cm_sel, int fold_mask) {
@@ -963,14 +980,25 @@ hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLCon
     if ((mode == FL_EVAL_FUSED || mode == FL_EVAL_LAGGED) && cm_out == nullptr) return hipErrorInvalidValue;
     const size_t lds = (size_t)e.lds_bytes;
     const bool lag = mode == FL_EVAL_LAGGED;
-#define FLB_TRAIN(RT_, LAG_)                                                                                \
-    hipLaunchKernelGGL((fl_train_bf16_kernel<RT_, LAG_>), dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, \
+#define FLB_TRAIN(RT_, LAG_, PL_)                                                                           \
+    hipLaunchKernelGGL((fl_train_bf16_kernel<RT_, LAG_, PL_>), dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, \
                        si, so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask)
     const bool lreg = lag && e.lag_reg;
     switch (c.R) {
-        case 16: if (lreg) FLB_TRAIN(1, 2); else if (lag) FLB_TRAIN(1, 1); else FLB_TRAIN(1, 0); break;
-        case 32: if (lreg) FLB_TRAIN(2, 2); else if (lag) FLB_TRAIN(2, 1); else FLB_TRAIN(2, 0); break;
-        case 64: if (lag) FLB_TRAIN(4, 1); else FLB_TRAIN(4, 0); break;
+        // plain_fwd (FLConfig): the training forward of several clients with register scoring (R <= 32)
+        case 16:
+            if (lreg) { if (c.plain_fwd) FLB_TRAIN(1, 2, true); else FLB_TRAIN(1, 2, false); }
+            else if (lag) FLB_TRAIN(1, 1, false);
+            else if (c.plain_fwd) FLB_TRAIN(1, 0, true);
+            else FLB_TRAIN(1, 0, false);
+            break;
+        case 32:
+            if (lreg) { if (c.plain_fwd) FLB_TRAIN(2, 2, true); else FLB_TRAIN(2, 2, false); }
+            else if (lag) FLB_TRAIN(2, 1, false);
+            else if (c.plain_fwd) FLB_TRAIN(2, 0, true);
+            else FLB_TRAIN(2, 0, false);
+            break;
+        case 64: if (lag) FLB_TRAIN(4, 1, false); else FLB_TRAIN(4, 0, false); break;
         default: return hipErrorInvalidValue;
     }
 #undef FLB_TRAIN
@@ -1030,21 +1058,28 @@ hipError_t fl_launch_pack_bf16(const MLPDesc& d, const MLPDescB& e, const float*
 
 hipError_t fl_launch_train_bf16_batch(const MLPDesc& d, const MLPDescB& e, int R, int n_slabs, const FLTrialDesc* T,
                                       int K, FLSel pg, FLSel si, FLSel so, int ls, int stage_local, int mode, FLSel cm,
-                                      int fold_mask, hipStream_t s) {
+                                      int fold_mask, hipStream_t s, int plain) {
     if (K < 1 || mode == FL_EVAL_LAGGED || (mode == FL_EVAL_FUSED && cm.base < 0)) return hipErrorInvalidValue;
+    if (plain && (R == 64 || mode == FL_EVAL_FUSED)) return hipErrorInvalidValue;
     const size_t lds = (size_t)e.lds_bytes;
     const dim3 grid(n_slabs, K);
     switch (R) {
         case 16:
-            hipLaunchKernelGGL(fl_train_bf16_batch_kernel<1>, grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
+            if (plain) hipLaunchKernelGGL((fl_train_bf16_batch_kernel<1, true>), grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so,
+                                          ls, stage_local, mode, cm, fold_mask);
+            else hipLaunchKernelGGL((fl_train_bf16_batch_kernel<1, false>), grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
                                stage_local, mode, cm, fold_mask);
             break;
         case 32:
-            hipLaunchKernelGGL(fl_train_bf16_batch_kernel<2>, grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
+            if (plain) hipLaunchKernelGGL((fl_train_bf16_batch_kernel<2, true>), grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so,
+                                          ls, stage_local, mode, cm, fold_mask);
+            else hipLaunchKernelGGL((fl_train_bf16_batch_kernel<2, false>), grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
                                stage_local, mode, cm, fold_mask);
             break;
         case 64:
-            hipLaunchKernelGGL(fl_train_bf16_batch_kernel<4>, grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
+            if (plain) hipLaunchKernelGGL((fl_train_bf16_batch_kernel<4, true>), grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so,
+                                          ls, stage_local, mode, cm, fold_mask);
+            else hipLaunchKernelGGL((fl_train_bf16_batch_kernel<4, false>), grid, dim3(FL_THREADS), lds, s, d, e, T, pg, si, so, ls,
                                stage_local, mode, cm, fold_mask);
             break;
         default: return hipErrorInvalidValue;
@@ -1090,14 +1125,17 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
 #define FLB_SET(fn)                                                                                     \
     if (r == hipSuccess)                                                                                \
     r = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, v)
-    FLB_SET((fl_train_bf16_kernel<1, 0>)); FLB_SET((fl_train_bf16_kernel<2, 0>));
-    FLB_SET((fl_train_bf16_kernel<4, 0>));
-    FLB_SET((fl_train_bf16_kernel<1, 1>)); FLB_SET((fl_train_bf16_kernel<2, 1>));
-    FLB_SET((fl_train_bf16_kernel<4, 1>));
-    FLB_SET((fl_train_bf16_kernel<1, 2>)); FLB_SET((fl_train_bf16_kernel<2, 2>));
+    FLB_SET((fl_train_bf16_kernel<1, 0, false>)); FLB_SET((fl_train_bf16_kernel<2, 0, false>));
+    FLB_SET((fl_train_bf16_kernel<4, 0, false>));
+    FLB_SET((fl_train_bf16_kernel<1, 1, false>)); FLB_SET((fl_train_bf16_kernel<2, 1, false>));
+    FLB_SET((fl_train_bf16_kernel<4, 1, false>));
+    FLB_SET((fl_train_bf16_kernel<1, 2, false>)); FLB_SET((fl_train_bf16_kernel<2, 2, false>));
+    FLB_SET((fl_train_bf16_kernel<1, 2, true>)); FLB_SET((fl_train_bf16_kernel<2, 2, true>));
+    FLB_SET((fl_train_bf16_kernel<1, 0, true>)); FLB_SET((fl_train_bf16_kernel<2, 0, true>));
     FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>); FLB_SET(fl_eval_bf16_kernel<4>);
-    FLB_SET(fl_train_bf16_batch_kernel<1>); FLB_SET(fl_train_bf16_batch_kernel<2>);
-    FLB_SET(fl_train_bf16_batch_kernel<4>);
+    FLB_SET((fl_train_bf16_batch_kernel<1, false>)); FLB_SET((fl_train_bf16_batch_kernel<2, false>));
+    FLB_SET((fl_train_bf16_batch_kernel<4, false>)); FLB_SET((fl_train_bf16_batch_kernel<1, true>));
+    FLB_SET((fl_train_bf16_batch_kernel<2, true>)); FLB_SET((fl_train_bf16_batch_kernel<4, true>));
     FLB_SET(fl_eval_bf16_batch_kernel<1>); FLB_SET(fl_eval_bf16_batch_kernel<2>); FLB_SET(fl_eval_bf16_batch_kernel<4>);
     FLB_SET(fl_eval_fedavg_bf16_kernel<1>); FLB_SET(fl_eval_fedavg_bf16_kernel<2>);
 #undef FLB_SET

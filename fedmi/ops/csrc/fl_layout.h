@@ -68,7 +68,7 @@ inline int fl_lag_reg_static_bytes(int R) { return (R / 16) * (FL_LAG_PARTS * 16
 inline bool fl_lag_reg_ok(const MLPDesc& d, const MLPDescB& e, int R) {
     const int L = d.L, C = d.dim[L];
     const int nw = FL_WAVES - 2 * (R / 16);
-    if (R % 16 != 0 || nw < 1 || (L != 2 && L != 3) || C > FL_LAG_MAX_C) return false;
+    if ((R != 16 && R != 32) || nw < 1 || (L != 2 && L != 3) || C > FL_LAG_MAX_C) return false;
     if (e.kp[0] > 32 || (L == 3 && e.kp[1] > 64)) return false;
     const int G = e.head_split;
     if (G > nw || G - (G + 1) / 2 > FL_LAG_PARTS) return false;

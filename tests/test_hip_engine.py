@@ -738,35 +738,44 @@ def test_bf16_train_kernel_gradient(R, slab):
 def test_lagged_register_scoring_equals_serial_pass(hidden, C, R, monkeypatch):
     """Lagged rounds (several clients: round r's post-step local model scored inside round r+1's
     train kernel) score in registers on the waves the training forward pass leaves idle
-    (fl_kernels_bf16.hip score_rows_regs): the per-client metrics, loss history and weights are
-    bit-identical to the serial scoring pass (FEDMI_LAG_REG=0) and to classic rounds with a
-    separate evaluation kernel -- one and two hidden layers, 16 / 32 rows per workgroup, C = 3, a
-    partial last row block; C = 5 (> FL_LAG_MAX_C) takes the serial pass."""
+    (fl_kernels_bf16.hip score_rows_regs), and the training forward of several clients is then
+    plain bf16 (FLConfig::plain_fwd) in every kind of round: per-client metrics, loss history and
+    weights of lagged rounds are bit-identical to classic rounds with a separate evaluation
+    kernel.  With FEDMI_LAG_REG=0 the serial scoring pass and the split training forward are
+    bit-identical to classic rounds likewise.  One and two hidden layers, 16 / 32 rows per
+    workgroup, C = 3, a partial last row block; C = 5 (> FL_LAG_MAX_C) takes the serial pass."""
     X, y = make_income_like(2100, seed=21)
     if C > 2:
         y = ((X[:, 0] > 0).astype(np.int64) + 2 * (X[:, 1] > 0) + (X[:, 2] > 0.5)) % C
     flat = init_flat([14, *hidden, C], 8)
-    out = []
-    for mode in ("reg", "serial", "classic"):
-        if mode == "serial":
-            monkeypatch.setenv("FEDMI_LAG_REG", "0")
-        else:
-            monkeypatch.delenv("FEDMI_LAG_REG", raising=False)
-        cfg = EngineConfig(hidden=tuple(hidden), max_rounds=40, early_stop=False, dtype="bf16", graph_rounds=4,
-                           rows_per_block=R, fused_eval=False, lagged_eval=mode != "classic")
-        e = HipRoundEngine(X, y, C, cfg, None, flat, emulate_clients=True)
-        assert bool(e.engine.lagged) == (mode != "classic")
-        if mode != "classic":
-            assert e.engine.layout()["lag_reg"] == (mode == "reg" and C <= 4)
-        e.run(3)
-        e.run(9)
-        e.sync_history()
-        h = e.history()
-        assert h["rounds_run"] == 12
-        out.append((e.global_flat(), h))
-    (wr, hr), (ws, hs), (wc, hc) = out
-    for w, h, name in ((ws, hs, "serial"), (wc, hc, "classic")):
-        np.testing.assert_array_equal(wr, w, err_msg=name)
-        np.testing.assert_array_equal(hr["global"], h["global"], err_msg=name)
-        np.testing.assert_array_equal(hr["per_rank"], h["per_rank"], err_msg=name)
-        np.testing.assert_array_equal(hr["loss"], h["loss"], err_msg=name)
+    eligible = C <= 4
+    out = {}
+    for env in (None, "0"):
+        for lagged in (True, False):
+            if env is None:
+                monkeypatch.delenv("FEDMI_LAG_REG", raising=False)
+            else:
+                monkeypatch.setenv("FEDMI_LAG_REG", env)
+            cfg = EngineConfig(hidden=tuple(hidden), max_rounds=40, early_stop=False, dtype="bf16", graph_rounds=4,
+                               rows_per_block=R, fused_eval=False, lagged_eval=lagged)
+            e = HipRoundEngine(X, y, C, cfg, None, flat, emulate_clients=True)
+            assert bool(e.engine.lagged) == lagged
+            lay = e.engine.layout()
+            assert lay["lag_reg"] == (env is None and eligible)
+            assert lay["plain_fwd"] == (env is None and eligible)
+            e.run(3)
+            e.run(9)
+            e.sync_history()
+            h = e.history()
+            assert h["rounds_run"] == 12
+            out[(env, lagged)] = (e.global_flat(), h)
+    for env in (None, "0"):
+        (wl, hl), (wc, hc) = out[(env, True)], out[(env, False)]
+        name = f"FEDMI_LAG_REG={env}"
+        np.testing.assert_array_equal(wl, wc, err_msg=name)
+        np.testing.assert_array_equal(hl["global"], hc["global"], err_msg=name)
+        np.testing.assert_array_equal(hl["per_rank"], hc["per_rank"], err_msg=name)
+        np.testing.assert_array_equal(hl["loss"], hc["loss"], err_msg=name)
+    if eligible:  # the plain training forward changes the trajectory, not its quality
+        a, b = out[(None, True)][1]["global"][-1], out[("0", True)][1]["global"][-1]
+        assert abs(a[0] - b[0]) < 0.02, (a, b)
