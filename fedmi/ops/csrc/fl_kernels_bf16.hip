@@ -614,13 +614,6 @@ __device__ __forceinline__ void lag_stamp(const FLBuffers& b, int slot, uint32_t
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-// timing experiments only (-DFL_LAG_EXP=1: every hidden tile re-reads tile 0's weights, an L1-hot
-// address -- wrong logits, for stamps)
-#if defined(FL_LAG_EXP) && FL_LAG_EXP == 1
-#define LAG_EXP_T(t) 0
-#else
-#define LAG_EXP_T(t) (t)
-#endif
 struct TileBits {  // one transposed tile after bias + ReLU: hi / lo bf16 pairs of features 4g..4g+3
     uint32_t h0, h1, l0, l1;
 };
@@ -735,15 +728,15 @@ __device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDe
     int w = half ? wA : 0, kend = min(ksteps, (w + 1) * kper);
     for (int ks = ks0; ks < ks1; ++ks) {
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) ldw_t(LAG_EXP_T(2 * ks + 1), kb, bh2[kb], bl2[kb]);
-        bbias = ldb_t(LAG_EXP_T(2 * ks + 1));
+        for (int kb = 0; kb < KB; ++kb) ldw_t(2 * ks + 1, kb, bh2[kb], bl2[kb]);
+        bbias = ldb_t(2 * ks + 1);
         const TileBits t0 = score_tile<KB>(ah, al, bh, bl, nkb, abias);
         int nx = min(2 * ks + 2, ntiles - 1);
         // set A reloads after tile 2ks consumed all of it (no register copy)
         asm volatile("" : "+s"(nx) : "v"(t0.h0), "v"(t0.h1), "v"(t0.l0), "v"(t0.l1));
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) ldw_t(LAG_EXP_T(nx), kb, ah[kb], al[kb]);
-        abias = ldb_t(LAG_EXP_T(nx));
+        for (int kb = 0; kb < KB; ++kb) ldw_t(nx, kb, ah[kb], al[kb]);
+        abias = ldb_t(nx);
         const TileBits t1 = score_tile<KB>(bh2, bl2, bh, bl, nkb, bbias);
 #ifdef FL_LAG_STAMPS
         if (ks == 1) lag_stamp(b, 12, t1.h0, last);
@@ -780,20 +773,38 @@ __device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDe
 struct ScoreIn {
     bf16x8 h[2], l[2];
 };
+// The first hidden layer's weights (<= 4 tiles, hi / lo / bias), loaded by the scoring waves at the
+// kernel start -- they stage nothing -- so they land while the other waves stage (issued after the
+// staging barrier they came from beyond the L2 in ~2 us, every CU asking for the same lines at once).
+struct ScorePre {
+    bf16x8 w0h[4][1], w0l[4][1];
+    f32x4 b0[4];
+};
+template <int RT>
+__device__ __forceinline__ void score_prefetch(const MLPDesc& d, const MLPDescB& e, const FLBuffers& b, ScorePre& pre) {
+    if (d.L != 3) return;
+    const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+    const int nt0 = e.kp[1] >> 4;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int t = nt < nt0 ? nt : 0;
+        score_ldw(e, b.pk_local, 0, t, 0, r, g, pre.w0h[nt][0], pre.w0l[nt][0]);
+        pre.b0[nt] = score_ldb(e, b.pk_local, 0, t, g);
+    }
+}
 
 // Input side of a scoring wave `sw` (2 per 16-row group; rows row0 + 16 (sw / 2) + (0..15)), after
 // the staging barrier: the staged rows (act_0 / alo_0, the B operand of the transposed product),
-// and with two hidden layers the first one (<= 4 tiles, every load issued first; both waves of
-// the group) -> `in` = the B operand of the last hidden layer.  (Tried: the rows from global
+// and with two hidden layers the first one (weights from score_prefetch; both waves of the group)
+// -> `in` = the B operand of the last hidden layer.  (Tried: the rows from global
 // memory and the first layer before the staging barrier, with or without a first touch of every
 // line of the local image -- the loads queue behind the staging's and delay the barrier;
 // profiles/lag_reg_ab_r3.log.)
 template <int RT>
 __device__ __forceinline__ void score_in_lds(const MLPDesc& d, const MLPDescB& e, const FLBuffers& b, const char* lds,
-                                             int sw, ScoreIn& in) {
+                                             int sw, const ScorePre& pre, ScoreIn& in) {
     const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
     const int swu = __builtin_amdgcn_readfirstlane(sw);
-    const char* __restrict__ pk = b.pk_local;
     const int xo = ((16 * (swu >> 1) + r) * e.lda[0] + 8 * g) * 2;
     bf16x8 xh[1], xl[1];
     xh[0] = ld128(lds + e.act_off[0] + xo);
@@ -804,18 +815,10 @@ __device__ __forceinline__ void score_in_lds(const MLPDesc& d, const MLPDescB& e
         return;
     }
     const int nt0 = e.kp[1] >> 4;
-    bf16x8 w0h[4][1], w0l[4][1];
-    f32x4 b0[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const int t = nt < nt0 ? nt : 0;
-        score_ldw(e, pk, 0, t, 0, r, g, w0h[nt][0], w0l[nt][0]);
-        b0[nt] = score_ldb(e, pk, 0, t, g);
-    }
     TileBits t0[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
-        if (nt < nt0) t0[nt] = score_tile<1>(w0h[nt], w0l[nt], xh, xl, 1, b0[nt]);
+        if (nt < nt0) t0[nt] = score_tile<1>(pre.w0h[nt], pre.w0l[nt], xh, xl, 1, pre.b0[nt]);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
         if (2 * kb < nt0) pair_to_b(t0[2 * kb], t0[2 * kb + 1], in.h[kb], in.l[kb]);

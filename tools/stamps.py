@@ -18,7 +18,11 @@ dtype = sys.argv[4] if len(sys.argv) > 4 else "fp32"
 X, y = make_income_like(rows, seed=1)
 cfg = EngineConfig(hidden=hidden, max_rounds=100, rows_per_block=R, graph_rounds=0, early_stop=False,
                    dtype=dtype)
-e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *hidden, 2], 0))
+# 5th argument "emulate": a multi-client engine (emulate_clients: lagged rounds, plain-bf16 training forward)
+emulate = len(sys.argv) > 5 and sys.argv[5] == "emulate"
+if emulate:
+    cfg.fused_eval = False
+e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, *hidden, 2], 0), emulate_clients=emulate)
 e.run(3)
 nb = (rows + R - 1) // R
 dbg = torch.zeros(nb * 16, dtype=torch.int64, device=e.device)
