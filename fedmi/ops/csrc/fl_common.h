@@ -29,11 +29,16 @@
 #define FL_THREADS 1024
 #endif
 #define FL_WAVES (FL_THREADS / 64)
-// Lagged rounds scored in registers (fl_layout.h fl_lag_reg_ok): two waves per 16-row group
-// split the last hidden layer; the upper one hands at most FL_LAG_PARTS logits partials (C <= 4
-// classes) to the lower one through LDS.
-#define FL_LAG_PARTS 4
+// Lagged rounds scored in registers (fl_layout.h fl_lag_reg_ok): FL_LAG_SPR waves per 16-row
+// group split the last hidden layer; each upper one hands at most FL_LAG_PARTS logits partials
+// (C <= 4 classes) to the group's first wave through LDS.
+#ifndef FL_LAG_SPR
+#define FL_LAG_SPR 3
+#endif
+#define FL_LAG_PARTS (FL_LAG_SPR == 2 ? 4 : 2)
 #define FL_LAG_MAX_C 4
+// logits part range of scoring wave j of a group (parts [fl_lag_w(G, j), fl_lag_w(G, j + 1)))
+__host__ __device__ inline int fl_lag_w(int G, int j) { return G - ((FL_LAG_SPR - j) * G) / FL_LAG_SPR; }
 
 // ldw = roundup16(K) + 4 (4 mod 8 floats): 16-byte aligned rows, and the 16 rows of a
 // 16-lane ds_read_b128 group land on 16 distinct 16-byte bank slots.

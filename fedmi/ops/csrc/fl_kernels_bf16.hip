@@ -257,7 +257,7 @@ __device__ __forceinline__ void params_store(const MLPDescB& e, const char* __re
 // `acl` (independent accumulation chains), z = acc + acl.  Hidden layers: ReLU -> act_{l+1}
 // hi / lo parts (all kp[l+1] columns, the padding comes out 0); last layer: fp32 logits [R][16].
 // NWV: waves that take the tiles (FL_WAVES; lagged rounds scored in registers: the first
-// FL_WAVES - 2 RT, fwd_sync).
+// FL_WAVES - FL_LAG_SPR RT, fwd_sync).
 // PLAIN: a_hi.W_hi only (the training forward of several clients, FLConfig::plain_fwd): no lo
 // operands, no lo parts of the outputs.
 template <int RT, int NWV = FL_WAVES, bool PLAIN = false>
@@ -498,12 +498,12 @@ __device__ void dgrad_layer_bf16(const MLPDesc& d, const MLPDescB& e, int l, cha
 // columns into part[w][row][c]; after a barrier, thread (row, c) sums the G partials in order
 // and adds the bias.  (One wave's chain of kp/32 dependent steps was the longest forward phase.)
 // Forward-phase barrier.  PART (lagged rounds scored in registers): only the first
-// FL_WAVES - 2 RT waves run the forward pass, so they meet through an LDS arrival count (`tgt`
-// grows by their number per phase) while the last 2 RT waves score (score_rows_regs).
+// FL_WAVES - FL_LAG_SPR RT waves run the forward pass, so they meet through an LDS arrival count (`tgt`
+// grows by their number per phase) while the last FL_LAG_SPR RT waves score (score_out).
 template <int RT, bool PART>
 __device__ __forceinline__ void fwd_sync(int* cnt, int& tgt) {
     if constexpr (PART) {
-        tgt += FL_WAVES - 2 * RT;
+        tgt += FL_WAVES - FL_LAG_SPR * RT;
         lds_count_arrive(cnt);
         lds_count_wait(cnt, tgt);
     } else {
@@ -581,7 +581,7 @@ __device__ __forceinline__ void forward_block_bf16(const MLPDesc& d, const MLPDe
         if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + 10 + l] = __builtin_amdgcn_s_memrealtime();
 #endif
         if (l + 1 == d.L && e.head_split > 1) fwd_head_split_bf16<RT, PART, PLAIN>(d, e, lds, cnt, tgt);
-        else fwd_layer_bf16<RT, PART ? FL_WAVES - 2 * RT : FL_WAVES, PLAIN>(d, e, l, lds);
+        else fwd_layer_bf16<RT, PART ? FL_WAVES - FL_LAG_SPR * RT : FL_WAVES, PLAIN>(d, e, l, lds);
         fwd_sync<RT, PART>(cnt, tgt);
     }
 }
@@ -674,23 +674,25 @@ __device__ __forceinline__ void pair_to_b(const TileBits& a, const TileBits& b, 
 // The last hidden layer l (input B operand bh/bl, nkb k-blocks) streamed into the logits
 // layer: each tile pair is one k-block of the logits' product, accumulated in the K-split
 // parts of fwd_head_split_bf16 (part w = k-blocks [w*kper, (w+1)*kper), z = ((p_0 + p_1) + ...)
-// + b; head_split 1 = fwd_layer_bf16's single chain).  Two waves share a 16-row group: `half` 0
-// takes parts [0, wA) (wA = ceil(G/2)) and their k-blocks, half 1 the rest; half 1 stores its
-// parts in `parts` (LDS, lane group 0 = classes 0..3) and counts itself in `ready`, half 0 adds
-// them to its own running sum in part order -- the same additions in the same order as one
+// + b; head_split 1 = fwd_layer_bf16's single chain).  FL_LAG_SPR waves share a 16-row group: wave
+// `sj` takes parts [fl_lag_w(G, sj), fl_lag_w(G, sj + 1)) and their k-blocks; the upper waves store
+// their parts in `parts` (LDS, lane group 0 = classes 0..3) and count themselves in `ready`, wave
+// 0 adds them to its own running sum in part order -- the same additions in the same order as one
 // wave (or fwd_head_split_bf16's partial sum) -- and returns the logits of lane (r, g): classes
-// 4g..4g+3 of row r (half 1 returns nothing useful).  W tiles and biases are prefetched one
-// tile ahead.
+// 4g..4g+3 of row r (the upper waves return nothing useful).  W tiles and biases are prefetched
+// one tile ahead.
 template <int KB>
 __device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDescB& e, const char* __restrict__ pk,
                                                    int l, const bf16x8 (&bh)[KB], const bf16x8 (&bl)[KB], int nkb,
-                                                   int m, int g, int half, f32x4* parts, int* ready,
+                                                   int m, int g, int sj, f32x4* parts, int* ready,
                                                    const FLBuffers& b, bool last) {
     const int lh = d.L - 1;
     const int ntiles = e.kp[l + 1] >> 4, ksteps = ntiles >> 1;
     const int G = e.head_split, kper = (ksteps + G - 1) / G;
-    const int wA = (G + 1) >> 1, KA = min(ksteps, kper * wA);
-    const int ks0 = half ? KA : 0, ks1 = half ? ksteps : KA;
+    // this wave's logits parts [wA, wB) and their k-blocks [ks0, ks1)
+    const int wA = fl_lag_w(G, sj), wB = fl_lag_w(G, sj + 1);
+    const int ks0 = min(ksteps, kper * wA), ks1 = min(ksteps, kper * wB);
+    f32x4* myparts = parts + (sj > 0 ? (sj - 1) * FL_LAG_PARTS * 16 : 0);
     // buffer loads: the per-lane part of every address (W row m of a tile, its swizzled chunk g,
     // the bias entries of lane group g) is fixed, the tile / k-block part scalar -- no address
     // arithmetic per load
@@ -725,7 +727,7 @@ __device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDe
     const f32x4 hb = score_ldb(e, pk, lh, 0, g);
     const f32x4 zero = (f32x4){0.f, 0.f, 0.f, 0.f};
     f32x4 acc = zero, acl = zero, s = zero;
-    int w = half ? wA : 0, kend = min(ksteps, (w + 1) * kper);
+    int w = wA, kend = min(ksteps, (w + 1) * kper);
     for (int ks = ks0; ks < ks1; ++ks) {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) ldw_t(2 * ks + 1, kb, bh2[kb], bl2[kb]);
@@ -749,8 +751,8 @@ __device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDe
         if (ks + 1 < ks1) ldh(ks + 1, hh, hl);
         if (ks + 1 == kend) {  // part w complete
             const f32x4 p = acc + acl;
-            if (half == 0) s = (w == 0) ? p : s + p;
-            else if (g == 0) parts[(w - wA) * 16 + m] = p;
+            if (sj == 0) s = (w == 0) ? p : s + p;
+            else if (g == 0) myparts[(w - wA) * 16 + m] = p;
             acc = zero;
             acl = zero;
             ++w;
@@ -758,13 +760,15 @@ __device__ __forceinline__ f32x4 score_hidden_head(const MLPDesc& d, const MLPDe
         }
     }
     // empty trailing parts (0 + 0), as fwd_head_split_bf16 sums them
-    if (half == 0) {
-        for (; w < wA; ++w) s = s + (acc + acl);
-        lds_count_wait(ready, 1);
-        for (w = wA; w < G; ++w) s = s + parts[(w - wA) * 16 + m];
+    if (sj == 0) {
+        for (; w < wB; ++w) s = s + (acc + acl);
+        lds_count_wait(ready, FL_LAG_SPR - 1);
+        for (int j = 1; j < FL_LAG_SPR; ++j)
+            for (int u = fl_lag_w(G, j); u < fl_lag_w(G, j + 1); ++u)
+                s = s + parts[((j - 1) * FL_LAG_PARTS + u - fl_lag_w(G, j)) * 16 + m];
     } else {
-        for (; w < G; ++w)
-            if (g == 0) parts[(w - wA) * 16 + m] = acc + acl;
+        for (; w < wB; ++w)
+            if (g == 0) myparts[(w - wA) * 16 + m] = acc + acl;
         lds_count_arrive(ready);
     }
     return s + hb;
@@ -805,7 +809,7 @@ __device__ __forceinline__ void score_in_lds(const MLPDesc& d, const MLPDescB& e
                                              int sw, const ScorePre& pre, ScoreIn& in) {
     const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
     const int swu = __builtin_amdgcn_readfirstlane(sw);
-    const int xo = ((16 * (swu >> 1) + r) * e.lda[0] + 8 * g) * 2;
+    const int xo = ((16 * (swu / FL_LAG_SPR) + r) * e.lda[0] + 8 * g) * 2;
     bf16x8 xh[1], xl[1];
     xh[0] = ld128(lds + e.act_off[0] + xo);
     xl[0] = ld128(lds + e.alo_off[0] + xo);
@@ -826,29 +830,29 @@ __device__ __forceinline__ void score_in_lds(const MLPDesc& d, const MLPDescB& e
 }
 
 // Output side, after the staging barrier: the last hidden layer + logits (score_hidden_head,
-// the group's two waves splitting it), argmax -> cm_s (LDS ints) by the group's half-0 wave;
+// the group's FL_LAG_SPR waves splitting it), argmax -> cm_s (LDS ints) by the group's wave 0;
 // ysc = the label of row r (lane r + 16 g).
 template <int RT>
 __device__ void score_out(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b, int* cm_s,
                           int sw, int row0, int ysc, const ScoreIn& in, f32x4* parts, int* ready) {
     const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
     const int swu = __builtin_amdgcn_readfirstlane(sw);  // wave-uniform: scalar tile indices
-    const int half = swu & 1;
+    const int sj = swu % FL_LAG_SPR;  // this wave's share of its row group (0: sums and counts)
     const char* __restrict__ pk = b.pk_local;
     const int C = d.dim[d.L];
-    const int row = row0 + 16 * (swu >> 1) + r;
+    const int row = row0 + 16 * (swu / FL_LAG_SPR) + r;
     const bool last = swu == 0;
     if (b.dbg != nullptr && lane == 0 && last) b.dbg[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
     f32x4 z;
     if (d.L == 2) {
         const bf16x8 xh[1] = {in.h[0]}, xl[1] = {in.l[0]};
-        z = score_hidden_head<1>(d, e, pk, 0, xh, xl, 1, r, g, half, parts, ready, b, last);
+        z = score_hidden_head<1>(d, e, pk, 0, xh, xl, 1, r, g, sj, parts, ready, b, last);
     } else {
         if ((e.kp[1] >> 5) == 2) {
-            z = score_hidden_head<2>(d, e, pk, 1, in.h, in.l, 2, r, g, half, parts, ready, b, last);
+            z = score_hidden_head<2>(d, e, pk, 1, in.h, in.l, 2, r, g, sj, parts, ready, b, last);
         } else {
             const bf16x8 xh[1] = {in.h[0]}, xl[1] = {in.l[0]};
-            z = score_hidden_head<1>(d, e, pk, 1, xh, xl, 1, r, g, half, parts, ready, b, last);
+            z = score_hidden_head<1>(d, e, pk, 1, xh, xl, 1, r, g, sj, parts, ready, b, last);
         }
     }
     // stamps (tools/stamps.py): 13 = the first scoring wave past the staging barrier, 14 = its logits done
@@ -859,7 +863,7 @@ __device__ void score_out(const MLPDesc& d, const MLPDescB& e, const FLConfig& c
 #pragma unroll
     for (int k = 1; k < FL_LAG_MAX_C; ++k)
         if (k < C && z[k] > bv) { bv = z[k]; best = k; }
-    if (half == 0 && g == 0 && row < c.n_rows) atomicAdd(&cm_s[ysc * C + best], 1);
+    if (sj == 0 && g == 0 && row < c.n_rows) atomicAdd(&cm_s[ysc * C + best], 1);
 }
 
 // ---------------------------------------------------------------------------------------

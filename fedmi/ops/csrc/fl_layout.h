@@ -58,20 +58,22 @@ inline void fl_build_fp32_layout(const int* dims, int L, int R, MLPDesc* d) {
 // Lagged rounds (FL_EVAL_LAGGED) score the previous round's local model in registers
 // (fl_kernels_bf16.hip score_rows_regs) when: one or two hidden layers; the register operands
 // fit (features <= 32, with two hidden layers the first <= 64 wide); C <= FL_LAG_MAX_C; the
-// logits' K split leaves the upper scoring wave at most FL_LAG_PARTS partials; the training
-// forward pass fits the first FL_WAVES - 2 R/16 waves (hidden tiles are strided over them; the
+// logits' K split leaves each upper scoring wave at most FL_LAG_PARTS partials; the training
+// forward pass fits the first FL_WAVES - FL_LAG_SPR R/16 waves (hidden tiles are strided over them; the
 // logits layer's split K loop and its partial sum must fit them as they are), so the last
-// 2 R/16 waves -- two per 16 rows -- score while the others train; and the LDS holds the
+// FL_LAG_SPR R/16 waves -- FL_LAG_SPR per 16 rows -- score while the others train; and the LDS holds the
 // partials beside the layout.  Otherwise the scoring pass runs before the training pass on the
 // whole workgroup.
-inline int fl_lag_reg_static_bytes(int R) { return (R / 16) * (FL_LAG_PARTS * 16 * 16 + 16); }
+inline int fl_lag_reg_static_bytes(int R) { return (R / 16) * ((FL_LAG_SPR - 1) * FL_LAG_PARTS * 16 * 16 + 16); }
 inline bool fl_lag_reg_ok(const MLPDesc& d, const MLPDescB& e, int R) {
     const int L = d.L, C = d.dim[L];
-    const int nw = FL_WAVES - 2 * (R / 16);
+    const int nw = FL_WAVES - FL_LAG_SPR * (R / 16);
     if ((R != 16 && R != 32) || nw < 1 || (L != 2 && L != 3) || C > FL_LAG_MAX_C) return false;
     if (e.kp[0] > 32 || (L == 3 && e.kp[1] > 64)) return false;
     const int G = e.head_split;
-    if (G > nw || G - (G + 1) / 2 > FL_LAG_PARTS) return false;
+    if (G > nw) return false;
+    for (int j = 1; j < FL_LAG_SPR; ++j)
+        if (fl_lag_w(G, j + 1) - fl_lag_w(G, j) > FL_LAG_PARTS) return false;
     if (R * C > nw * 64) return false;  // the logits' partial sums (fwd_head_split_bf16) run on thread < R*C
     // the partials ride in static LDS beside the dynamic layout (FL_LDS_DYNAMIC_MAX keeps 2 KB for
     // the kernels' own small statics; ~256 B are taken)

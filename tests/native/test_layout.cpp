@@ -384,12 +384,17 @@ static void check_fp32(const MLPDesc& d, int R) {
 // bias entries < kp[l+1]) and inside their register arrays (layer-0 input 1 k-block, the stored
 // first hidden layer <= 2 k-blocks, <= 4 tiles).
 static void check_lag_reg(const MLPDesc& d, const MLPDescB& e, int R) {
-    const int L = d.L, C = d.dim[L], nw = FL_WAVES - 2 * (R / 16);
+    const int L = d.L, C = d.dim[L], nw = FL_WAVES - FL_LAG_SPR * (R / 16);
     for (int l = 0; l + 1 < L; ++l)  // fwd_layer_bf16<RT, nw>: tile nt on wave nt % nw
         for (int nt = 0; nt < (e.kp[l + 1] >> 4); ++nt) CHECK(nt % nw < nw, "lag_reg: layer %d tile %d on a scoring wave", l, nt);
     CHECK(e.head_split <= nw && R * C <= nw * 64 && ((C + 15) >> 4) <= nw, "lag_reg: logits phase on a scoring wave");
     const int G = e.head_split;
-    CHECK(C <= FL_LAG_MAX_C && G - (G + 1) / 2 <= FL_LAG_PARTS, "lag_reg: C %d, logits split %d", C, G);
+    CHECK(C <= FL_LAG_MAX_C, "lag_reg: C %d", C);
+    for (int j = 0; j < FL_LAG_SPR; ++j) {  // part ranges tile [0, G); upper waves' fit their LDS slots
+        CHECK(fl_lag_w(G, j) <= fl_lag_w(G, j + 1), "lag_reg: part range %d of split %d", j, G);
+        if (j > 0) CHECK(fl_lag_w(G, j + 1) - fl_lag_w(G, j) <= FL_LAG_PARTS, "lag_reg: parts of wave %d, split %d", j, G);
+    }
+    CHECK(fl_lag_w(G, 0) == 0 && fl_lag_w(G, FL_LAG_SPR) == G, "lag_reg: part ranges of split %d", G);
     CHECK(e.lds_bytes + fl_lag_reg_static_bytes(R) + 256 <= 160 * 1024, "lag_reg: LDS %d", e.lds_bytes);
     CHECK(L == 2 || L == 3, "lag_reg: %d layers", L);
     CHECK(e.kp[0] / 32 == 1, "lag_reg: input k-blocks %d", e.kp[0] / 32);
