@@ -9,14 +9,20 @@ metrics), and the sample-size-weighted FedAvg of all clients' weights (one RCCL
 all-reduce; per-round metrics and the early-stop state ride in the same collective).
 
 Data: synthetic balanced-income-shaped rows (14 features, 2 classes) generated on the
-device, ``--rows-per-client`` rows per client (default 8000 = the reference's
-single-client training shard), weights random-init.  Per-GPU work is fixed
-as N grows (weak scaling).  ``value`` = training samples processed per second summed over
-all clients; ``vs_baseline`` divides by the reference's measured train samples/s/client
-at the same client count times N (408k / 398k / 323k / 264k per client at
-k = 1 / 2 / 4 / 8; the reference's time excludes its eval and FedAvg, ours includes
-them).  After the timed region, rounds-to-target on the real income CSV (compat mode,
-this client count) is measured and reported as ``rounds_to_target``.
+device, weights random-init.  Shards follow the reference's chunking of its 8000 training
+rows over the k clients (``_split_data``, FL_CustomMLP...Multiple_Rounds.py:57-60: chunk =
+8000 // k, the last rank takes the remainder), i.e. 8000 / 4000 / 2000 / 1000 rows per
+client at k = 1 / 2 / 4 / 8 -- exactly the shard sizes BASELINE.md's k-columns were measured
+on, so the total work is fixed as N grows (strong scaling).  ``value`` = training samples
+processed per second summed over all clients; ``vs_baseline`` divides by the reference's
+measured train samples/s/client at the same k times N (408k / 398k / 323k /
+264k; the reference's time excludes its eval and FedAvg, ours includes them).  The
+early-stop rule (C:181-192, atol 1e-4 on the 4-metric vector) is evaluated on the device in
+every timed round, with a patience no timed round can exhaust, so every timed round is live.
+Companion key ``weak_8000_rows_per_client``: the same round with 8000 rows on every client
+(per-GPU work fixed).  After the timed region, rounds-to-target on the real income CSV
+(compat mode, this client count, the same shards) is measured and reported as
+``rounds_to_target``.
 
     python bench.py --gpus 1 --steps 2000 --warmup 200
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 ...
@@ -45,6 +51,18 @@ def ref_per_client(n: int) -> float:
     ks = sorted(REF_PER_CLIENT)
     k = min(ks, key=lambda x: abs(x - n))
     return REF_PER_CLIENT[k]
+
+
+REF_TRAIN_ROWS = 8000  # the reference's training split (8000 of 10 000 rows, C:239)
+
+
+def reference_rows(total: int, world: int, rank: int) -> int:
+    """Rows of ``rank``'s shard under the reference's chunking (C:57-60): chunk = max(1, total //
+    world) rows per rank, the last rank also takes the remainder."""
+    chunk = max(1, total // world)
+    if rank < world - 1:
+        return chunk
+    return total - chunk * (world - 1)
 
 
 def synth_shard(n_rows: int, rank: int, device, seed: int = 7):
@@ -147,9 +165,19 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--rows-per-client", type=int, default=8000)
+    ap.add_argument("--rows-per-client", type=int, default=0,
+                    help="rows on every client (0: the reference's chunking of --total-rows over the N clients, "
+                         "C:57-60 -- 8000 // N each, the last rank takes the remainder)")
+    ap.add_argument("--total-rows", type=int, default=REF_TRAIN_ROWS)
+    ap.add_argument("--no-weak", action="store_true",
+                    help="skip the companion run with 8000 rows on every client (weak scaling)")
+    ap.add_argument("--no-early-stop", dest="early_stop", action="store_false",
+                    help="do not evaluate the early-stop rule in the timed rounds")
+    ap.add_argument("--patience", type=int, default=0,
+                    help="early-stop patience in the timed run (0: longer than the run, so every timed round is live)")
     ap.add_argument("--hidden", type=int, nargs="+", default=[50, 200])
-    ap.add_argument("--rows-per-block", type=int, default=32)
+    ap.add_argument("--rows-per-block", type=int, default=0,
+                    help="rows per workgroup of the fused kernels (0: the engine's choice for the shard size)")
     ap.add_argument("--graph-rounds", type=int, default=0,
                     help="rounds per captured HIP graph (0: largest even divisor of --steps up to 64)")
     ap.add_argument("--backend", default="auto", choices=["auto", "xgmi", "rccl", "nccl"],
@@ -206,50 +234,77 @@ def main(argv=None):
     if N != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
     dev = comm.device
-    X, y = synth_shard(a.rows_per_client, comm.rank, dev)
     dims = [14, *a.hidden, 2]
     g = a.graph_rounds or _pick_graph_rounds(a.steps)
     # (ranks sharing one GPU: with more than two, the Adam kernels' in-kernel chunk exchange can
     # wait on a peer whose kernel cannot become resident; classic rounds there -- the record's
     # data_plane says so)
     lag_off_shared = a.share_gpu and N > 2
-    cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=a.warmup + a.steps + g + 16, early_stop=False,
-                       rows_per_block=a.rows_per_block, graph_rounds=g, dtype=a.dtype,
-                       lagged_eval=not lag_off_shared)
-    eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank),
-                         n_total=a.rows_per_client * N)
+    max_rounds = a.warmup + a.steps + g + 16
+    # the early-stop rule runs in every round; a patience above the run's length keeps every
+    # timed round live (a stop would turn the remaining rounds into no-ops)
+    patience = a.patience if a.patience > 0 else max_rounds + 1
+    if patience <= max_rounds and a.early_stop:
+        print(f"warning: patience {patience} may stop the timed region early", file=sys.stderr)
 
     def barrier():
         if N > 1:
             dist.barrier()
 
-    # warm-up: the requested rounds, then (uncounted) the graph of the timed region is
-    # captured, instantiated and replayed once, so the timed steps are steady-state replays
-    eng.run(a.warmup, check_every=max(a.warmup, 1))
-    primed = eng.prime_graph(g)
-    eng.stream.synchronize()
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    eng._issue(a.steps, close=False)  # exactly K rounds, no host polling inside
-    eng.stream.synchronize()
-    torch.cuda.synchronize(dev)
-    barrier()
-    dt = time.perf_counter() - t0
-    if N > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    eng._issue(1)  # untimed closing round: scores the last timed round
-    eng.sync_history()
+    def timed_rounds(rows_local: int, rows_total: int):
+        """Build a client with `rows_local` rows (FedAvg weight rows_local / rows_total), warm up,
+        time exactly a.steps rounds (max over ranks), close + check; returns (dt, engine, primed)."""
+        X, y = synth_shard(rows_local, comm.rank, dev)
+        cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=max_rounds, early_stop=a.early_stop,
+                           patience=patience, rows_per_block=a.rows_per_block, graph_rounds=g,
+                           dtype=a.dtype, lagged_eval=not lag_off_shared)
+        eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank), n_total=rows_total)
+        # warm-up: the requested rounds, then (uncounted) the graph of the timed region is
+        # captured, instantiated and replayed once, so the timed steps are steady-state replays
+        eng.run(a.warmup, check_every=max(a.warmup, 1))
+        primed = eng.prime_graph(g)
+        eng.stream.synchronize()
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        eng._issue(a.steps, close=False)  # exactly K rounds, no host polling inside
+        eng.stream.synchronize()
+        torch.cuda.synchronize(dev)
+        barrier()
+        dt = time.perf_counter() - t0
+        if N > 1:
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        eng._issue(1)  # untimed closing round: scores the last timed round
+        eng.sync_history()
+        h = eng.history()
+        # every timed round was live and folded (a stop would leave rounds_run short)
+        assert h["rounds_run"] == a.warmup + primed + a.steps + 1 and h["stop_round"] < 0, \
+            (h["rounds_run"], primed, h["stop_round"])
+        return dt, eng, primed
+
+    rows_local = a.rows_per_client or reference_rows(a.total_rows, N, comm.rank)
+    rows_total = a.rows_per_client * N if a.rows_per_client else a.total_rows
+    dt, eng, primed = timed_rounds(rows_local, rows_total)
     h = eng.history()
-    assert h["rounds_run"] == a.warmup + primed + a.steps + 1, (h["rounds_run"], primed)
     # every rank must hold the same global model and metric history (raises otherwise: no number
     # is reported for a run whose FedAvg was not FedAvg)
     from fedmi.parallel.consistency import check_replicas
     replicas_ok = check_replicas(comm, [eng.global_flat(), np.asarray(h["global"])])
-    samples = a.rows_per_client * N * a.steps
-    value = samples / dt
+    value = rows_total * a.steps / dt
+    # companion: per-GPU work fixed at the reference's one-client shard (8000 rows on every client)
+    weak = None
+    if not a.rows_per_client and not a.no_weak:
+        if N == 1 and rows_local == REF_TRAIN_ROWS:
+            weak = {"value": value, "us_per_round": dt / a.steps * 1e6, "rows_per_client": REF_TRAIN_ROWS}
+        else:
+            dtw, engw, _ = timed_rounds(REF_TRAIN_ROWS, REF_TRAIN_ROWS * N)
+            weak = {"value": REF_TRAIN_ROWS * N * a.steps / dtw, "us_per_round": dtw / a.steps * 1e6,
+                    "rows_per_client": REF_TRAIN_ROWS, "scaling": "weak",
+                    "replicas_consistent": check_replicas(comm, [engw.global_flat()])}
+            del engw
+    X, y = eng.X, eng.y
     anchor = None
     if not a.no_anchor:
         if comm.rank == 0:
@@ -259,7 +314,7 @@ def main(argv=None):
     if N == 1 and a.dtype != "fp32" and not a.no_fp32:
         fp32_us = fp32_round_us(X, y, dims, a)
     # rounds-to-target is measured with the same kernels (dtype) as the throughput
-    rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=cfg.lagged_eval)
+    rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=eng.cfg.lagged_eval)
     if comm.rank == 0:
         rec = {
             "metric": METRIC,
@@ -270,12 +325,15 @@ def main(argv=None):
             "warmup": a.warmup,
             "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if a.rows_per_client else "strong",
             "vs_baseline": value / (ref_per_client(N) * N),
             "dtype": a.dtype,
-            "data": f"synthetic income-shaped (device Philox), {a.rows_per_client} rows/client; random-init weights",
+            "data": (f"synthetic income-shaped (device Philox), {rows_total} training rows "
+                     + (f"({a.rows_per_client}/client)" if a.rows_per_client else
+                        f"chunked over {N} client(s) as the reference does ({rows_local} on rank {comm.rank})")
+                     + "; random-init weights"),
             "config": {"model": f"MLP {'-'.join(map(str, dims))} (reference [C])",
-                       "global_batch": a.rows_per_client * N, "seq_len": 1,
+                       "global_batch": rows_total, "seq_len": 1,
                        "parallelism": f"fedavg{N} (1 client/{'shared ' if a.share_gpu else ''}GPU, "
                                       f"{eng.aggregation} all-reduce)",
                        "data_plane": eng.aggregation + (
@@ -283,12 +341,21 @@ def main(argv=None):
                            if lag_off_shared else ""),
                        "round_design": ("fused-eval" if N == 1 else
                                         "lagged-eval+adam-fedavg" if eng.engine.adam_exchange else
+                                        "lagged-eval+late-fold" if eng.engine.late_fold else
                                         "lagged-eval" if eng.engine.lagged else "classic"),
                        "rccl_env": comm.rccl_env,
-                       "rows_per_client": a.rows_per_client, "optimizer": "Adam(0.004)+StepLR(30,0.5)",
+                       "rows_per_client": a.rows_per_client or reference_rows(a.total_rows, N, 0),
+                       "rows_last_client": a.rows_per_client or reference_rows(a.total_rows, N, N - 1),
+                       "rows_per_block": eng.R,
+                       "optimizer": "Adam(0.004)+StepLR(30,0.5)",
+                       "early_stop": {"enabled": bool(a.early_stop), "patience": patience, "atol": 1e-4,
+                                      "rtol": 1e-5, "note": "rule evaluated on the device every timed round; "
+                                      "patience longer than the run so every timed round is live"},
+                       "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
                        "graph_rounds": g, "share_gpu": bool(a.share_gpu)},
             "samples_per_sec_per_client": value / N,
             "us_per_round": dt / a.steps * 1e6,
+            "weak_8000_rows_per_client": weak,
             "torch_eager_us_per_round_1client": anchor,
             "fp32_us_per_round": fp32_us if a.dtype != "fp32" else dt / a.steps * 1e6,
             "final_train_acc_synthetic": float(h["global"][-1][0]),

@@ -73,7 +73,8 @@ class EngineConfig:
     eval_fedavg: bool = True
     # world > 1, bf16: score round r's post-step local model inside round r+1's train kernel --
     # no evaluation kernel in the round; the counts are exchanged inside round r+1's Adam
-    # kernel (one-shot xGMI) or, without early stopping, ride round r+1's all-reduce; the
+    # kernel (one-shot xGMI) or ride round r+1's all-reduce (RCCL; with early stopping a round
+    # run past the stop is discarded bit-exactly, fl_common.h FLState::late); the
     # last round of every run() evaluates itself (fl_common.h FL_EVAL_LAGGED).  Metrics,
     # history, early-stop round and weights are identical to classic rounds.
     lagged_eval: bool = True
@@ -83,6 +84,13 @@ class EngineConfig:
     # |feature| <= FP16_SLAB_MAX_ABS_X (standardised data: a partial over R <= 64 rows stays far
     # inside fp16's range), else fp32.  The fp32 kernels always use an fp32 slab.
     grad_slab: str = "auto"
+    # bf16 kernels, several clients: run the TRAINING forward pass in plain bf16 (a_hi.W_hi) instead
+    # of split-bf16 -- no round is scored from it there (lagged rounds score in registers, classic
+    # rounds in the eval kernel, both split-bf16); None = auto (on for world > 1 / emulated
+    # clients with register scoring), False = the split forward everywhere, True = on where it is
+    # valid (never for one fused client, whose evaluation IS the training forward).  The engine's
+    # layout()["plain_fwd"] reports what runs; bench records and checkpoints carry it.
+    plain_fwd: Optional[bool] = None
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -357,6 +365,20 @@ class TorchRoundEngine(RoundEngineBase):
     def sync_history(self) -> None:
         pass
 
+    def run_streaming(self, n_rounds: int, chunk: int = 16, on_history=None, guard=None) -> int:
+        """:meth:`run` round by round, ``on_history`` after every round (host-driven rounds: each
+        round's metrics are on the host as soon as it ends)."""
+        import contextlib
+        ran = 0
+        for _ in range(int(n_rounds)):
+            if self.stopper.stopped or self.rounds_issued >= self.cfg.max_rounds:
+                break
+            with (guard(f"round {self.rounds_issued}") if guard else contextlib.nullcontext()):
+                ran += self.run(1)
+            if on_history is not None:
+                on_history(self.history())
+        return ran
+
     @property
     def stopped(self) -> bool:
         return self.stopper.stopped
@@ -452,7 +474,7 @@ class TorchRoundEngine(RoundEngineBase):
 # ---------------------------------------------------------------------------------------
 _STATE_DTYPE = np.dtype([("next_round", "<i4"), ("finalized", "<i4"), ("stopped", "<i4"), ("live", "<i4"),
                          ("cur_round", "<i4"), ("count", "<i4"), ("has_prev", "<i4"), ("stop_round", "<i4"),
-                         ("calls", "<u4"), ("pad0", "<i4"), ("prev", "<f8", (4,))])
+                         ("calls", "<u4"), ("late", "<i4"), ("prev", "<f8", (4,))])
 
 
 class HipRoundEngine(RoundEngineBase):
@@ -492,8 +514,9 @@ class HipRoundEngine(RoundEngineBase):
         self.Pimg = image_layout(self.dims)[2]
         # lagged evaluation carries a second metric region after the tails (fl_common.h)
         # (emulate_clients: one process measures the multi-client round shape, tools/round_emulate.py)
-        # (with early stopping the native engine runs lagged rounds only with the Adam-fused
-        # exchange, which folds each round's metrics in time)
+        # (with early stopping the native engine runs lagged rounds with the Adam-fused exchange,
+        # which folds each round's metrics in time, or over RCCL, folded one round late with the
+        # round run past a stop discarded bit-exactly: FLEngine.late_fold)
         self._lag = ((self.world > 1 or emulate_clients) and cfg.dtype == "bf16"
                      and comm_buffers is None and bool(cfg.lagged_eval))
         comm_len = self.Pimg + self.world * self.tail_stride * (2 if self._lag else 1)
@@ -543,6 +566,7 @@ class HipRoundEngine(RoundEngineBase):
             "lagged_eval": self._lag,
             "emulate_clients": bool(emulate_clients),
             "slab_f16": self._pick_slab_f16(cfg),
+            "plain_fwd": -1 if cfg.plain_fwd is None else int(bool(cfg.plain_fwd)),
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),
@@ -715,19 +739,19 @@ class HipRoundEngine(RoundEngineBase):
         self.sync_history()
         return {k + "_us": v / max(n, 1) for k, v in acc.items()}
 
-    def _issue(self, n: int, close: bool = True) -> None:
+    def _issue(self, n: int, close: bool = True, graph_rounds: Optional[int] = None) -> None:
         """Issue rounds [rounds_issued, rounds_issued + n) on the current stream.
 
         ``close=False`` (lagged engines): the last round stays lagged -- its evaluation is
         done by the next issued round's train kernel, so every round of the call can be a
         graph replay.  The host must issue at least one more (closing) round before it reads
-        the history."""
+        the history.  ``graph_rounds``: rounds per replayed graph (default: the config's)."""
         if self.cfg.debug:
             self._issue_debug(n)
             return
         s = self._stream()
         r0 = self.rounds_issued
-        g = int(self.cfg.graph_rounds)
+        g = int(self.cfg.graph_rounds if graph_rounds is None else graph_rounds)
         if self.world > 1 and not self._engine_reduces():
             # torch-owned communicator: all-reduce from Python between rounds
             with torch.cuda.stream(self.stream):
@@ -828,6 +852,97 @@ class HipRoundEngine(RoundEngineBase):
         self.sync_history()
         return self.hist.rounds_run - before
 
+    def run_streaming(self, n_rounds: int, chunk: int = 16, on_history=None, guard=None) -> int:
+        """:meth:`run` with the metrics streamed as the rounds complete: rounds are issued in
+        chunks of ``chunk``, and after each chunk a finalize plus an asynchronous copy of the
+        round state and metric history into pinned host memory are queued behind it.  Chunk k+1
+        is issued BEFORE chunk k's copy is waited on, so the device never idles on the host, and
+        ``on_history(history)`` sees round r while at most one chunk (<= ``chunk`` rounds) runs
+        after it (the reference prints every round as it completes, C:139-179).  ``guard(desc)``:
+        optional context manager around each chunk (the collective watchdog).  Returns the number
+        of live rounds; rounds issued past an early stop are exact no-ops on the device."""
+        import contextlib
+        before = self.hist.rounds_run
+        left = min(int(n_rounds), self.cfg.max_rounds - self.rounds_issued)
+        if self.cfg.debug or (self.world > 1 and not self._engine_reduces()):
+            while left > 0 and not self._stopped_seen:   # host-driven rounds: chunk by chunk
+                n = min(chunk, left)
+                with (guard(f"rounds {self.rounds_issued}..{self.rounds_issued + n - 1}") if guard
+                      else contextlib.nullcontext()):
+                    self.run(n, check_every=n)
+                left -= n
+                if on_history is not None:
+                    on_history(self.history())
+            return self.hist.rounds_run - before
+        # graph rounds per chunk: lagged engines close every chunk with an eager self-evaluating
+        # round, so their graphs leave room for it (graph + lagged + closing round)
+        g = int(self.cfg.graph_rounds)
+        if g >= 2:
+            gs = max(2, (min(g, chunk) - (2 if self.engine.lagged else 0)) & ~1)
+            step = gs + (2 if self.engine.lagged else 0)
+        else:
+            gs, step = 0, max(1, chunk)
+        mirror = self._host_mirror()
+        s = self._stream()
+        pend = None
+        slot = 0
+        while True:
+            new = None
+            if left > 0 and not self._stopped_seen:
+                n = min(step, left)
+                desc = f"rounds {self.rounds_issued}..{self.rounds_issued + n - 1}"
+                with (guard(desc) if guard else contextlib.nullcontext()):
+                    self._issue(n, graph_rounds=gs)
+                left -= n
+                r = self.rounds_issued
+                self.engine.finalize(r, s)
+                m = mirror[slot]
+                with torch.cuda.stream(self.stream):
+                    m["state"].copy_(self.state[(r + 1) & 1], non_blocking=True)
+                    m["glob"].copy_(self.h_global, non_blocking=True)
+                    m["rank"].copy_(self.h_rank, non_blocking=True)
+                    m["loss"].copy_(self.h_loss, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+                new = (ev, slot, desc)
+                slot ^= 1
+            if pend is not None:
+                with (guard(pend[2]) if guard else contextlib.nullcontext()):
+                    pend[0].synchronize()
+                self._fold_mirror(mirror[pend[1]])
+                if on_history is not None:
+                    on_history(self.history())
+            pend = new
+            if pend is None:
+                break
+        if self._peer is not None:
+            from ..parallel.peer import check_peer_error
+            check_peer_error(self._peer)
+        self._check_slab_saturation()
+        return self.hist.rounds_run - before
+
+    def _host_mirror(self):
+        """Two pinned-host copies (double-buffered by chunk) of the round state and history."""
+        if getattr(self, "_mirror", None) is None:
+            pin = torch.cuda.is_available()
+            mk = lambda t: torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+            self._mirror = [{"state": mk(self.state[0]), "glob": mk(self.h_global), "rank": mk(self.h_rank),
+                             "loss": mk(self.h_loss)} for _ in range(2)]
+        return self._mirror
+
+    def _fold_mirror(self, m) -> None:
+        st = m["state"].numpy().view(_STATE_DTYPE)[0]
+        n = int(st["finalized"])
+        self.hist.rounds_run = n
+        if n:
+            self.hist.glob[:n] = m["glob"][:n * 4].numpy().reshape(n, 4)
+            self.hist.rank[:n] = m["rank"][:n * self.world * 4].numpy().reshape(n, self.world, 4)
+            self.hist.loss[:n] = m["loss"][:n].numpy()
+        if st["stopped"]:
+            self.hist.stop_round = int(st["stop_round"])
+            self.hist.stop_trigger = int(st["stop_round"]) - 1
+            self._stopped_seen = True
+
     @property
     def stopped(self) -> bool:
         return self._stopped_seen
@@ -853,6 +968,9 @@ class HipRoundEngine(RoundEngineBase):
             self.hist.stop_round = int(st["stop_round"])
             self.hist.stop_trigger = int(st["stop_round"]) - 1
             self._stopped_seen = True
+        self._check_slab_saturation()
+
+    def _check_slab_saturation(self) -> None:
         if self.slab_f16 and not self.slab_saturated and int(self.sat.item()):
             self.slab_saturated = True
             msg = ("fp16 gradient slab saturated (a per-workgroup partial reached +-65504 or is not finite): the "

@@ -14,7 +14,8 @@ Differences by design (each switchable):
   :meth:`evaluate_global`.
 * ``train_and_evaluate`` does not bounce through the host every round: the engine runs
   the whole loop (device-side early stop, one all-reduce per round) and the reference
-  console lines are printed from the metric history afterwards / per chunk.
+  console lines are printed from the metric history as chunks of <= 16 rounds complete
+  (pinned-host mirror read while the next chunk runs, ``HipRoundEngine.run_streaming``).
 """
 from __future__ import annotations
 
@@ -91,7 +92,7 @@ class FederatedMLPLearning:
 
     def train_and_evaluate(self, comm=None, rounds: int = 5, termination_patience: int = 10,
                            tolerance: float = 1e-4, verbose: bool = True, chunk: int = 64,
-                           fault=None, watchdog_s: float = 0.0):
+                           fault=None, watchdog_s: float = 0.0, stream_chunk: int = 16):
         """Multi-round FedAvg with early stopping (C:122-207).  Returns the reference's
         ``global_metrics`` dict of per-round lists.
 
@@ -106,20 +107,32 @@ class FederatedMLPLearning:
         printed = eng.hist.rounds_run
         abort = (comm.Abort if comm is not None and hasattr(comm, "Abort") else (lambda: None))
         wd = Watchdog(watchdog_s, abort, rank=self.rank)
+        # verbose: the console follows the rounds as they complete (every rank runs the same
+        # chunking -- the collectives of the rounds must match -- and rank 0 prints):
+        # run_streaming keeps one chunk of <= `stream_chunk` rounds in flight behind the printed ones
+        stream = verbose and hasattr(eng, "run_streaming")
+
+        def on_history(h):
+            nonlocal printed
+            if self.rank == 0:
+                printed = print_history(h, termination_patience, start=printed)
         try:
             left = rounds - eng.rounds_issued
             while left > 0 and not eng.stopped:
-                n = min(chunk, left)
+                n = left if stream else min(chunk, left)
                 if fault is not None and fault.applies(self.rank):
                     to_fault = fault.round - eng.rounds_issued
                     if to_fault <= 0:
                         fault.trigger(self.rank, eng.rounds_issued)
                     n = min(n, to_fault)
-                with wd.guard(f"rounds {eng.rounds_issued}..{eng.rounds_issued + n - 1}"):
-                    eng.run(n)
+                if stream:
+                    eng.run_streaming(n, chunk=stream_chunk, on_history=on_history, guard=wd.guard)
+                else:
+                    with wd.guard(f"rounds {eng.rounds_issued}..{eng.rounds_issued + n - 1}"):
+                        eng.run(n)
+                    if verbose and self.rank == 0:
+                        printed = print_history(eng.history(), termination_patience, start=printed)
                 left -= n
-                if verbose and self.rank == 0:
-                    printed = print_history(eng.history(), termination_patience, start=printed)
         except Exception as e:  # reference C:203-205
             print(f"Rank {self.rank} encountered an error: {e}", flush=True)
             if comm is not None and hasattr(comm, "Abort") and getattr(comm, "size", 1) > 1:

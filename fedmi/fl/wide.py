@@ -39,7 +39,7 @@ WIDE_LR = 1e-4
 
 class WideClient:
     def __init__(self, X: torch.Tensor, y: torch.Tensor, dims: Sequence[int], comm=None, n_total: Optional[int] = None,
-                 micro_batch: int = 131072, lr: float = 0.004, betas=(0.9, 0.999), eps: float = 1e-8,
+                 micro_batch: int = 131072, lr: Optional[float] = None, betas=(0.9, 0.999), eps: float = 1e-8,
                  step_size: int = 30, gamma: float = 0.5, seed: int = 0, dtype: str = "bf16",
                  eval_rows: int = 0, allreduce_dtype: str = "fp32", warmup_rounds: int = 0,
                  fused_eval: Optional[bool] = None):
@@ -55,7 +55,8 @@ class WideClient:
         self.n_total = n_total or self.n * self.world
         self.agg = self.n / self.n_total
         self.mb = min(micro_batch, self.n)
-        self.lr, self.betas, self.eps = lr, betas, eps
+        # (None: WIDE_LR -- the reference's 0.004 diverges at width 4096, see WIDE_LR)
+        self.lr, self.betas, self.eps = (WIDE_LR if lr is None else float(lr)), betas, eps
         self.step_size, self.gamma = step_size, gamma
         # linear LR warm-up over the first rounds (0: none, the reference's schedule), then StepLR
         self.warmup_rounds = int(warmup_rounds)
@@ -554,47 +555,71 @@ def run_wide_fedavg(comm, dims: Sequence[int], rows_per_client: int, rounds: int
 
 
 def save_wide(path: str, client: WideClient) -> None:
-    """Wide-client checkpoint (rank 0 writes the global weights, every rank its Adam state):
-    ``weights.safetensors`` under the reference's ``model.{2i}.weight`` [out, in] / ``.bias`` keys
-    (C:93-94), ``client{r}.safetensors`` with the flat fp32 Adam moments, ``wide_meta.json`` with the
-    dims and the round (= StepLR epoch and Adam step; every wide client trains every round)."""
-    import json
+    """Wide-client checkpoint (rank 0 writes the global weights, every rank its Adam state), as
+    a round-tagged set (fedmi/ckpt/checkpoint.py ``tagged``): ``weights.r<R>.safetensors`` under the
+    reference's ``model.{2i}.weight`` [out, in] / ``.bias`` keys (C:93-94),
+    ``client{r}.r<R>.safetensors`` with the flat fp32 Adam moments, and -- last, after a barrier --
+    ``wide_meta.json`` with the dims, the round (= StepLR epoch and Adam step; every wide client
+    trains every round) and the set's file names.  A pending fused evaluation is scored first, so
+    :meth:`WideClient.metrics` after the save reports the round it was requested for."""
     import os
-    from ..ckpt.checkpoint import save_weights
+    from ..ckpt.checkpoint import _atomic, _prune, _publish_meta, save_weights, tagged
     from ..models.mlp import flat_to_dict
     from safetensors.numpy import save_file
+    if client._eval_pending:
+        client._evaluate_now()
     client.sync()
     client.stream.synchronize()
     rank = client.comm.rank if client.comm is not None else 0
+    multi = client.comm is not None and client.world > 1
+    R = int(client.round)
     os.makedirs(path, exist_ok=True)
-    save_file({"exp_avg": client.m_.cpu().numpy(), "exp_avg_sq": client.v_.cpu().numpy()},
-              os.path.join(path, f"client{rank}.safetensors"))
+    m_, v_ = client.m_.cpu().numpy(), client.v_.cpu().numpy()
+    cname = f"client{rank}.safetensors"
+    _atomic(os.path.join(path, tagged(cname, R)),
+            lambda tmp: save_file({"exp_avg": m_, "exp_avg_sq": v_}, tmp, metadata={"round": str(R)}))
     if rank == 0:
-        save_weights(os.path.join(path, "weights.safetensors"), flat_to_dict(client.params.cpu().numpy(), client.dims))
-        with open(os.path.join(path, "wide_meta.json"), "w") as f:
-            json.dump({"format": "fedmi-wide-ckpt-1", "dims": client.dims, "round": int(client.round),
-                       "world": client.world, "lr": client.lr, "step_size": client.step_size,
-                       "gamma": client.gamma}, f)
-    if client.comm is not None and client.world > 1:
+        w = flat_to_dict(client.params.cpu().numpy(), client.dims)
+        _atomic(os.path.join(path, tagged("weights.safetensors", R)), lambda tmp: save_weights(tmp, w, R))
+    if multi:
         client.comm.Barrier()
+    if rank == 0:
+        _publish_meta(path, {"format": "fedmi-wide-ckpt-2", "dims": client.dims, "round": R,
+                             "files": {"weights": tagged("weights.safetensors", R),
+                                       "client": tagged("client{rank}.safetensors", R)},
+                             "world": client.world, "lr": client.lr, "step_size": client.step_size,
+                             "gamma": client.gamma}, name="wide_meta.json")
+    if multi:
+        client.comm.Barrier()
+    _prune(path, cname, R)
+    if rank == 0:
+        _prune(path, "weights.safetensors", R)
 
 
 def load_wide(path: str, client: WideClient) -> int:
-    """Restore :func:`save_wide` into a client of the same dims / client count; returns the round."""
+    """Restore :func:`save_wide` into a client of the same dims / client count; returns the round.
+    A pending fused evaluation of the client's current model is scored before it is replaced."""
     import json
     import os
-    from ..ckpt.checkpoint import load_weights
+    from ..ckpt.checkpoint import _check_round, load_weights
     from ..models.mlp import dict_to_flat
     from safetensors.numpy import load_file
     with open(os.path.join(path, "wide_meta.json")) as f:
         meta = json.load(f)
-    if meta.get("format") != "fedmi-wide-ckpt-1" or list(meta["dims"]) != client.dims:
+    fmt = meta.get("format")
+    if fmt not in ("fedmi-wide-ckpt-1", "fedmi-wide-ckpt-2") or list(meta["dims"]) != client.dims:
         raise ValueError(f"{path}: not a wide checkpoint for dims {client.dims}")
     if int(meta["world"]) != client.world:
         raise ValueError(f"{path}: saved with {meta['world']} clients, this run has {client.world}")
+    R = int(meta["round"]) if fmt == "fedmi-wide-ckpt-2" else None
+    files = meta.get("files", {"weights": "weights.safetensors", "client": "client{rank}.safetensors"})
     rank = client.comm.rank if client.comm is not None else 0
-    flat = dict_to_flat(load_weights(os.path.join(path, "weights.safetensors")), client.dims)
-    st = load_file(os.path.join(path, f"client{rank}.safetensors"))
+    flat = dict_to_flat(load_weights(os.path.join(path, files["weights"]), expect_round=R), client.dims)
+    cp = os.path.join(path, files["client"].format(rank=rank))
+    _check_round(cp, R)
+    st = load_file(cp)
+    if client._eval_pending:
+        client._evaluate_now()
     client.sync()
     with torch.cuda.stream(client.stream):
         client.params.copy_(torch.as_tensor(flat, device=client.dev))
@@ -602,7 +627,6 @@ def load_wide(path: str, client: WideClient) -> int:
         client.v_.copy_(torch.as_tensor(st["exp_avg_sq"], device=client.dev))
         if client.gprev is not None:
             client.gprev.copy_(client.params)
-    client._eval_pending = False  # (an evaluation of the replaced weights)
     client._quantize()
     client.stream.synchronize()
     client.round = int(meta["round"])

@@ -105,51 +105,96 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
 
 
 def _trial_file(r: TrialResult) -> str:
-    return "trial_h" + "-".join(str(h) for h in r.hidden) + f"_lr{r.lr:g}.safetensors"
+    # repr(lr): the shortest string that round-trips the float, so nearby grid rates never share a file
+    return "trial_h" + "-".join(str(h) for h in r.hidden) + f"_lr{float(r.lr)!r}.safetensors"
+
+
+def _trial_tag(r: TrialResult) -> str:
+    return "-".join(str(h) for h in r.hidden) + "|" + repr(float(r.lr))
+
+
+def _run_key(meta: dict) -> str:
+    """The run settings a trial file belongs to (sweep.json's metadata, without the trial list)."""
+    import json
+    return json.dumps({k: v for k, v in meta.items() if k not in ("trials", "best")}, sort_keys=True, default=str)
 
 
 def save_sweep(path: str, results: Sequence[TrialResult], best: Optional[TrialResult], meta: dict) -> None:
     """[H] checkpoint: every trial's metrics (JSON) + the best trial's averaged weights in the
     reference's coefs_ + intercepts_ layout (H:119, H:130-132) as ``best.safetensors``.
-    Incremental: called after every finished trial (hyperparameters_tuning.py), it writes only
-    the weights files it has not written yet (named by the trial's grid key) and then replaces
-    ``sweep.json`` atomically, so a crash part-way leaves a resumable sweep of the trials done."""
+    Incremental: called after every finished trial (hyperparameters_tuning.py).  A trial's weights
+    file is skipped only when the directory's current ``sweep.json`` is of THIS run (same metadata)
+    and already lists that file; anything else is (re)written to a temporary name and renamed, so a
+    directory left by another run never lends its weights to this one.  Every file's
+    header names its trial and run, checked by :func:`load_sweep`; ``sweep.json`` is replaced last,
+    atomically, so a crash part-way leaves a resumable sweep of the trials done."""
     import json
     import os
-    from ..ckpt.checkpoint import save_sklearn_weights
+    from ..ckpt.checkpoint import _publish_meta
+    from safetensors.numpy import save_file
     os.makedirs(path, exist_ok=True)
-    # every trial's averaged weights, so a resumed sweep can still return any of them as the best
+    # one result per (hidden, lr), the latest: a resumed, partly-done hidden config retrains some
+    # rates that `done` already holds
+    uniq = {}
     for r in results:
-        fp = os.path.join(path, _trial_file(r))
-        if not os.path.isfile(fp):
-            tmp = fp + ".tmp"
-            save_sklearn_weights(tmp, r.weights)
-            os.replace(tmp, fp)
+        uniq[(tuple(r.hidden), float(r.lr))] = r
+    results = list(uniq.values())
+    key = _run_key(meta)
+    trusted = set()
+    sj = os.path.join(path, "sweep.json")
+    if os.path.isfile(sj):
+        try:
+            with open(sj) as f:
+                old = json.load(f)
+            if _run_key(old) == key:
+                trusted = {t.get("file") for t in old.get("trials", [])}
+        except (OSError, ValueError):
+            trusted = set()
+
+    def write(fp, w, tag):
+        ws = [np.ascontiguousarray(np.asarray(x, dtype=np.float64)) for x in w]
+        L = len(ws) // 2
+        t = {f"coefs_.{i}": ws[i] for i in range(L)}
+        t.update({f"intercepts_.{i}": ws[L + i] for i in range(L)})
+        tmp = fp + f".tmp{os.getpid()}"
+        save_file(t, tmp, metadata={"trial": tag, "run": key})
+        os.replace(tmp, fp)
+
+    for r in results:
+        name = _trial_file(r)
+        fp = os.path.join(path, name)
+        if name not in trusted or not os.path.isfile(fp):
+            write(fp, r.weights, _trial_tag(r))
     if best is not None:
-        save_sklearn_weights(os.path.join(path, "best.safetensors.tmp"), best.weights)
-        os.replace(os.path.join(path, "best.safetensors.tmp"), os.path.join(path, "best.safetensors"))
+        write(os.path.join(path, "best.safetensors"), best.weights, _trial_tag(best))
     rows = [{"hidden": list(r.hidden), "lr": r.lr, "local": r.local, "global": r.global_, "n_iter": r.n_iter,
              "file": _trial_file(r)} for r in results]
-    tmp = os.path.join(path, "sweep.json.tmp")
-    with open(tmp, "w") as f:
-        json.dump(dict(meta, trials=rows, best={"hidden": list(best.hidden), "lr": best.lr} if best else None), f)
-    os.replace(tmp, os.path.join(path, "sweep.json"))
+    _publish_meta(path, dict(meta, trials=rows, best={"hidden": list(best.hidden), "lr": best.lr} if best else None),
+                  name="sweep.json")
 
 
 def load_sweep(path: str, expect: Optional[dict] = None) -> List[TrialResult]:
     """Trials of a saved sweep.  ``expect``: run settings (world, max_iter, data digest, ...)
     that must equal the saved ones -- trials of a different run must not mix into this one's
-    best-trial selection."""
+    best-trial selection.  Each weights file must carry its trial's and this run's tag."""
     import json
     import os
+    from safetensors import safe_open
     from ..ckpt.checkpoint import load_sklearn_weights
     with open(os.path.join(path, "sweep.json")) as f:
         m = json.load(f)
     for k, v in (expect or {}).items():
         if m.get(k) != v:
             raise ValueError(f"{path}: saved with {k}={m.get(k)!r}, this run has {k}={v!r}; not resuming")
+    key = _run_key(m)
     out = []
     for i, r in enumerate(m["trials"]):
-        w = load_sklearn_weights(os.path.join(path, r.get("file", f"trial{i}.safetensors")))
-        out.append(TrialResult(tuple(r["hidden"]), float(r["lr"]), r["local"], r["global"], int(r["n_iter"]), w))
+        fp = os.path.join(path, r.get("file", f"trial{i}.safetensors"))
+        res = TrialResult(tuple(r["hidden"]), float(r["lr"]), r["local"], r["global"], int(r["n_iter"]), [])
+        with safe_open(fp, framework="numpy") as f:
+            md = f.metadata() or {}
+        if "trial" in md and (md["trial"] != _trial_tag(res) or md.get("run") != key):
+            raise ValueError(f"{fp}: weights of trial {md['trial']!r} of another run, not of {_trial_tag(res)!r}")
+        res.weights = load_sklearn_weights(fp)
+        out.append(res)
     return out

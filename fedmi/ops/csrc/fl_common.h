@@ -189,7 +189,12 @@ struct FLState {
     int has_prev;
     int stop_round;     // round index at which the stop took effect (-1 = none)
     unsigned calls;     // Adam-fused FedAvg exchanges done (call index of the chunk flags, peer_device.h)
-    int pad0;
+    // 1: this round's fold found a stop triggered by round next_round - 2 (lag region A folded one
+    // round late: lagged rounds over an external all-reduce with early stopping), so round
+    // next_round - 1 ran past the stop.  Its output is discarded: the round republishes the image
+    // still held by its own comm buffer -- round next_round - 2's all-reduced output (the comm
+    // buffer of round q is the output buffer of round q - 2) -- instead of its input.
+    int late;
     double prev[4];     // prev_metric (C:126)
 };
 
@@ -246,7 +251,9 @@ struct FLBuffers {
 //                     of round r's exchange, so no round needs a separate evaluation kernel.
 //                     With the Adam-fused exchange region A is exchanged and folded inside
 //                     round r's Adam kernel (in time for early stopping); riding an external
-//                     all-reduce it is folded one round later (early stopping off).
+//                     all-reduce (RCCL) it is folded one round later, by round r+1's Adam
+//                     kernel -- with early stopping round r runs before round r-1's stop is
+//                     known and is then discarded bit-exactly (FLState::late).
 #define FL_EVAL_LAGGED 3
 // Metric regions of an all-reduced comm buffer that a fold consumes (fl_device.h).
 #define FL_FOLD_A 1  // lag region: round next_round - 2
@@ -309,9 +316,11 @@ hipError_t fl_launch_adam_ll(const MLPDesc& d, const FLConfig& c, const FLBuffer
                              int xchg, int afold, hipStream_t s);
 hipError_t fl_launch_eval(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
                           const float* params, float* comm, const FLState* st, hipStream_t s);
+// `prev_out` (may be null): the other parameter buffer -- the round before pg's output.  When
+// the fold finds a late stop (FLState::late) pg's image is replaced by it.
 hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b,
-                              const float* pg, const FLState* st_in, FLState* st_out,
-                              hipStream_t s, int mask = FL_FOLD_B);
+                              float* pg, const FLState* st_in, FLState* st_out,
+                              hipStream_t s, int mask = FL_FOLD_B, const float* prev_out = nullptr);
 // bf16-operand variants (split-bf16 forward, bf16 backward, fp32 accumulate, fp32 master
 // weights / slab / Adam state).
 hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,

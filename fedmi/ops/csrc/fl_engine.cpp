@@ -205,17 +205,20 @@ class FLEngine {
         comm_len_ = d_.Pimg + c_.tail_len * (lag_req ? 2 : 1);
         const bool emulate = cfg.contains("emulate_clients") && cfg["emulate_clients"].cast<bool>();
         emulate_ = emulate;
-        // (with early stopping the rounds are lagged only when the FedAvg runs inside the Adam
-        // kernel, which then also exchanges and folds the metrics in time: see lagged())
+        // (with early stopping the rounds are lagged when the FedAvg runs inside the Adam kernel,
+        // which folds the metrics in time, or rides RCCL, folded one round late: see lagged())
         // (the lagged train kernel scores the previous local model in the train layout itself)
         lag_ok_ = lag_req && dtype_ == 1 && (c_.world > 1 || emulate) && !fused_;
         // several clients + register scoring: the training forward pass is plain bf16 (no round
-        // scores from it), in every round kind of the engine alike (lagged, classic, step API);
-        // FEDMI_PLAIN_FWD=0 keeps the split forward (A/B)
+        // scores from it), in every round kind of the engine alike (lagged, classic, step API).
+        // cfg["plain_fwd"] (EngineConfig.plain_fwd): -1 auto, 0 off, 1 on wherever valid;
+        // FEDMI_PLAIN_FWD=0 forces the split forward (A/B builds)
         {
+            const int req = cfg.contains("plain_fwd") ? cfg["plain_fwd"].cast<int>() : -1;
             const char* pf = std::getenv("FEDMI_PLAIN_FWD");
-            c_.plain_fwd = (dtype_ == 1 && (c_.world > 1 || emulate) && e_.lag_reg && !fused_ &&
-                            !(pf != nullptr && pf[0] == '0')) ? 1 : 0;
+            const bool valid = dtype_ == 1 && e_.lag_reg && !fused_;
+            const bool want = req < 0 ? (c_.world > 1 || emulate) : req > 0;
+            c_.plain_fwd = (valid && want && !(pf != nullptr && pf[0] == '0')) ? 1 : 0;
         }
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
@@ -301,7 +304,8 @@ class FLEngine {
         if (rec_ != nullptr)
             rec_->push_back({FLLaunchRec::FINALIZE, {mask, 0, 0, 0}, {pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1]}});
         else
-            HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s, mask));
+            HIP_CHECK(fl_launch_finalize(d_, c_, b_, pbuf_[r & 1], st_[r & 1], st_[(r + 1) & 1], s, mask,
+                                         late_fold() ? pbuf_[(r + 1) & 1] : nullptr));
         cm_in_tail_ = false;
     }
 
@@ -315,6 +319,7 @@ class FLEngine {
         hipStream_t s = as_stream(stream);
         const bool pend = pending_cm_, tail = cm_in_tail_, plag = prev_lagged_, pscore = prev_scored_,
                    pafold = prev_afold_;
+        const long long ev0 = eval_launches_;
         HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
             for (int r = 0; r < n; ++r) issue_round(r, s, comm, true, lagged());
@@ -327,11 +332,14 @@ class FLEngine {
             prev_lagged_ = plag;
             prev_scored_ = pscore;
             prev_afold_ = pafold;
+            eval_launches_ = ev0;
             throw;
         }
         HIP_CHECK(hipStreamEndCapture(s, &graph_));
         HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
         graph_rounds_ = n;
+        graph_evals_ = eval_launches_ - ev0;  // counted per replay, not at capture
+        eval_launches_ = ev0;
         pending_cm_ = pend;  // nothing ran yet: replay() applies the rounds' effect
         cm_in_tail_ = tail;
         prev_lagged_ = plag;
@@ -343,6 +351,7 @@ class FLEngine {
         if (!exec_) throw std::runtime_error("replay: no captured graph");
         if (needs_eager_round()) throw std::runtime_error("replay: issue one eager round first");
         HIP_CHECK(hipGraphLaunch(exec_, as_stream(stream)));
+        eval_launches_ += graph_evals_;
         pending_cm_ = fused_;
         cm_in_tail_ = !fused_;
         prev_lagged_ = lagged();
@@ -351,6 +360,9 @@ class FLEngine {
     }
 
     int graph_rounds() const { return graph_rounds_; }
+    // Stand-alone evaluation kernels issued so far (eager launches + every graph replay's):
+    // a one-client fused run launches one per host-side weight change / run end, not per round.
+    long long eval_launches() const { return eval_launches_; }
 
     // Host-side round bookkeeping (which metrics the last issued round left pending) as a bit
     // set.  A caller that captures rounds of this engine into its own graph (a trial group)
@@ -377,8 +389,13 @@ class FLEngine {
         return fused_ ? cm_in_tail_ : pending_cm_;
     }
     // Lagged rounds: allowed by the layout, and either no early stopping (metrics may be
-    // folded one round late) or the Adam-fused exchange (which folds them in time).
-    bool lagged() const { return lag_ok_ && (!c_.es_enabled || xchg_); }
+    // folded one round late), the Adam-fused exchange (which folds them in time) or an
+    // external all-reduce (RCCL: folded one round late, a round run past a stop is discarded
+    // bit-exactly -- late_fold()).  A peer all-reduce kernel without the in-kernel exchange
+    // (several local steps) keeps classic rounds with early stopping: its send buffer is not the
+    // output buffer a late stop republishes from.
+    bool lagged() const { return lag_ok_ && (!c_.es_enabled || xchg_ || peer_ == nullptr); }
+    bool late_fold() const { return lagged() && c_.es_enabled && !xchg_; }
     bool adam_exchange() const { return xchg_; }
     bool fused() const { return fused_; }
 
@@ -539,6 +556,10 @@ class FLEngine {
                 rec_->push_back({FLLaunchRec::TRAIN, {ls, 0, mode, fold_mask}, {pg, si, so, cm_out}});
             else
                 HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s, mode, cm_out, fold_mask));
+            // (the fp32 kernels read the fp32 image directly: nothing to repack, but the flag
+            // also tells issue_train that the host replaced the weights -- consumed here, or
+            // every fused round would flush a separate evaluation)
+            need_pack_ = false;
         } else {
             // the round's input weights -> packed bf16 image.  With one client the FedAvg
             // output IS the local model (agg_scale = 1), which the Adam kernel already packed,
@@ -570,6 +591,7 @@ class FLEngine {
                                  fold, tail_a, fold_mask, peer, wx, afold));
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
+        ++eval_launches_;
         if (rec_ != nullptr) {
             rec_->push_back({FLLaunchRec::EVAL, {0, 0, 0, 0}, {params, comm, st}});
             return;
@@ -720,6 +742,8 @@ class FLEngine {
     hipGraph_t graph_ = nullptr;
     hipGraphExec_t exec_ = nullptr;
     int graph_rounds_ = 0;
+    long long eval_launches_ = 0;  // see eval_launches()
+    long long graph_evals_ = 0;    // evaluation kernels inside the captured graph
     std::vector<FLLaunchRec>* rec_ = nullptr;  // TrialBatch: record launches instead of issuing them
 };
 
@@ -982,6 +1006,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("flags", &FLEngine::flags)
         .def("set_flags", &FLEngine::set_flags)
         .def("graph_rounds", &FLEngine::graph_rounds)
+        .def_property_readonly("eval_launches", &FLEngine::eval_launches)
         .def("time_kernels", &FLEngine::time_kernels)
         .def("set_debug", &FLEngine::set_debug)
         .def("invalidate", &FLEngine::invalidate)
@@ -993,6 +1018,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def_property_readonly("fused", &FLEngine::fused)
         .def_property_readonly("lagged", &FLEngine::lagged)
         .def_property_readonly("adam_exchange", &FLEngine::adam_exchange)
+        .def_property_readonly("late_fold", &FLEngine::late_fold)
         .def("launch_one", &FLEngine::launch_one)
         .def("confusion", &FLEngine::confusion)
         .def("layout", &FLEngine::layout);

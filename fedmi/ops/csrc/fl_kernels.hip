@@ -396,12 +396,22 @@ fl_eval_fedavg_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restric
     }
 }
 
-__global__ void fl_finalize_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pg,
-                                   const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int mask) {
+__global__ void fl_finalize_kernel(MLPDesc d, FLConfig c, FLBuffers b, float* __restrict__ pg,
+                                   const FLState* __restrict__ st_in, FLState* __restrict__ st_out, int mask,
+                                   const float* __restrict__ prev_out) {
     if (blockIdx.x != 0) return;
-    FLState S = finalize_state(d, c, b, pg, *st_in, true, mask);
+    const FLState Sin = *st_in;
+    FLState S = finalize_state(d, c, b, pg, Sin, true, mask);
+    // a stop found one round late (fold of region A, FLState::late): the last round ran past it;
+    // its output image is replaced by the round before's, still intact in the other buffer
+    int late = (threadIdx.x == 0 && !Sin.stopped && S.stopped && S.stop_round < Sin.next_round) ? 1 : 0;
+    late = __shfl(late, 0, 64);
+    if (late && prev_out != nullptr)
+        for (int i = threadIdx.x * 4; i < d.Pimg; i += 64 * 4)
+            *reinterpret_cast<float4*>(pg + i) = *reinterpret_cast<const float4*>(prev_out + i);
     if (threadIdx.x != 0) return;
     S.live = 0;
+    S.late = late;
     *st_out = S;
 }
 
@@ -586,9 +596,10 @@ hipError_t fl_launch_eval_fedavg(const MLPDesc& d, const FLConfig& c, const FLBu
     return hipGetLastError();
 }
 
-hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pg,
-                              const FLState* si, FLState* so, hipStream_t s, int mask) {
-    hipLaunchKernelGGL(fl_finalize_kernel, dim3(1), dim3(64), 0, s, d, c, b, pg, si, so, mask);
+hipError_t fl_launch_finalize(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, float* pg,
+                              const FLState* si, FLState* so, hipStream_t s, int mask, const float* prev_out) {
+    if ((d.Pimg & 3) != 0) return hipErrorInvalidValue;  // the image copy moves float4s
+    hipLaunchKernelGGL(fl_finalize_kernel, dim3(1), dim3(64), 0, s, d, c, b, pg, si, so, mask, prev_out);
     return hipGetLastError();
 }
 

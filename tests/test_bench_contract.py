@@ -25,11 +25,33 @@ def _run(args, n=1, timeout=300):
     return rec
 
 
+def test_reference_chunking():
+    """bench.py's shards follow the reference's _split_data chunking (C:57-60): 8000 // N rows per
+    client, the last rank takes the remainder -- BASELINE.md's k-columns' shard sizes."""
+    sys.path.insert(0, ROOT)
+    from bench import REF_TRAIN_ROWS, reference_rows
+    assert REF_TRAIN_ROWS == 8000
+    for n, rows in ((1, 8000), (2, 4000), (4, 2000), (8, 1000)):
+        assert [reference_rows(8000, n, r) for r in range(n)] == [rows] * n
+    assert [reference_rows(8000, 3, r) for r in range(3)] == [2666, 2666, 2668]
+    assert sum(reference_rows(10, 4, r) for r in range(4)) == 10
+
+
+def _check_headline_config(rec, n):
+    c = rec["config"]
+    assert c["rows_per_client"] == 8000 // n and c["global_batch"] == 8000
+    assert rec["scaling"] == "strong"
+    assert c["early_stop"]["enabled"] is True and c["early_stop"]["patience"] > rec["steps"] + rec["warmup"]
+    weak = rec["weak_8000_rows_per_client"]
+    assert weak["rows_per_client"] == 8000 and weak["value"] > 0
+
+
 @pytest.mark.gpu
 def test_bench_headline_contract():
     rec = _run(["--steps", "50", "--warmup", "10", "--no-convergence"])
     assert rec["steps"] == 50 and rec["warmup"] == 10 and rec["dtype"] == "bf16"
     assert rec["vs_baseline"] > 0 and rec["replicas_consistent"] is True
+    _check_headline_config(rec, 1)
 
 
 @pytest.mark.gpu
@@ -42,6 +64,8 @@ def test_bench_self_launch_shared_gpu():
     assert rec["config"]["data_plane"] == "xgmi-oneshot+adam", rec["config"]
     assert rec["config"]["share_gpu"] is True
     assert rec["replicas_consistent"] is True
+    _check_headline_config(rec, 2)
+    assert rec["weak_8000_rows_per_client"]["replicas_consistent"] is True
 
 
 @pytest.mark.gpu
@@ -55,6 +79,7 @@ def test_bench_self_launch_eight_ranks_shared_gpu():
     assert rec["config"]["data_plane"].startswith("xgmi-oneshot (classic rounds"), rec["config"]
     assert rec["config"]["round_design"] == "classic"
     assert rec["replicas_consistent"] is True
+    _check_headline_config(rec, 8)
 
 
 @pytest.mark.gpu

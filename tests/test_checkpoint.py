@@ -44,7 +44,12 @@ def test_checkpoint_layout_is_reference_state_dict(tmp_path):
     e = _engine(X, y, dims)
     e.run(2)
     save_checkpoint(str(tmp_path), e)
-    assert sorted(os.listdir(tmp_path)) == ["client0.safetensors", "meta.json", "weights.safetensors"]
+    assert sorted(os.listdir(tmp_path)) == ["client0.r2.safetensors", "meta.json", "weights.r2.safetensors",
+                                            "weights.safetensors"]
+    e.run(1)
+    save_checkpoint(str(tmp_path), e)   # the next round's set replaces (prunes) round 2's
+    assert sorted(os.listdir(tmp_path)) == ["client0.r3.safetensors", "meta.json", "weights.r3.safetensors",
+                                            "weights.safetensors"]
     ck = load_checkpoint(str(tmp_path), rank=0)
     model = MLPModel(14, [50, 200], 2)
     # plain torch load of the reference key names: model.{0,2,4}.{weight,bias}
@@ -54,7 +59,54 @@ def test_checkpoint_layout_is_reference_state_dict(tmp_path):
     ref.load_state_dict({k.split("model.", 1)[1]: v for k, v in sd.items()})
     assert set(ck["weights"]) == {n for n, _ in model.named_parameters()}
     meta = json.load(open(tmp_path / "meta.json"))
-    assert meta["rounds"] == 2 and meta["dims"] == dims
+    assert meta["rounds"] == 3 and meta["dims"] == dims
+
+
+def test_checkpoint_crash_before_meta_keeps_previous_round(tmp_path, monkeypatch):
+    """A crash after the new round's weight files are in place but before meta.json is rewritten
+    leaves the previous round's complete set loadable; a file from another round under
+    meta.json's name is refused."""
+    import fedmi.ckpt.checkpoint as ck
+    X, y = make_income_like(300, seed=1)
+    dims = [14, 8, 2]
+    e = _engine(X, y, dims)
+    e.run(2)
+    save_checkpoint(str(tmp_path), e)
+    g2 = e.global_flat()
+    e.run(1)
+
+    def crash(*a, **k):
+        raise RuntimeError("simulated crash before meta.json")
+    monkeypatch.setattr(ck, "_publish_meta", crash)
+    with pytest.raises(RuntimeError):
+        save_checkpoint(str(tmp_path), e)
+    monkeypatch.undo()
+    assert {"client0.r3.safetensors", "weights.r3.safetensors"} <= set(os.listdir(tmp_path))
+    b = _engine(X, y, dims)
+    assert resume(str(tmp_path), b) == 2
+    np.testing.assert_array_equal(b.global_flat(), g2)
+    # a round-3 file under round 2's name: the header round check refuses it
+    os.replace(tmp_path / "client0.r3.safetensors", tmp_path / "client0.r2.safetensors")
+    with pytest.raises(ValueError, match="round"):
+        resume(str(tmp_path), _engine(X, y, dims))
+
+
+def test_sklearn_run_crash_before_meta_keeps_previous_round(tmp_path, monkeypatch):
+    import fedmi.ckpt.checkpoint as ck
+    rs = np.random.RandomState(0)
+    mk = lambda: [rs.randn(4, 3), rs.randn(3, 1), rs.randn(3), rs.randn(1)]
+    w1l, w1g = mk(), mk()
+    ck.save_sklearn_run(str(tmp_path), 0, 1, w1g, w1l, {"history": []})
+    monkeypatch.setattr(ck, "_publish_meta", lambda *a, **k: (_ for _ in ()).throw(RuntimeError("crash")))
+    with pytest.raises(RuntimeError):
+        ck.save_sklearn_run(str(tmp_path), 0, 2, mk(), mk(), {"history": []})
+    monkeypatch.undo()
+    out = ck.load_sklearn_run(str(tmp_path), 0)
+    assert out["meta"]["rounds"] == 1
+    for a, b in zip(out["local"] + out["global"], w1l + w1g):
+        np.testing.assert_array_equal(a, b)
+    ck.save_sklearn_run(str(tmp_path), 0, 2, w1g, w1l, {"history": []})
+    assert sorted(os.listdir(tmp_path)) == ["client0.r2.safetensors", "global.r2.safetensors", "meta.json"]
 
 
 def test_resume_rejects_mismatched_dims(tmp_path):
@@ -165,3 +217,29 @@ def test_wide_client_checkpoint_exact(tmp_path):
     a.sync(); b.sync()
     torch.cuda.synchronize()
     assert torch.equal(a.params, b.params)
+
+
+def test_hpo_sweep_save_overwrites_stale_trial_files(tmp_path):
+    """a --save directory left by an earlier run (other data / max_iter) must not lend
+    its trial weights to this run's sweep.json: files of another run are rewritten, a mismatched
+    file under this run's sweep.json is refused on load, duplicate trials are saved once, and
+    nearby learning rates get distinct files."""
+    from fedmi.data.tabular import load_tabular
+    from fedmi.hpo.sweep import _trial_file, TrialResult, load_sweep, run_sweep, save_sweep
+    ds = load_tabular(with_mean=False)
+    X, y = ds.X_train[:400], ds.y_train[:400]
+    best_a, res_a = run_sweep(X, y, None, [(5,)], [0.01], max_iter=3, backend="numpy")
+    save_sweep(str(tmp_path), res_a, best_a, {"world": 1, "max_iter": 3})
+    best_b, res_b = run_sweep(X, y, None, [(5,)], [0.01], max_iter=9, backend="numpy")
+    save_sweep(str(tmp_path), res_b + res_b, best_b, {"world": 1, "max_iter": 9})
+    back = load_sweep(str(tmp_path), expect={"max_iter": 9})
+    assert len(back) == 1
+    for u, v in zip(back[0].weights, res_b[0].weights):
+        np.testing.assert_array_equal(u, v)
+    # swap in the other run's file under this run's name: refused
+    save_sweep(str(tmp_path / "other"), res_a, best_a, {"world": 1, "max_iter": 3})
+    os.replace(tmp_path / "other" / _trial_file(res_a[0]), tmp_path / _trial_file(res_b[0]))
+    with pytest.raises(ValueError, match="another run"):
+        load_sweep(str(tmp_path))
+    mk = lambda lr: TrialResult((5,), lr, {}, {}, 1, [])
+    assert _trial_file(mk(0.0012345671)) != _trial_file(mk(0.0012345674))

@@ -125,3 +125,44 @@ def test_grad_slab_selection_rule():
     assert not pick(small, EngineConfig(dtype="fp32", grad_slab="fp16"))
     with pytest.raises(ValueError):
         pick(small, EngineConfig(dtype="bf16", grad_slab="bf16"))
+
+
+@pytest.mark.parametrize("backend,dtype", [("torch", "fp32"), pytest.param("hip", "fp32", marks=pytest.mark.gpu),
+                                           pytest.param("hip", "bf16", marks=pytest.mark.gpu)])
+def test_console_streams_rounds_as_they_complete(backend, dtype, capsys):
+    """train_and_evaluate(verbose=True) prints each round's reference lines
+    (C:139-179) while at most one chunk of <= 16 rounds runs behind them -- not after a 64-round
+    chunk -- and the printed text equals the non-streamed print of the same history."""
+    import fedmi.obs.console as console
+    from fedmi.fl.trainer import FederatedMLPLearning
+    torch.set_num_threads(1)
+    X, y = make_income_like(1500, seed=8)
+    tr = FederatedMLPLearning(X, y, 0, 1, config=EngineConfig(max_rounds=150, dtype=dtype), backend=backend, seed=2)
+    seen = []
+    real = console.print_history
+
+    def spy(h, patience, start=0, **kw):
+        seen.append((start, h["rounds_run"], tr.engine.rounds_issued))
+        return real(h, patience, start=start, **kw)
+    import fedmi.fl.trainer as trainer_mod
+    old = trainer_mod.print_history
+    trainer_mod.print_history = spy
+    try:
+        tr.train_and_evaluate(rounds=150, termination_patience=3, tolerance=5e-3, verbose=True)
+    finally:
+        trainer_mod.print_history = old
+    out = capsys.readouterr().out
+    h = tr.history()
+    assert h["stop_round"] > 0
+    printed_upto = 0
+    for start, upto, issued in seen:
+        assert start == printed_upto
+        # rounds issued beyond the last printed round: at most one chunk in flight
+        if upto < h["rounds_run"]:
+            assert issued - upto <= 16, (issued, upto)
+        printed_upto = upto
+    assert printed_upto == h["rounds_run"]
+    assert len([s for s in seen if s[1] > s[0]]) >= h["rounds_run"] // 16   # printed chunk by chunk
+    lines = []
+    real(h, 3, print_fn=lambda s, **k: lines.append(s))
+    assert out == "".join(s + "\n" for s in lines)

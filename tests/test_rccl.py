@@ -94,6 +94,44 @@ def test_round_engine_fedavg_through_rccl(dtype):
     rc.destroy()
 
 
+@pytest.mark.parametrize("check_every,seed", [(2, 6), (2, 7), (7, 6), (64, 6), (64, 8)])
+def test_lagged_rounds_with_early_stop_over_rccl(check_every, seed):
+    """Lagged rounds with early stopping when the FedAvg rides RCCL: region
+    A is folded one round late, so the round after the stop's trigger has already run when the
+    stop is found -- by the next Adam kernel or by the finalize kernel (``check_every`` 2: every
+    other round closes a host chunk) -- and is discarded.  Weights, metric history, loss and the
+    stop round are bitwise equal to classic rounds (a separate evaluation per round) over the same
+    one-rank RCCL communicator."""
+    import torch
+    from fedmi.data.synthetic import make_income_like
+    from fedmi.fl.engine import EngineConfig, HipRoundEngine
+    from fedmi.models.mlp import init_flat
+    m, rc = _rccl()
+    X, y = make_income_like(3000, seed=11)
+    flat = init_flat([14, 50, 200, 2], seed)
+    res = []
+    for lag in (True, False):
+        cfg = EngineConfig(max_rounds=300, patience=4, tolerance=2e-3, dtype="bf16", fused_eval=False,
+                           lagged_eval=lag, graph_rounds=4)
+        e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=True)
+        e._native_comm = rc
+        assert e.engine.lagged == lag and e.engine.late_fold == lag
+        e.run(300, check_every=check_every)
+        h = e.history()
+        res.append((e.global_flat(), h, e.engine.eval_launches))
+    (wl, hl, ev_l), (wc, hc, ev_c) = res
+    assert hc["stop_round"] > 0, "the classic run must stop early for this test to mean anything"
+    assert hl["stop_round"] == hc["stop_round"] and hl["rounds_run"] == hc["rounds_run"]
+    np.testing.assert_array_equal(wl, wc)
+    np.testing.assert_array_equal(hl["global"], hc["global"])
+    np.testing.assert_array_equal(hl["per_rank"], hc["per_rank"])
+    np.testing.assert_array_equal(hl["loss"], hc["loss"])
+    # lagged rounds evaluate only the closing round of each host chunk
+    assert ev_l < ev_c
+    torch.cuda.synchronize()
+    rc.destroy()
+
+
 @pytest.mark.parametrize("wire", ["fp32", "bf16"])
 def test_wide_aggregate_through_rccl(wire):
     """WideClient.aggregate: per-layer buckets all-reduced as n_i/N-scaled sums on the comm

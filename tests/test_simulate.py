@@ -54,13 +54,17 @@ def test_torch_rounds_to_target_keys():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_hip_client_group_tracks_torch(dtype):
-    """k = 4 HIP clients on one device (classic rounds, device-side sums) vs the torch group."""
+@pytest.mark.parametrize("dtype,plain", [("fp32", None), ("bf16", None), ("bf16", False)])
+def test_hip_client_group_tracks_torch(dtype, plain):
+    """k = 4 HIP clients on one device (classic rounds, device-side sums) vs the torch group.
+    bf16: the default (plain-bf16 training forward at world > 1, EngineConfig.plain_fwd None) and
+    the split forward (plain_fwd False) both stay within the same drift bound of the fp32 oracle
+    (pin the plain forward's drift at N > 1)."""
     ds = load_tabular()
     X, y = ds.X_train, ds.y_train
-    cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype)
+    cfg = EngineConfig(max_rounds=30, early_stop=False, dtype=dtype, plain_fwd=plain)
     h = ClientGroup(X, y, 4, cfg, backend="hip", seed=1)
+    assert all(bool(c.layout["plain_fwd"]) == (dtype == "bf16" and plain is None) for c in h.clients)
     t = ClientGroup(X, y, 4, EngineConfig(max_rounds=30, early_stop=False), backend="torch", seed=1)
     h.run(30)
     t.run(30)

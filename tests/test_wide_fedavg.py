@@ -42,7 +42,7 @@ def _worker(rank, port, q, wires, rounds, step_size, gamma):
         X, y = _data(rank, comm.device)
         res = {}
         for wire in wires:
-            c = WideClient(X, y, DIMS, comm=comm, n_total=sum(ROWS), micro_batch=512, dtype="bf16",
+            c = WideClient(X, y, DIMS, comm=comm, n_total=sum(ROWS), micro_batch=512, dtype="bf16", lr=0.004,
                            allreduce_dtype=wire, step_size=step_size, gamma=gamma)
             snaps = []
             for _ in range(rounds):
@@ -91,7 +91,7 @@ def test_wide_fedavg_buckets_match_simulation(wire, tol):
     import torch
     from fedmi.fl.wide import WideClient
     dev = torch.device("cuda", 0)
-    cl = [WideClient(*_data(r, dev), DIMS, micro_batch=512, dtype="bf16") for r in range(2)]
+    cl = [WideClient(*_data(r, dev), DIMS, micro_batch=512, dtype="bf16", lr=0.004) for r in range(2)]
     n = sum(ROWS)
     for _ in range(ROUNDS):
         for c in cl:

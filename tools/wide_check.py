@@ -40,7 +40,7 @@ m.gemm_nt_set_variant(3)
 X, y = make_income_like(4096, seed=0)
 Xt = torch.as_tensor(X, device=dev); yt = torch.as_tensor(y, device=dev)
 for dt_, dims in (("fp32", [14, 64, 48, 2]), ("bf16", [14, 64, 48, 2]), ("bf16", [14, 256, 256, 2])):
-    c = WideClient(Xt, yt, dims, micro_batch=1024, dtype=dt_)
+    c = WideClient(Xt, yt, dims, micro_batch=1024, dtype=dt_, lr=0.004)
     layers = []
     for a, b in zip(dims[:-1], dims[1:]):
         layers += [torch.nn.Linear(a, b), torch.nn.ReLU()]
