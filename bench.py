@@ -458,12 +458,15 @@ def main_sweep(a) -> int:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={N}")
     trials = grid(((50, 200), (100, 50), (50, 100)), (0.002, 0.004), (1, 2))
     trials = (trials * ((a.trials + len(trials) - 1) // len(trials)))[:a.trials]
-    X, y = synth_shard(a.rows_per_client, comm.rank, comm.device)
+    # rows per client: --rows-per-client, else the reference's chunking of --total-rows (C:57-60)
+    rows_local = a.rows_per_client or reference_rows(a.total_rows, N, comm.rank)
+    rows_total = a.rows_per_client * N if a.rows_per_client else a.total_rows
+    X, y = synth_shard(rows_local, comm.rank, comm.device)
     g_rounds = 16
     base = EngineConfig(max_rounds=a.warmup + a.steps + 2 * g_rounds + 4, early_stop=False, dtype=a.dtype,
                         rows_per_block=a.trial_rows_per_block,
                         graph_rounds=g_rounds)
-    grp = FedTrialGroup(X, y, 2, trials, comm if N > 1 else None, base, n_total=a.rows_per_client * N,
+    grp = FedTrialGroup(X, y, 2, trials, comm if N > 1 else None, base, n_total=rows_total,
                         group_graph_rounds=g_rounds)
 
     def barrier():
@@ -492,9 +495,11 @@ def main_sweep(a) -> int:
             "metric": "trial-rounds/s, packed federated hyperparameter sweep (BASELINE config 5)", "value": value,
             "unit": "trial-rounds/s (sum over GPUs; step = one federated round of every trial incl. eval + FedAvg)",
             "n_gpus": N, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": f"synthetic income-shaped (device Philox), {a.rows_per_client} rows/client; random-init weights",
-            "config": {"model": "MLP 14-{hidden}-2 grid", "global_batch": a.rows_per_client * N, "seq_len": 1,
+            "higher_is_better": True, "scaling": "weak" if a.rows_per_client else "strong", "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": f"synthetic income-shaped (device Philox), {rows_total} training rows ({rows_local} on rank 0); "
+                    "random-init weights",
+            "config": {"model": "MLP 14-{hidden}-2 grid", "global_batch": rows_total, "seq_len": 1,
                        "parallelism": f"fedavg{N} x {len(trials)} trials/GPU ({len(grp.batches)} trial batches, "
                                       f"one all-reduce per round)", "rccl_env": comm.rccl_env,
                        "trials": [[list(t.hidden), t.lr, t.local_steps] for t in trials],

@@ -60,6 +60,8 @@ def device_shard(n_rows: int, rank: int, device, seed: int = 7, label_noise: flo
     sample of the same distribution, each flipped with probability ``label_noise``."""
     import torch
     from ..ops import native
+    if n_rows <= 0:
+        raise ValueError(f"device_shard needs n_rows > 0 (got {n_rows})")
     m = native()
     w1, w2 = teacher_weights()
     Xs, _ = make_income_like(4096, seed=123)

@@ -112,10 +112,13 @@ class FederatedMLPLearning:
         # run_streaming keeps one chunk of <= `stream_chunk` rounds in flight behind the printed ones
         stream = verbose and hasattr(eng, "run_streaming")
 
+        announced = False   # the stop line is printed once (a chunk in flight past the stop re-reports it)
+
         def on_history(h):
-            nonlocal printed
-            if self.rank == 0:
+            nonlocal printed, announced
+            if self.rank == 0 and not announced:
                 printed = print_history(h, termination_patience, start=printed)
+                announced = h.get("stop_round", -1) >= 0 and printed == h["stop_round"]
         try:
             left = rounds - eng.rounds_issued
             while left > 0 and not eng.stopped:
@@ -130,8 +133,8 @@ class FederatedMLPLearning:
                 else:
                     with wd.guard(f"rounds {eng.rounds_issued}..{eng.rounds_issued + n - 1}"):
                         eng.run(n)
-                    if verbose and self.rank == 0:
-                        printed = print_history(eng.history(), termination_patience, start=printed)
+                    if verbose:
+                        on_history(eng.history())
                 left -= n
         except Exception as e:  # reference C:203-205
             print(f"Rank {self.rank} encountered an error: {e}", flush=True)

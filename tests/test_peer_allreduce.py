@@ -60,9 +60,11 @@ def _run_early_stop(comm, peer: bool, X, y, flat, lagged: bool = True):
     cfg = EngineConfig(max_rounds=200, patience=4, tolerance=2e-3, dtype="bf16", graph_rounds=8,
                        lagged_eval=lagged)
     e = HipRoundEngine(X, y, 2, cfg, comm, flat)
-    # with the peer data plane, early stopping runs lagged rounds (metrics exchanged and
-    # folded inside the next round's Adam kernel)
-    assert bool(e.engine.lagged) == (peer and lagged)
+    # early stopping runs lagged rounds: with the peer data plane the metrics are exchanged and
+    # folded inside the next round's Adam kernel; over an external all-reduce (here gloo) they are
+    # folded one round late and a round run past the stop is discarded bit-exactly (late fold)
+    assert bool(e.engine.lagged) == lagged
+    assert bool(e.engine.late_fold) == (lagged and not peer)
     e.run(200)
     return e.global_flat(), e.history()
 

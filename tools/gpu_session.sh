@@ -14,7 +14,7 @@ export FEDMI_NO_BUILD=1
 BENCH_ARGS=${BENCH_ARGS:-}
 
 run_tests() {
-    cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+    cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X--x} -v --timeout 240 --timeout-method thread \
         > $out/pytest_gpu.log 2>&1
     local rc=$?; tail -3 $out/pytest_gpu.log; return $rc
 }
