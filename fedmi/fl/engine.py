@@ -33,6 +33,12 @@ from .early_stop import EarlyStopper
 from .metrics import METRIC_NAMES, confusion_matrix, metrics_from_confusion, metric_vector
 
 
+# bf16 shards of at most this many rows default to 16 rows per workgroup (EngineConfig.rows_per_block = 0):
+# measured on MI355X (profiles/round_emulate_r4_shards.log), R = 16 wins at 1000 and 2000 rows,
+# R = 32 at 4000 and 8000.
+SMALL_SHARD_ROWS = 2000
+
+
 @dataclass
 class EngineConfig:
     hidden: Sequence[int] = (50, 200)
@@ -51,7 +57,8 @@ class EngineConfig:
     max_rounds: int = 300
     metric_mode: str = "mean"       # 'mean' (C:169) | 'pooled' (S:130)
     rows_per_block: int = 0         # R rows per workgroup of the fused kernels (16 | 32 | 64 (bf16); 0 = auto:
-                                    # 32 if it fits LDS, else 16; -1 = the largest that fits, 64 first (bf16))
+                                    # 16 for bf16 shards of <= SMALL_SHARD_ROWS rows, else 32 if it fits LDS, else 16;
+                                    # -1 = the largest that fits, 64 first (bf16))
     graph_rounds: int = 16          # rounds per captured HIP graph (0 = eager launches)
     seed: int = 0
     # partial participation (client sampling): each round max(1, round(participation * world))
@@ -507,7 +514,10 @@ class HipRoundEngine(RoundEngineBase):
         # largest that fits, 64 first (bf16: half the workgroups and gradient-slab rows -- what
         # packed trial batches want, whose throughput is workgroup-slots x workgroup latency)
         rpb = int(cfg.rows_per_block)
-        R_try = [32, 16] if rpb == 0 else ([64, 32, 16] if cfg.dtype == "bf16" else [32, 16]) if rpb == -1 else [rpb]
+        # (auto: small shards -- the reference's 8000 // k rows at k >= 4 -- run twice the
+        # workgroups at 16 rows each, lower per-workgroup latency; profiles/round_emulate_r4_shards.log)
+        auto = [16, 32] if (Xn_len <= SMALL_SHARD_ROWS and cfg.dtype == "bf16") else [32, 16]
+        R_try = auto if rpb == 0 else ([64, 32, 16] if cfg.dtype == "bf16" else [32, 16]) if rpb == -1 else [rpb]
         R = R_try[0]
         slab_stride = ((self.P + 1) + 3) & ~3
         # device parameter buffers use the padded image layout (fl_common.h)

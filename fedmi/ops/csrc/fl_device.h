@@ -165,6 +165,15 @@ static __device__ FLState fold_round(const MLPDesc& d, const FLConfig& c, const 
     return S;
 }
 
+// Can folding the pending rounds (at most two: regions A and B below) stop training?  Only
+// then does a block other than the history block need the fold itself: otherwise the round's
+// liveness -- all such a block takes from the fold -- is decided by the state on entry (the
+// patience counter is >= 1 after any fold that starts above 2: a "close" round decrements it,
+// any other resets it to the patience).  The history block (write_hist) always folds.
+__device__ __forceinline__ bool fold_may_stop(const FLConfig& c, const FLState& S) {
+    return c.es_enabled && !S.stopped && S.count <= 2;
+}
+
 // Regions of the all-reduced comm buffer `pg` that hold metrics (fl_common.h FL_FOLD_*):
 //   B (tail_off): the previous round's (next_round - 1) own evaluation;
 //   A (lag_off) : lagged rounds -- the round before it (next_round - 2), scored inside the

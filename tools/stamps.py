@@ -6,7 +6,7 @@ forward, used to report the effective shader clock.  Adam-kernel slots (paramete
 0 start, 1 first slab batch issued, 2 round state folded, 3 slab sums done, 4 partials
 combined, 5 update stored, 15 stores complete; "train->adam" = the gap between the last train
 workgroup's end and the first Adam block's start when the two are launched back to back."""
-import sys, numpy as np, torch
+import os, sys, numpy as np, torch
 sys.path.insert(0, ".")
 from fedmi.data.synthetic import make_income_like
 from fedmi.fl.engine import EngineConfig, HipRoundEngine
@@ -16,8 +16,9 @@ R = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 hidden = tuple(int(h) for h in sys.argv[3].split(",")) if len(sys.argv) > 3 else (50, 200)
 dtype = sys.argv[4] if len(sys.argv) > 4 else "fp32"
 X, y = make_income_like(rows, seed=1)
-cfg = EngineConfig(hidden=hidden, max_rounds=100, rows_per_block=R, graph_rounds=0, early_stop=False,
-                   dtype=dtype)
+# FEDMI_STAMPS_ES=1: early stopping on (every Adam block's wave 0 folds the round state)
+cfg = EngineConfig(hidden=hidden, max_rounds=100, rows_per_block=R, graph_rounds=0,
+                   early_stop=os.environ.get("FEDMI_STAMPS_ES", "0") == "1", patience=1000, dtype=dtype)
 # 5th argument "emulate": a multi-client engine (emulate_clients: lagged rounds, plain-bf16 training forward)
 emulate = len(sys.argv) > 5 and sys.argv[5] == "emulate"
 if emulate:
