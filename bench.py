@@ -206,6 +206,10 @@ def main(argv=None):
     ap.add_argument("--wide-allreduce", default="fp32", choices=["fp32", "bf16"],
                     help="--config wide: FedAvg bucket dtype on the wire (bf16: the round's delta; fp32 master "
                          "weights either way)")
+    ap.add_argument("--no-fused-eval", dest="fused_eval", action="store_false",
+                    help="--config wide: evaluate every round with its own forward pass over the shard (the round "
+                         "shape of a client at N > 1, where the next round's forward sees the global model) even "
+                         "at one client")
     ap.add_argument("--wide-lr", type=float, default=None,
                     help="--config wide: Adam lr (default fedmi.fl.wide.WIDE_LR = 1e-4; 0.004 diverges at width 4096)")
     a = ap.parse_args(argv)
@@ -268,8 +272,7 @@ def main(argv=None):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         eng._issue(a.steps, close=False)  # exactly K rounds, no host polling inside
-        eng.stream.synchronize()
-        torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)       # (waits for the engine's stream too: one wake-up, not two)
         barrier()
         dt = time.perf_counter() - t0
         if N > 1:
@@ -384,7 +387,8 @@ def main_wide(a) -> None:
     X, y = synth_shard(a.wide_rows, comm.rank, comm.device)
     lr = a.wide_lr if a.wide_lr is not None else WIDE_LR
     c = WideClient(X, y, dims, comm=comm if N > 1 else None, n_total=a.wide_rows * N, dtype="bf16", seed=0,
-                   micro_batch=a.micro_batch, allreduce_dtype=a.wide_allreduce, lr=lr)
+                   micro_batch=a.micro_batch, allreduce_dtype=a.wide_allreduce, lr=lr,
+                   fused_eval=None if a.fused_eval else False)
 
     def barrier():
         if N > 1:

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--idle-us", type=float, nargs="+", default=[0.0, 200.0, 5000.0],
                     help="host sleep between the pre-region synchronize and t0")
+    ap.add_argument("--fresh", type=int, default=3, help="fresh engines whose first timed replays are reported")
+    ap.add_argument("--fresh-only", action="store_true")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -47,6 +49,30 @@ def main():
         return e
 
     print(f"rows {a.rows}; times in us; device clock not pinned", flush=True)
+    # fresh engines, bench.py's exact sequence (warm-up rounds, prime = capture + first replay),
+    # then successive K = 20 regions of one g = 20 replay each: is the first timed replay (the
+    # graph's second launch, what bench.py times) slower than later ones?
+    for trial in range(a.fresh):
+        e = engine(20)
+        walls, gpus = [], []
+        for rep in range(6):
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e.stream.synchronize()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            ev0.record(e.stream)
+            e.engine.replay(e._stream())
+            ev1.record(e.stream)
+            e.rounds_issued += 20
+            e.stream.synchronize()
+            torch.cuda.synchronize(dev)
+            walls.append((time.perf_counter() - t0) * 1e6 / 20)
+            gpus.append(ev0.elapsed_time(ev1) * 1e3 / 20)
+        print(f"fresh engine {trial}: launch 2..7 wall/round " + " ".join(f"{w:.2f}" for w in walls)
+              + "  gpu/round " + " ".join(f"{g:.2f}" for g in gpus), flush=True)
+        del e
+    if a.fresh_only:
+        return
     for K, g in ((20, 0), (20, 20), (20, 10), (20, 4), (20, 2), (200, 0), (200, 20), (2000, 40)):
         e = engine(g if g else 20)
         for idle in a.idle_us:
