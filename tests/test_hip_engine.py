@@ -798,3 +798,30 @@ def test_lagged_register_scoring_equals_serial_pass(hidden, C, R, monkeypatch):
     if eligible:  # the plain training forward changes the trajectory, not its quality
         a, b = out[(None, True)][1]["global"][-1], out[("0", True)][1]["global"][-1]
         assert abs(a[0] - b[0]) < 0.02, (a, b)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("patience", [1, 2, 3, 5])
+def test_early_stop_fold_only_where_it_can_stop(dtype, patience):
+    """Blocks other than the history block fold the previous round only when the fold can stop
+    training (patience counter <= 2, fl_device.h fold_may_stop).  For every patience: the device's
+    stop round is the host rule (EarlyStopper, C:181-192) applied to the device's own metric
+    history, and the rounds issued past the stop leave the model bit-identical to a run that
+    simply ends at the stop round -- so no block ever updated a round the rule had stopped."""
+    from fedmi.fl.early_stop import EarlyStopper
+    X, y = make_income_like(2500, seed=17)
+    flat = init_flat(DIMS, 8)
+    cfg = EngineConfig(max_rounds=160, patience=patience, tolerance=3e-3, dtype=dtype, graph_rounds=8)
+    e = HipRoundEngine(X, y, 2, cfg, None, flat)
+    e.run(160)
+    h = e.history()
+    s = h["stop_round"]
+    assert 0 < s < 160, s
+    es = EarlyStopper(patience, 3e-3)
+    host = next(r + 1 for r in range(h["rounds_run"]) if es.update(h["global"][r]))
+    assert host == s, (host, s)
+    ref = HipRoundEngine(X, y, 2, EngineConfig(max_rounds=s, early_stop=False, dtype=dtype, graph_rounds=8), None,
+                         flat)
+    ref.run(s)
+    np.testing.assert_array_equal(e.global_flat(), ref.global_flat())
+    np.testing.assert_array_equal(e.history()["global"][:s], ref.history()["global"][:s])

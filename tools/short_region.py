@@ -29,8 +29,16 @@ def main():
                     help="host sleep between the pre-region synchronize and t0")
     ap.add_argument("--fresh", type=int, default=3, help="fresh engines whose first timed replays are reported")
     ap.add_argument("--fresh-only", action="store_true")
+    ap.add_argument("--shift-kb", type=int, nargs="*", default=[],
+                    help="per fresh engine: KB of device memory allocated (and kept) before it")
     a = ap.parse_args()
     import numpy as np
+    if os.environ.get("FEDMI_SPIN_SYNC", "0") == "1":
+        # synchronizations spin instead of yielding (hipDeviceScheduleSpin = 1), set before torch
+        # creates the device context
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        print("hipSetDeviceFlags(spin):", hip.hipSetDeviceFlags(ctypes.c_uint(1)), flush=True)
     import torch
     import bench
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
@@ -52,8 +60,15 @@ def main():
     # fresh engines, bench.py's exact sequence (warm-up rounds, prime = capture + first replay),
     # then successive K = 20 regions of one g = 20 replay each: is the first timed replay (the
     # graph's second launch, what bench.py times) slower than later ones?
+    pads = []
     for trial in range(a.fresh):
+        if a.shift_kb:   # shift the engine's allocations: a pad of shift_kb[trial] KB allocated (and kept) first
+            kb = a.shift_kb[trial % len(a.shift_kb)]
+            if kb:
+                pads.append(torch.empty(kb * 256, dtype=torch.float32, device=dev))
         e = engine(20)
+        print(f"engine {trial}: slab {e.slab.data_ptr():#x} X {e.X.data_ptr():#x} params {e.params[0].data_ptr():#x} "
+              f"(mod 2 MiB: slab {e.slab.data_ptr() % (2 << 20):#x})", flush=True)
         walls, gpus = [], []
         for rep in range(6):
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
