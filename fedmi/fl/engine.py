@@ -98,6 +98,12 @@ class EngineConfig:
     # valid (never for one fused client, whose evaluation IS the training forward).  The engine's
     # layout()["plain_fwd"] reports what runs; bench records and checkpoints carry it.
     plain_fwd: Optional[bool] = None
+    # lagged rounds (several clients, bf16): score the previous round's local model with the
+    # evaluation kernel on a side stream, concurrently with the train kernel, instead of with
+    # scoring waves inside the train kernel.  None: auto (when the two grids fit the GPU's CUs
+    # side by side -- small shards such as the reference's 8000 // k rows at k >= 2); the counts
+    # are identical either way.  layout()["side_eval"] reports what runs.
+    side_eval: Optional[bool] = None
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -577,6 +583,7 @@ class HipRoundEngine(RoundEngineBase):
             "emulate_clients": bool(emulate_clients),
             "slab_f16": self._pick_slab_f16(cfg),
             "plain_fwd": -1 if cfg.plain_fwd is None else int(bool(cfg.plain_fwd)),
+            "side_eval": -1 if cfg.side_eval is None else int(bool(cfg.side_eval)),
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),

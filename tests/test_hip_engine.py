@@ -825,3 +825,52 @@ def test_early_stop_fold_only_where_it_can_stop(dtype, patience):
     ref.run(s)
     np.testing.assert_array_equal(e.global_flat(), ref.global_flat())
     np.testing.assert_array_equal(e.history()["global"][:s], ref.history()["global"][:s])
+
+
+@pytest.mark.parametrize("R", [16, 32])
+@pytest.mark.parametrize("es", [False, True])
+def test_side_stream_scoring_equals_in_kernel_scoring(R, es):
+    """Lagged rounds of small shards score the previous round's local model with the evaluation
+    kernel on a side stream, concurrently with the (non-scoring) train kernel; the Adam kernel
+    joins both (EngineConfig.side_eval).  Weights, per-client metrics, loss history and the
+    early-stop round are bit-identical to scoring inside the train kernel and to classic rounds,
+    eager and graph-captured (the fork/join is captured into the round graph)."""
+    X, y = make_income_like(1500, seed=23)
+    flat = init_flat(DIMS, 9)
+    out = {}
+    n = 120 if es else 40
+    for mode in ("side", "in-kernel", "classic"):
+        cfg = EngineConfig(max_rounds=n, early_stop=es, patience=3, tolerance=3e-3, dtype="bf16", graph_rounds=4,
+                           rows_per_block=R, fused_eval=False, lagged_eval=mode != "classic",
+                           side_eval=mode == "side")
+        e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=True)
+        assert bool(e.engine.lagged) == (mode != "classic")
+        assert bool(e.layout["side_eval"]) == (mode == "side")
+        e.run(3)
+        e.run(n)
+        e.sync_history()
+        out[mode] = (e.global_flat(), e.history())
+    ws, hs = out["side"]
+    if es:
+        assert 0 < hs["stop_round"] < n, hs["stop_round"]
+    for other in ("in-kernel", "classic"):
+        w, h = out[other]
+        assert h["rounds_run"] == hs["rounds_run"] and h["stop_round"] == hs["stop_round"], other
+        np.testing.assert_array_equal(ws, w, err_msg=other)
+        np.testing.assert_array_equal(hs["global"], h["global"], err_msg=other)
+        np.testing.assert_array_equal(hs["per_rank"], h["per_rank"], err_msg=other)
+        np.testing.assert_array_equal(hs["loss"], h["loss"], err_msg=other)
+
+
+def test_side_stream_scoring_auto_rule():
+    """side_eval=None picks side-stream scoring when the train and evaluation grids fit the GPU's
+    CUs side by side (the reference's 1000-row shards at k = 8: 63 + 63 workgroups) and keeps
+    in-kernel scoring when they do not (8000 rows, R = 32: 250 + 250 > 256 CUs)."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    flat = init_flat(DIMS, 9)
+    for rows in (1000, 8000):
+        X, y = make_income_like(rows, seed=5)
+        e = HipRoundEngine(X, y, 2, EngineConfig(max_rounds=8, dtype="bf16", fused_eval=False), None, flat,
+                           emulate_clients=True)
+        assert bool(e.layout["side_eval"]) == (2 * ((rows + e.R - 1) // e.R) <= cus), (rows, e.R, cus)
