@@ -343,10 +343,9 @@ def main(argv=None):
                            " (classic rounds: lagged evaluation disabled for > 2 ranks sharing one GPU)"
                            if lag_off_shared else ""),
                        "round_design": ("fused-eval" if N == 1 else
-                                        ("lagged-eval" + ("(side-stream scoring)" if eng.layout.get("side_eval") else "")
-                                         + ("+adam-fedavg" if eng.engine.adam_exchange else
-                                            "+late-fold" if eng.engine.late_fold else ""))
-                                        if eng.engine.lagged else "classic"),
+                                        "lagged-eval+adam-fedavg" if eng.engine.adam_exchange else
+                                        "lagged-eval+late-fold" if eng.engine.late_fold else
+                                        "lagged-eval" if eng.engine.lagged else "classic"),
                        "rccl_env": comm.rccl_env,
                        "rows_per_client": a.rows_per_client or reference_rows(a.total_rows, N, 0),
                        "rows_last_client": a.rows_per_client or reference_rows(a.total_rows, N, N - 1),

@@ -98,12 +98,6 @@ class EngineConfig:
     # valid (never for one fused client, whose evaluation IS the training forward).  The engine's
     # layout()["plain_fwd"] reports what runs; bench records and checkpoints carry it.
     plain_fwd: Optional[bool] = None
-    # lagged rounds (several clients, bf16): score the previous round's local model with the
-    # evaluation kernel on a side stream, concurrently with the train kernel, instead of with
-    # scoring waves inside the train kernel.  None: auto (when the two grids fit the GPU's CUs
-    # side by side -- small shards such as the reference's 8000 // k rows at k >= 2); the counts
-    # are identical either way.  layout()["side_eval"] reports what runs.
-    side_eval: Optional[bool] = None
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -583,7 +577,6 @@ class HipRoundEngine(RoundEngineBase):
             "emulate_clients": bool(emulate_clients),
             "slab_f16": self._pick_slab_f16(cfg),
             "plain_fwd": -1 if cfg.plain_fwd is None else int(bool(cfg.plain_fwd)),
-            "side_eval": -1 if cfg.side_eval is None else int(bool(cfg.side_eval)),
         }
         bufs = {
             "X": self.X.data_ptr(), "y": self.y.data_ptr(),
@@ -892,11 +885,13 @@ class HipRoundEngine(RoundEngineBase):
                     on_history(self.history())
             return self.hist.rounds_run - before
         # graph rounds per chunk: lagged engines close every chunk with an eager self-evaluating
-        # round, so their graphs leave room for it (graph + lagged + closing round)
+        # round, and a lagged graph starts only behind a lagged round that scored its predecessor
+        # (FLEngine::needs_eager_round), so a chunk is 2 eager lagged rounds + the graph + 1 lagged
+        # + the closing round (graph + 4, even, so every chunk starts on an even round)
         g = int(self.cfg.graph_rounds)
         if g >= 2:
-            gs = max(2, (min(g, chunk) - (2 if self.engine.lagged else 0)) & ~1)
-            step = gs + (2 if self.engine.lagged else 0)
+            gs = max(2, (min(g, chunk) - (4 if self.engine.lagged else 0)) & ~1)
+            step = gs + (4 if self.engine.lagged else 0)
         else:
             gs, step = 0, max(1, chunk)
         mirror = self._host_mirror()

@@ -329,10 +329,6 @@ hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLCon
                                 float* cm_out = nullptr, int fold_mask = FL_FOLD_B);
 hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
                                const float* params, float* comm, const FLState* st, hipStream_t s);
-// Lagged rounds scored on a side stream: round r-1's local model (pk_local) -> counts in b.cnt,
-// skipped unless round r (input state `st`) is tentatively live (fl_kernels_bf16.hip)
-hipError_t fl_launch_score_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
-                                const FLState* st, hipStream_t s);
 hipError_t fl_set_lds_limit_bf16(size_t bytes);
 // fp32 parameter image -> packed bf16 LDS-layout parameter region (MLPDescB)
 // Local evaluation + FedAvg in one kernel (world > 1 with the one-shot xGMI all-reduce,

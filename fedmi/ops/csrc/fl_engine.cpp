@@ -221,27 +221,6 @@ class FLEngine {
             c_.plain_fwd = (valid && want && !(pf != nullptr && pf[0] == '0')) ? 1 : 0;
         }
 
-        // Lagged rounds of small shards score on a side stream (side_eval_, issue_train): the
-        // evaluation grid runs beside the train grid when both fit the GPU's CUs at once (one
-        // workgroup per CU each: their LDS layouts take most of a CU's 160 KB).  cfg["side_eval"]
-        // (EngineConfig.side_eval): -1 auto, 0 off, 1 on wherever valid; FEDMI_SIDE_EVAL=0|1
-        // overrides (A/B builds).
-        {
-            int dev = 0, cus = 0;
-            HIP_CHECK(hipGetDevice(&dev));
-            HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            const int req = cfg.contains("side_eval") ? cfg["side_eval"].cast<int>() : -1;
-            const char* se = std::getenv("FEDMI_SIDE_EVAL");
-            const int want = (se != nullptr && (se[0] == '0' || se[0] == '1')) ? se[0] - '0' : req;
-            const bool valid = lag_ok_ && (c_.R == 16 || c_.R == 32);
-            side_eval_ = valid && (want < 0 ? 2 * c_.n_slabs <= cus : want > 0);
-            if (side_eval_) {
-                HIP_CHECK(hipStreamCreateWithFlags(&s2_, hipStreamNonBlocking));
-                HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-                HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-            }
-        }
-
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
         b_.slab = as_ptr<float>(bufs["slab"].cast<uintptr_t>());
@@ -279,9 +258,6 @@ class FLEngine {
 
     ~FLEngine() {
         drop_graph();
-        if (ev_fork_) (void)hipEventDestroy(ev_fork_);
-        if (ev_join_) (void)hipEventDestroy(ev_join_);
-        if (s2_) (void)hipStreamDestroy(s2_);
         if (pk_) (void)hipFree(pk_);
         if (lagbuf_) (void)hipFree(lagbuf_);
     }
@@ -407,9 +383,14 @@ class FLEngine {
     // The captured rounds assume the steady state of their kind: a fused graph must not
     // start behind a classic round (whose counts already sit in the tail), a classic graph
     // not behind a fused one (whose counts were never computed).
-    // A lagged graph must start behind a lagged round (its rounds score their predecessor).
+    // A lagged graph must start behind a lagged round that scored ITS predecessor: the first
+    // captured round's fold mask (region A of the round before) is fixed at capture, and every
+    // replay after the first starts behind such a round.  (Captured behind a lagged round that
+    // followed a self-evaluating one -- e.g. a warm-up that closed on an odd round count -- every
+    // replay's first round skipped the region-A fold: that round's metrics never reached the
+    // history or the early-stop rule.  The Adam-fused exchange folds in time and was unaffected.)
     bool needs_eager_round() const {
-        if (lagged()) return !prev_lagged_;
+        if (lagged()) return !prev_lagged_ || !prev_scored_;
         return fused_ ? cm_in_tail_ : pending_cm_;
     }
     // Lagged rounds: allowed by the layout, and either no early stopping (metrics may be
@@ -568,7 +549,6 @@ class FLEngine {
         o["tail_len"] = c_.tail_len;
         o["comm_len"] = comm_len_;
         o["lagged_eval"] = lagged();
-        o["side_eval"] = side_eval_;                     // lagged rounds scored on a side stream
         o["state_bytes"] = (int)sizeof(FLState);
         return o;
     }
@@ -650,23 +630,9 @@ class FLEngine {
         const int mask = fused ? FL_FOLD_B
                                : ((prev_scored_ && !prev_afold_ ? FL_FOLD_A : 0) | (prev_lagged_ ? 0 : FL_FOLD_B));
         float* cm_out = score ? b_.cnt : pg + c_.tail_off + c_.rank * c_.tail_stride;
-        // side_eval_: the predecessor's local model is scored by the score kernel on s2_ (forked
-        // behind the previous round's Adam kernel, which wrote that model), concurrently with this
-        // round's train kernel, which then scores nothing (FUSED_SKIP: the Adam kernel folds, as
-        // for LAGGED); this round's first Adam kernel joins s2_ -- it reads the counts and
-        // overwrites the local model.  Same counts, same fold: bit-identical rounds.
-        const bool side = score && side_eval_ && rec_ == nullptr;
-        if (side) {
-            HIP_CHECK(hipEventRecord(ev_fork_, s));
-            HIP_CHECK(hipStreamWaitEvent(s2_, ev_fork_, 0));
-            HIP_CHECK(fl_launch_score_bf16(d_, ev_, c_, b_, si, s2_));
-            HIP_CHECK(hipEventRecord(ev_join_, s2_));
-            mode = FL_EVAL_FUSED_SKIP;
-        }
         for (int ls = 0; ls < c_.local_steps; ++ls) {
             const bool first = ls == 0;
             launch_train(pg, first ? si : so, so, ls, s, first ? mode : FL_EVAL_CLASSIC, cm_out, mask);
-            if (first && side) HIP_CHECK(hipStreamWaitEvent(s, ev_join_, 0));
             if (first && (xchg || afold)) {
                 const PeerArgs pa = peer_->args((r + 1) & 1, pbuf_[(r + 1) & 1]);
                 launch_adam(pg, pg, cb, si, ls, s, so, 1, score ? 1 : 0, mask, &pa, xchg ? 1 : 0, afold ? 1 : 0);
@@ -762,9 +728,6 @@ class FLEngine {
     float* lagbuf_ = nullptr;  // FL_EVAL_LAGGED count + loss carry-over
     long long comm_len_ = 0;   // floats of a comm buffer: image + tails (+ lag region)
     bool lag_ok_ = false;      // lagged rounds possible (layout, clients, bf16): see lagged()
-    bool side_eval_ = false;   // lagged rounds score their predecessor on s2_ beside the train kernel
-    hipStream_t s2_ = nullptr;
-    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
     bool emulate_ = false;     // one process stands in for a multi-client round (measurements, tests)
     bool xchg_ = false;        // lagged rounds: FedAvg inside the Adam kernel (no all-reduce kernel)
     bool prev_lagged_ = false; // the last issued round had no evaluation of its own

@@ -943,20 +943,6 @@ fl_eval_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const float*
     eval_rows_bf16<RT>(d, e, c, b, params, cm_out, blockIdx.x, lds);
 }
 
-// Lagged rounds scored on a side stream (FLEngine side_eval): round r-1's post-step local model
-// (its packed image pk_local) on the local shard, counts into b.cnt -- exactly what the lagged
-// train kernel of round r scores beside its training pass, under the same condition (round r
-// tentatively live, `st` = round r's input state), with the same split-bf16 forward, so the
-// counts are identical.  Runs concurrently with round r's (non-scoring) train kernel on CUs the
-// train grid leaves free; round r's Adam kernel waits for both.
-template <int RT>
-__global__ void __launch_bounds__(FL_THREADS)
-fl_score_bf16_kernel(MLPDesc d, MLPDescB e, FLConfig c, FLBuffers b, const FLState* __restrict__ st) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    if (st->stopped || st->next_round >= c.max_rounds) return;
-    eval_rows_bf16<RT>(d, e, c, b, b.local, b.cnt, blockIdx.x, lds);
-}
-
 template <int RT>
 __global__ void __launch_bounds__(FL_THREADS)
 fl_eval_bf16_batch_kernel(MLPDesc d, MLPDescB e, const FLTrialDesc* __restrict__ T, FLSel params, FLSel comm,
@@ -1042,22 +1028,6 @@ hipError_t fl_launch_eval_bf16(const MLPDesc& d, const MLPDescB& e, const FLConf
         case 64:
             hipLaunchKernelGGL(fl_eval_bf16_kernel<4>, dim3(blocks), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b,
                                params, cm, st);
-            break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-hipError_t fl_launch_score_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b,
-                                const FLState* st, hipStream_t s) {
-    if (st == nullptr || b.cnt == nullptr || b.pk_local == nullptr) return hipErrorInvalidValue;
-    const int blocks = (c.n_rows + c.R - 1) / c.R;
-    switch (c.R) {
-        case 16:
-            hipLaunchKernelGGL(fl_score_bf16_kernel<1>, dim3(blocks), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b, st);
-            break;
-        case 32:
-            hipLaunchKernelGGL(fl_score_bf16_kernel<2>, dim3(blocks), dim3(FL_THREADS), e.lds_bytes, s, d, e, c, b, st);
             break;
         default: return hipErrorInvalidValue;
     }
@@ -1170,7 +1140,6 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
     FLB_SET((fl_train_bf16_kernel<1, 2, true>)); FLB_SET((fl_train_bf16_kernel<2, 2, true>));
     FLB_SET((fl_train_bf16_kernel<1, 0, true>)); FLB_SET((fl_train_bf16_kernel<2, 0, true>));
     FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>); FLB_SET(fl_eval_bf16_kernel<4>);
-    FLB_SET(fl_score_bf16_kernel<1>); FLB_SET(fl_score_bf16_kernel<2>);
     FLB_SET((fl_train_bf16_batch_kernel<1, false>)); FLB_SET((fl_train_bf16_batch_kernel<2, false>));
     FLB_SET((fl_train_bf16_batch_kernel<4, false>)); FLB_SET((fl_train_bf16_batch_kernel<1, true>));
     FLB_SET((fl_train_bf16_batch_kernel<2, true>)); FLB_SET((fl_train_bf16_batch_kernel<4, true>));

@@ -46,8 +46,6 @@ def main():
     ap.add_argument("--rpb", type=int, nargs="+", default=[0], help="rows per workgroup (0: engine default)")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--cases", nargs="+", default=list(CASES), choices=list(CASES))
-    ap.add_argument("--side", default="auto", choices=["auto", "on", "off", "ab"],
-                    help="lagged rounds: score on a side stream (EngineConfig.side_eval); ab = both, off first")
     a = ap.parse_args()
     import torch
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
@@ -64,16 +62,14 @@ def main():
     for rows in a.rows:
         X, y = bench.synth_shard(rows, 0, dev)
         for rpb in a.rpb:
-            for key, side in [(k, s) for k in a.cases
-                              for s in ((False, True) if a.side == "ab" and CASES[k][3] else
-                                        ({"auto": None, "on": True, "off": False}[a.side if a.side != "ab" else "auto"],))]:
+            for key in a.cases:
                 name, fused, ef, lag, adam_x, es, use_rccl = CASES[key]
                 if lag and a.dtype != "bf16":
                     continue
                 # early stopping on with a patience never reached: every round's fold runs the rule
                 cfg = EngineConfig(max_rounds=a.rounds + 256, early_stop=es, patience=10 ** 6,
                                    dtype=a.dtype, graph_rounds=16, rows_per_block=rpb,
-                                   fused_eval=fused, eval_fedavg=bool(ef), lagged_eval=lag, side_eval=side)
+                                   fused_eval=fused, eval_fedavg=bool(ef), lagged_eval=lag)
                 e = HipRoundEngine(X, y, 2, cfg, None, flat, emulate_clients=not fused)
                 h = None
                 if ef is not None:
@@ -85,8 +81,6 @@ def main():
                     e._native_comm = rc
                 design = ("late-fold" if e.engine.late_fold else "adam-x" if e.engine.adam_exchange else
                           "lagged" if e.engine.lagged else "fused" if e.engine.fused else "classic")
-                if e.engine.lagged:
-                    design += ", side-stream scoring" if e.layout.get("side_eval") else ", in-kernel scoring"
                 e.run(64)
                 e.stream.synchronize()
                 t0 = time.perf_counter()
