@@ -30,6 +30,7 @@ Companion key ``weak_8000_rows_per_client``: the same round with 8000 rows on ev
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -141,7 +142,7 @@ def torch_eager_anchor(X, y, dims, rounds: int = 60, warmup: int = 10) -> float:
     return (time.perf_counter() - t0) / rounds * 1e6
 
 
-def fp32_round_us(X, y, dims, a, rounds: int = 200) -> float:
+def fp32_round_us(X, y, dims, a, rounds: int = 200, stream=None) -> float:
     """Untimed companion number at the reference's precision: the same one-client round with
     the exact-fp32 kernels (v_mfma_f32_16x16x4_f32; reference [C] trains in fp32, C:65-66),
     graph-replayed, microseconds per round (after the bf16 timed region, one client)."""
@@ -150,7 +151,7 @@ def fp32_round_us(X, y, dims, a, rounds: int = 200) -> float:
     g = _pick_graph_rounds(rounds)
     cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=rounds + 3 * g + 64, early_stop=False,
                        graph_rounds=g, dtype="fp32")
-    eng = HipRoundEngine(X, y, 2, cfg, None, init_flat(dims, seed=0))
+    eng = HipRoundEngine(X, y, 2, cfg, None, init_flat(dims, seed=0), stream=stream)
     eng.run(32, check_every=32)
     eng.prime_graph(g)
     eng.stream.synchronize()
@@ -255,6 +256,10 @@ def main(argv=None):
         if N > 1:
             dist.barrier()
 
+    # every engine of this process issues on ONE stream (HipRoundEngine `stream`: with ranks sharing
+    # a GPU, the companion run's engine on a fresh stream ran 2.3x slower)
+    stream = torch.cuda.Stream(device=dev)
+
     def timed_rounds(rows_local: int, rows_total: int):
         """Build a client with `rows_local` rows (FedAvg weight rows_local / rows_total), warm up,
         time exactly a.steps rounds (max over ranks), close + check; returns (dt, engine, primed)."""
@@ -262,7 +267,7 @@ def main(argv=None):
         cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=max_rounds, early_stop=a.early_stop,
                            patience=patience, rows_per_block=a.rows_per_block, graph_rounds=g,
                            dtype=a.dtype, lagged_eval=not lag_off_shared)
-        eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank), n_total=rows_total)
+        eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank), n_total=rows_total, stream=stream)
         # warm-up: the requested rounds, then (uncounted) the graph of the timed region is
         # captured, instantiated and replayed once, so the timed steps are steady-state replays
         eng.run(a.warmup, check_every=max(a.warmup, 1))
@@ -296,6 +301,19 @@ def main(argv=None):
     from fedmi.parallel.consistency import check_replicas
     replicas_ok = check_replicas(comm, [eng.global_flat(), np.asarray(h["global"])])
     value = rows_total * a.steps / dt
+    # what the record needs from the timed engine; then it is released (its graph, buffers and
+    # xGMI peer mappings) before any other engine of this process runs
+    design = {"aggregation": eng.aggregation,
+              "round_design": ("fused-eval" if N == 1 else
+                               "lagged-eval+adam-fedavg" if eng.engine.adam_exchange else
+                               "lagged-eval+late-fold" if eng.engine.late_fold else
+                               "lagged-eval" if eng.engine.lagged else "classic"),
+              "rows_per_block": eng.R, "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
+              "lagged_eval": eng.cfg.lagged_eval, "final_acc": float(h["global"][-1][0])}
+    X, y = eng.X, eng.y
+    del eng
+    gc.collect()
+    torch.cuda.synchronize(dev)
     # companion: per-GPU work fixed at the reference's one-client shard (8000 rows on every client)
     weak = None
     if not a.rows_per_client and not a.no_weak:
@@ -307,7 +325,7 @@ def main(argv=None):
                     "rows_per_client": REF_TRAIN_ROWS, "scaling": "weak",
                     "replicas_consistent": check_replicas(comm, [engw.global_flat()])}
             del engw
-    X, y = eng.X, eng.y
+            gc.collect()
     anchor = None
     if not a.no_anchor:
         if comm.rank == 0:
@@ -315,9 +333,9 @@ def main(argv=None):
         barrier()
     fp32_us = None
     if N == 1 and a.dtype != "fp32" and not a.no_fp32:
-        fp32_us = fp32_round_us(X, y, dims, a)
+        fp32_us = fp32_round_us(X, y, dims, a, stream=stream)
     # rounds-to-target is measured with the same kernels (dtype) as the throughput
-    rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=eng.cfg.lagged_eval)
+    rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=design["lagged_eval"])
     if comm.rank == 0:
         rec = {
             "metric": METRIC,
@@ -338,30 +356,27 @@ def main(argv=None):
             "config": {"model": f"MLP {'-'.join(map(str, dims))} (reference [C])",
                        "global_batch": rows_total, "seq_len": 1,
                        "parallelism": f"fedavg{N} (1 client/{'shared ' if a.share_gpu else ''}GPU, "
-                                      f"{eng.aggregation} all-reduce)",
-                       "data_plane": eng.aggregation + (
+                                      f"{design['aggregation']} all-reduce)",
+                       "data_plane": design["aggregation"] + (
                            " (classic rounds: lagged evaluation disabled for > 2 ranks sharing one GPU)"
                            if lag_off_shared else ""),
-                       "round_design": ("fused-eval" if N == 1 else
-                                        "lagged-eval+adam-fedavg" if eng.engine.adam_exchange else
-                                        "lagged-eval+late-fold" if eng.engine.late_fold else
-                                        "lagged-eval" if eng.engine.lagged else "classic"),
+                       "round_design": design["round_design"],
                        "rccl_env": comm.rccl_env,
                        "rows_per_client": a.rows_per_client or reference_rows(a.total_rows, N, 0),
                        "rows_last_client": a.rows_per_client or reference_rows(a.total_rows, N, N - 1),
-                       "rows_per_block": eng.R,
+                       "rows_per_block": design["rows_per_block"],
                        "optimizer": "Adam(0.004)+StepLR(30,0.5)",
                        "early_stop": {"enabled": bool(a.early_stop), "patience": patience, "atol": 1e-4,
                                       "rtol": 1e-5, "note": "rule evaluated on the device every timed round; "
                                       "patience longer than the run so every timed round is live"},
-                       "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
+                       "plain_fwd": design["plain_fwd"],
                        "graph_rounds": g, "share_gpu": bool(a.share_gpu)},
             "samples_per_sec_per_client": value / N,
             "us_per_round": dt / a.steps * 1e6,
             "weak_8000_rows_per_client": weak,
             "torch_eager_us_per_round_1client": anchor,
             "fp32_us_per_round": fp32_us if a.dtype != "fp32" else dt / a.steps * 1e6,
-            "final_train_acc_synthetic": float(h["global"][-1][0]),
+            "final_train_acc_synthetic": design["final_acc"],
             "replicas_consistent": replicas_ok,
             "rounds_to_target": rtt,
         }

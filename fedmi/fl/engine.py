@@ -489,8 +489,12 @@ class HipRoundEngine(RoundEngineBase):
     tensors already on the device (e.g. from the synthetic generator)."""
 
     def __init__(self, X, y, n_classes, cfg: EngineConfig, comm, init_flat, n_total=None, device=None,
-                 comm_buffers=None, emulate_clients: bool = False, client_sizes=None):
-        """``comm_buffers``: optional pair of float32 device views of length
+                 comm_buffers=None, emulate_clients: bool = False, client_sizes=None, stream=None):
+        """``stream``: the torch stream the engine issues on (default: a new one).  Engines created one
+        after another in a process (bench.py's timed runs) should share one: with ranks sharing a
+        GPU, a second engine on a fresh stream ran its Adam-exchange rounds 2.3x slower
+        (108 vs 46 us per round, profiles/bench_r4_n2_share_stream.log).
+        ``comm_buffers``: optional pair of float32 device views of length
         :meth:`comm_len` to use as the double-buffered FedAvg buffers (trial packing shares one
         all-reduce between engines by handing each a slice of one allocation).
         ``client_sizes``: every client's shard size (client sampling weighs the sampled clients
@@ -605,7 +609,7 @@ class HipRoundEngine(RoundEngineBase):
         if (self.layout["Pimg"], list(self.layout["iw_off"]), list(self.layout["ib_off"])) != (self.Pimg, iw, ib):
             raise RuntimeError(f"image layout mismatch between C++ and Python: {self.layout}")
         # the engine owns a non-default stream: graph capture is illegal on the null stream
-        self.stream = torch.cuda.Stream(device=dev)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=dev)
         self.stream.wait_stream(torch.cuda.current_stream(dev))
         self.rounds_issued = 0
         self._stopped_seen = False
