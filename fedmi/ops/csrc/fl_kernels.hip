@@ -142,6 +142,19 @@ __device__ void fwd_head_valu(const float* w, int ldw, const float* bias, int K,
     }
 }
 
+// Waves that take wgrad tiles in the backward phase of layer l (the fp32 twin of
+// wgrad_waves_bf16): the dgrad items (one per 16 input columns, handed out from the last wave
+// down) are chains of ochunks dependent 16-deep steps; when they are long (the 50 -> 200 layer:
+// 4 items of 13 steps, 104 MFMAs each) their waves take no wgrad tiles -- which otherwise
+// stacked in front of the chain on the same waves (stamps: the last wave started its dgrad
+// 4.8 us into the phase, then ran 3.2 us) -- and the phase ends with an LDS arrival count of
+// those waves instead of a barrier (fl_train_body.inc).  Only the work-to-wave map changes.
+__device__ __forceinline__ int wgrad_waves_fp32(int K, int N, int l) {
+    const int items = l > 0 ? (K + 15) >> 4 : 0;
+    const int chunks = (N + 15) >> 4;
+    return (items > 0 && chunks >= 4 && 2 * items <= FL_WAVES) ? FL_WAVES - items : FL_WAVES;
+}
+
 // dH[r][i] = (sum_o dZ[r][o] W[o][i]) * (act[r][i] > 0) -> out (separate buffer, so the
 // same phase can run the layer's wgrad, which reads act).  Item = 16-column tile of dH (all
 // R rows); B fragment W[o][i] reused across the RT rows.  Items are handed out from the
@@ -153,6 +166,11 @@ __device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* 
     const int lr = lane & 15, lg = lane >> 4;
     const int itiles = (K + 15) >> 4;
     const int ochunks = (N + 15) >> 4;
+    // long dgrad chains (their own waves, wgrad_waves_fp32) issue ahead of the wgrad tiles that
+    // share their SIMDs: the chain is the phase's critical path (fp32 round 29.5 -> 28.6 us,
+    // profiles/fp32_backward_r4.log)
+    const bool prio = ochunks >= 4 && wave < itiles;
+    if (prio) __builtin_amdgcn_s_setprio(2);
     for (int it = wave; it < itiles; it += FL_WAVES) {
         const int i = it * 16 + lr;
         const float* wc = w + 4 * lg * ldw + i;     // B: W[16q + 4lg + j][i]
@@ -194,20 +212,25 @@ __device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* 
                 out[o] = (ivalid && act[o] > 0.f) ? acc[rt][j] : 0.f;
             }
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
 }
 
 // dW[o][i] = sum_r dZ[r][o] act[r][i] over the block's rows -> gW ([N][K] dense, global);
 // gb[o] = sum_r dZ[r][o].  Two output tiles per wave are interleaved (independent chains);
 // row r = 16q + 4lg + j of chunk q feeds MFMA step j of lane group lg.
+// Tiles go to `nw` waves: waves [0, nw) from wave 0 up, or (`top`) the last nw waves from the
+// top down; waves outside them take none (they run a long dgrad chain, wgrad_waves_fp32).  A
+// wave's lone last tile runs alone (no duplicate second chain on the MFMA pipe).
 template <int RT>
 __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float* act, int ld_a,
-                            float* __restrict__ gW, float* __restrict__ gb) {
+                            float* __restrict__ gW, float* __restrict__ gb, int nw = FL_WAVES, bool top = false) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     const int otiles = (N + 15) >> 4, itiles = (K + 15) >> 4;
     const int ntile = otiles * itiles;
-    for (int t0 = wave; t0 < ntile; t0 += 2 * FL_WAVES) {
-        const int t1raw = t0 + FL_WAVES;
+    const int w = top ? FL_WAVES - 1 - wave : wave;
+    for (int t0 = w < nw ? w : ntile; t0 < ntile; t0 += 2 * nw) {
+        const int t1raw = t0 + nw;
         const bool has1 = t1raw < ntile;
         const int t1 = has1 ? t1raw : t0;
         const int ot0 = t0 / itiles, it0 = t0 - ot0 * itiles;
@@ -227,10 +250,15 @@ __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float
             }
         __builtin_amdgcn_sched_barrier(0);
         f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+        if (has1) {  // (wave-uniform)
 #pragma unroll
-        for (int s = 0; s < RT * 4; ++s) {
-            acc0 = mfma_f32(a0[s], b0[s], acc0);
-            acc1 = mfma_f32(a1[s], b1[s], acc1);
+            for (int s = 0; s < RT * 4; ++s) {
+                acc0 = mfma_f32(a0[s], b0[s], acc0);
+                acc1 = mfma_f32(a1[s], b1[s], acc1);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < RT * 4; ++s) acc0 = mfma_f32(a0[s], b0[s], acc0);
         }
         __builtin_amdgcn_sched_barrier(0);
         const int i0 = it0 * 16 + lr, i1 = it1 * 16 + lr;
