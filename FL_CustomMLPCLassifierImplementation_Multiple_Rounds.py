@@ -79,6 +79,9 @@ def parse_args(argv=None):
     ap.add_argument("--profile", type=int, default=0, metavar="N",
                     help="time the first N rounds per phase with hipEvents (HIP engine)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--timing", action="store_true",
+                    help="rank 0 prints main()'s wall time and BASELINE's end-to-end metric: shard rows x rounds "
+                         "run / main() wall (CSV load, set-up and console included)")
     ap.add_argument("--wide", action="store_true",
                     help="BASELINE config 3: layer-by-layer wide-MLP client (e.g. --hidden 4096 4096 4096) on "
                          "device-generated synthetic shards of --synthetic-rows rows per client")
@@ -170,6 +173,7 @@ def main_clients(a, comm):
 
 
 def main(argv=None):
+    t_main = time.perf_counter()
     a = parse_args(argv)
     if not 0.0 < a.participation <= 1.0:
         raise SystemExit("--participation must be in (0, 1]")
@@ -231,6 +235,12 @@ def main(argv=None):
         w.close()
     if a.save:
         save_checkpoint(a.save, trainer)   # collective: every client writes its optimizer state
+    if a.timing and rank == 0:
+        # BASELINE.md "[C] samples/s/client (e2e)": shard rows / (wall of main() / rounds run)
+        rounds_run = max(int(trainer.history()["rounds_run"]), 1)
+        wall = time.perf_counter() - t_main
+        print(f"main() wall {wall:.3f} s for {rounds_run} rounds ({t_train:.3f} s in train_and_evaluate): "
+              f"e2e {len(trainer.X_local) * rounds_run / wall:,.0f} samples/s/client", flush=True)
     comm.close()
     return global_metrics
 
