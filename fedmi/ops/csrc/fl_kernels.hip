@@ -73,6 +73,10 @@ __device__ void fwd_layer_mfma(const float* w, int ldw, const float* bias, int K
         float4 bc = lds4(wr), ac[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) ac[rt] = lds4(ar + rt * 16 * ld_in);
+        // the last chunk's steps j >= K - 16q are all-padding when K - 16q <= 4 (step j of lane
+        // group g takes k = 16q + 4g + j): skipped -- they would add exact zeros (a (50, 200) layer
+        // runs 14 of 16 steps)
+        const int klast = K - 16 * (kchunks - 1);
         for (int q = 0; q < kchunks; ++q) {
             const int qn = (q + 1 < kchunks) ? q + 1 : q;  // prefetch (last: harmless reload)
             const float4 bn = lds4(wr + 16 * qn);
@@ -80,10 +84,12 @@ __device__ void fwd_layer_mfma(const float* w, int ldw, const float* bias, int K
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) an[rt] = lds4(ar + rt * 16 * ld_in + 16 * qn);
             __builtin_amdgcn_sched_barrier(0);
+            const int jmax = (q + 1 < kchunks || klast > 4) ? 4 : klast;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
+                if (j < jmax)
 #pragma unroll
-                for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma_f32(f4(ac[rt], j), f4(bc, j), acc[rt]);
+                    for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma_f32(f4(ac[rt], j), f4(bc, j), acc[rt]);
             __builtin_amdgcn_sched_barrier(0);
             bc = bn;
 #pragma unroll
