@@ -627,6 +627,16 @@ class HipRoundEngine(RoundEngineBase):
                 self.engine.attach_peer(self._peer)
         self._graph_ready = False
 
+    def slab_partials(self) -> torch.Tensor:
+        """The last train kernel's per-workgroup gradient partials as [n_slabs, P] (a copy of the
+        slab rows, fp32 or fp16, in dense-parameter order).  fp16 partials are sums of the
+        unscaled gradient (the Adam kernel applies the 1/n)."""
+        lay = self.engine.layout()
+        ns, stride, P = int(lay["n_slabs"]), int(lay["slab_stride"]), self.P
+        if self.slab_f16:  # fp16 partial e at half e of the row (fl_device.h slab_store_h)
+            return self.slab.view(torch.float16).view(-1, 2 * stride)[:ns, :P].clone()
+        return self.slab.view(-1, stride)[:ns, :P].clone()
+
     def _pick_slab_f16(self, cfg) -> bool:
         if cfg.grad_slab not in ("auto", "fp16", "fp32"):
             raise ValueError(f"grad_slab must be 'auto', 'fp16' or 'fp32', got {cfg.grad_slab!r}")

@@ -730,12 +730,10 @@ def test_bf16_train_kernel_gradient(R, slab):
     e.stream.synchronize()
     P = e.P
     lay = e.engine.layout()
-    stride = int(lay["slab_stride"])
     assert lay["slab_f16"] == (slab == "fp16") == e.slab_f16
+    g = e.slab_partials().double().sum(0).cpu().numpy()
     if slab == "fp16":
-        g = e.slab.view(torch.float16).view(-1, 2 * stride)[:, :P].double().sum(0).cpu().numpy() / len(X)
-    else:
-        g = e.slab.view(-1, stride)[:, :P].double().sum(0).cpu().numpy()
+        g /= len(X)
     ref = _split_bf16_reference_grad(flat, X, y, dims, scaled_delta=slab == "fp32")
     model = TorchRoundEngine(X, y, 2, EngineConfig(max_rounds=2), None, flat)
     out = model.model(torch.as_tensor(X))
