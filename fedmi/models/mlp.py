@@ -122,7 +122,8 @@ def _r16(n: int) -> int:
 
 def image_layout(dims: Sequence[int]):
     """Offsets of the padded device parameter image (fedmi/ops/csrc/fl_common.h): per layer
-    W_l as [roundup16(N)][roundup16(K)+4] then b_l as [roundup16(N)], zero padded."""
+    W_l as [roundup16(N)][roundup16(K)+4] then b_l as [roundup16(N)], zero padded; W_l[n][k] at
+    column k ^ swz(n) of row n (_image_cols)."""
     iw, ib, off = [], [], 0
     for l in range(len(dims) - 1):
         K, N = dims[l], dims[l + 1]
@@ -131,6 +132,13 @@ def image_layout(dims: Sequence[int]):
         ib.append(off)
         off += _r16(N)
     return iw, ib, (off + 3) & ~3
+
+
+def _image_cols(N: int, K: int) -> np.ndarray:
+    """[N, K] image column of W[n][k]: k ^ swz(n), swz(n) = 4 for n mod 16 in [4, 12) (the fp32
+    kernels' LDS chunk swizzle, fl_common.h fl_swz)."""
+    n = np.arange(N)[:, None]
+    return np.arange(K)[None, :] ^ (((n + 4) & 8) >> 1)
 
 
 def dense_to_image(flat: np.ndarray, dims: Sequence[int]) -> np.ndarray:
@@ -142,7 +150,8 @@ def dense_to_image(flat: np.ndarray, dims: Sequence[int]) -> np.ndarray:
         W = flat[off:off + N * K].reshape(N, K)
         bo = off + N * K
         ldw = _ldw(K)
-        img[iw[l]:iw[l] + _r16(N) * ldw].reshape(_r16(N), ldw)[:N, :K] = W
+        rows = img[iw[l]:iw[l] + _r16(N) * ldw].reshape(_r16(N), ldw)
+        rows[np.arange(N)[:, None], _image_cols(N, K)] = W
         img[ib[l]:ib[l] + N] = flat[bo:bo + N]
     return img
 
@@ -154,7 +163,8 @@ def image_to_dense(img: np.ndarray, dims: Sequence[int]) -> np.ndarray:
     for l, (name, shape, off) in enumerate(param_layout(dims)[0::2]):
         N, K = shape
         ldw = _ldw(K)
-        out[off:off + N * K] = img[iw[l]:iw[l] + _r16(N) * ldw].reshape(_r16(N), ldw)[:N, :K].reshape(-1)
+        rows = img[iw[l]:iw[l] + _r16(N) * ldw].reshape(_r16(N), ldw)
+        out[off:off + N * K] = rows[np.arange(N)[:, None], _image_cols(N, K)].reshape(-1)
         out[off + N * K:off + N * K + N] = img[ib[l]:ib[l] + N]
     return out
 

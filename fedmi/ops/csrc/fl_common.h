@@ -8,10 +8,11 @@
 //
 // Parameter "image" layout.  Every parameter-shaped device buffer (global/comm, local, m, v)
 // stores, per layer l, W_l ([N][K], torch Linear layout) as fl_wrows(N) rows of fl_ldw(K)
-// floats followed by b_l padded to roundup16(N), all padding zero.  The image is exactly the
-// LDS image the kernels compute from, so staging a model into LDS is one contiguous float4
-// copy, and every MFMA operand read of a 16x16 tile / 16-deep k chunk is in bounds and reads
-// zeros in the padding (no predication, no exec-mask branches in inner loops).  The dense
+// floats followed by b_l padded to roundup16(N), all padding zero; W_l[n][k] sits at column
+// k ^ fl_swz(n) of row n (the fp32 kernels' LDS chunk swizzle, fl_kernels.hip).  The image is
+// exactly the LDS image the fp32 kernels compute from, so staging a model into LDS is one
+// contiguous float4 copy, and every MFMA operand read of a 16x16 tile / 16-deep k chunk is in
+// bounds and reads zeros in the padding (no predication, no exec-mask branches in inner loops).  The dense
 // reference layout (named_parameters() order: model.0.weight, model.0.bias, ...; C:93-99)
 // exists only at the API boundary (get/set weights, checkpoints) and in the gradient slab.
 #pragma once
@@ -44,6 +45,10 @@ __host__ __device__ inline int fl_lag_w(int G, int j) { return G - ((FL_LAG_SPR 
 // 16-lane ds_read_b128 group land on 16 distinct 16-byte bank slots.
 __host__ __device__ inline int fl_ldw(int K) { return ((K + 15) & ~15) + 4; }
 __host__ __device__ inline int fl_wrows(int N) { return (N + 15) & ~15; }
+// fp32 LDS / image chunk swizzle: row r keeps logical column k < roundup16(width) at column
+// k ^ fl_swz(r) -- the 4-float chunks of rows 4..11 (mod 16) trade places in pairs
+// (fl_kernels.hip; models/mlp.py mirrors it).
+__host__ __device__ inline int fl_swz(int r) { return ((r + 4) & 8) >> 1; }
 
 struct MLPDesc {
     int L;                            // number of Linear layers

@@ -44,10 +44,22 @@ __device__ __forceinline__ f32x4 mfma_f32(float a, float b, f32x4 c) {
 //   A lane l -> A[l&15][l>>4], B lane l -> B[l>>4][l&15], C/D: col l&15, row 4(l>>4)+j).
 // The contraction order is free, so k is permuted: in a 16-deep chunk q, MFMA step j takes
 // k = 16q + 4*lg + j from lane group lg.  A lane then owns 4 CONSECUTIVE k, i.e. one 16-byte
-// ds_read_b128 per operand wherever k runs along an LDS row (row strides are 4 mod 8 floats,
-// so 16 rows of one 16-lane group hit 16 distinct 16-byte bank slots).  All loads of a chunk
-// are issued before its MFMAs (sched_barrier), so LDS latency overlaps the matrix pipe.
+// ds_read_b128 per operand wherever k runs along an LDS row.  All loads of a chunk are issued
+// before its MFMAs (sched_barrier), so LDS latency overlaps the matrix pipe.
+//
+// LDS chunk swizzle: every fp32 LDS matrix (activations, deltas, logits, and the weight rows,
+// already swizzled in the parameter image, fl_common.h) keeps logical column k <
+// roundup16(width) of row r at column k ^ fl_swz(r), i.e. the
+// 4-float chunks of rows 4..11 (mod 16) trade places in pairs (pad columns stay put).  A b128
+// operand read -- lane (row lr, chunk lg) -- covers 8 rows at chunk g and 8 rows at chunk g ^ 1
+// in each of the four gfx950 b128 lane groups; with row strides 4 mod 8 floats those collided
+// on one 16-byte bank slot (4 extra LDS cycles per read: 0.55 conflict cycles per LDS
+// instruction measured, profiles/pmc_summary_r3s2.txt), with the swizzle all 16 land on distinct
+// slots (tools/bank_fp32.py models both).  b32 accesses of 16 consecutive columns of a row touch
+// the same banks as before.  Rows 16t + 4g + j of a C/D fragment share fl_swz(4g): one per-lane
+// constant (fl_swz_lg) for every output / b32 access.
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int fl_swz_lg(int lg) { return (lg == 1 || lg == 2) ? 4 : 0; }  // = fl_swz(4 lg + j)
 
 __device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float f4(const float4& v, int j) {
@@ -65,8 +77,9 @@ __device__ void fwd_layer_mfma(const float* w, int ldw, const float* bias, int K
     const int kchunks = (K + 15) >> 4;
     for (int nt = wave; nt < ntiles; nt += FL_WAVES) {
         const int n = nt * 16 + lr;
-        const float* wr = w + n * ldw + 4 * lg;
-        const float* ar = in + lr * ld_in + 4 * lg;
+        const int ck = (4 * lg) ^ fl_swz(lr);  // operand chunk (rows n and lr + 16 rt: fl_swz(lr))
+        const float* wr = w + n * ldw + ck;
+        const float* ar = in + lr * ld_in + ck;
         f32x4 acc[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -96,13 +109,14 @@ __device__ void fwd_layer_mfma(const float* w, int ldw, const float* bias, int K
             for (int rt = 0; rt < RT; ++rt) ac[rt] = an[rt];
         }
         const float bv = bias[n];
+        const int ns = n ^ fl_swz_lg(lg);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float v = acc[rt][j] + bv;
                 if (relu) v = fmaxf(v, 0.f);
-                out[(rt * 16 + lg * 4 + j) * ld_out + n] = v;
+                out[(rt * 16 + lg * 4 + j) * ld_out + ns] = v;
             }
     }
 }
@@ -124,27 +138,28 @@ __device__ void fwd_head_valu(const float* w, int ldw, const float* bias, int K,
         const int r = oc / C, c = oc - r * C;
         const float* ar = in + r * ld_in;
         const float* wr = w + c * ldw;
+        const int sa = fl_swz(r), sw = fl_swz(c);
         float s0 = 0.f, s1 = 0.f;
         // 4 consecutive k per thread per step: float4 reads
         int k = 4 * part;
         for (; k + 4 * T < K16; k += 8 * T) {
-            const float4 a0 = lds4(ar + k), w0 = lds4(wr + k);
-            const float4 a1 = lds4(ar + k + 4 * T), w1 = lds4(wr + k + 4 * T);
+            const float4 a0 = lds4(ar + (k ^ sa)), w0 = lds4(wr + (k ^ sw));
+            const float4 a1 = lds4(ar + ((k + 4 * T) ^ sa)), w1 = lds4(wr + ((k + 4 * T) ^ sw));
             s0 = fmaf(a0.x, w0.x, s0); s0 = fmaf(a0.y, w0.y, s0); s0 = fmaf(a0.z, w0.z, s0); s0 = fmaf(a0.w, w0.w, s0);
             s1 = fmaf(a1.x, w1.x, s1); s1 = fmaf(a1.y, w1.y, s1); s1 = fmaf(a1.z, w1.z, s1); s1 = fmaf(a1.w, w1.w, s1);
         }
         if (k < K16) {
-            const float4 a0 = lds4(ar + k), w0 = lds4(wr + k);
+            const float4 a0 = lds4(ar + (k ^ sa)), w0 = lds4(wr + (k ^ sw));
             s0 = fmaf(a0.x, w0.x, s0); s0 = fmaf(a0.y, w0.y, s0); s0 = fmaf(a0.z, w0.z, s0); s0 = fmaf(a0.w, w0.w, s0);
         }
         float s = s0 + s1;
         for (int off = 1; off < T; off <<= 1) s += __shfl_xor(s, off, 64);
-        if (o < nout && part == 0) out[r * ld_out + c] = s + bias[c];
+        if (o < nout && part == 0) out[r * ld_out + (c ^ sa)] = s + bias[c];
     }
     const int Cp = (C + 15) & ~15;  // zero padded columns [C, roundup16(C))
     for (int e = threadIdx.x; e < R * (Cp - C); e += FL_THREADS) {
         const int r = e / (Cp - C), c = C + (e - r * (Cp - C));
-        out[r * ld_out + c] = 0.f;
+        out[r * ld_out + (c ^ fl_swz(r))] = 0.f;
     }
 }
 
@@ -179,8 +194,9 @@ __device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* 
     if (prio) __builtin_amdgcn_s_setprio(2);
     for (int it = wave; it < itiles; it += FL_WAVES) {
         const int i = it * 16 + lr;
-        const float* wc = w + 4 * lg * ldw + i;     // B: W[16q + 4lg + j][i]
-        const float* ar = dz + lr * ld_z + 4 * lg;  // A: dZ[r][16q + 4lg + j]
+        const int is = i ^ fl_swz_lg(lg);                        // column i of rows 16t + 4lg + j
+        const float* wc = w + 4 * lg * ldw + is;                 // B: W[16q + 4lg + j][i]
+        const float* ar = dz + lr * ld_z + ((4 * lg) ^ fl_swz(lr));  // A: dZ[r][16q + 4lg + j]
         f32x4 acc[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -214,7 +230,7 @@ __device__ void dgrad_layer(const float* w, int ldw, int K, int N, const float* 
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int o = (rt * 16 + lg * 4 + j) * ld_a + i;
+                const int o = (rt * 16 + lg * 4 + j) * ld_a + is;
                 out[o] = (ivalid && act[o] > 0.f) ? acc[rt][j] : 0.f;
             }
     }
@@ -241,10 +257,11 @@ __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float
         const int t1 = has1 ? t1raw : t0;
         const int ot0 = t0 / itiles, it0 = t0 - ot0 * itiles;
         const int ot1 = t1 / itiles, it1 = t1 - ot1 * itiles;
-        const float* ap0 = dz + 4 * lg * ld_z + ot0 * 16 + lr;
-        const float* bp0 = act + 4 * lg * ld_a + it0 * 16 + lr;
-        const float* ap1 = dz + 4 * lg * ld_z + ot1 * 16 + lr;
-        const float* bp1 = act + 4 * lg * ld_a + it1 * 16 + lr;
+        const int ls = lr ^ fl_swz_lg(lg);  // columns of rows 16q + 4lg + j
+        const float* ap0 = dz + 4 * lg * ld_z + ot0 * 16 + ls;
+        const float* bp0 = act + 4 * lg * ld_a + it0 * 16 + ls;
+        const float* ap1 = dz + 4 * lg * ld_z + ot1 * 16 + ls;
+        const float* bp1 = act + 4 * lg * ld_a + it1 * 16 + ls;
         float a0[RT * 4], b0[RT * 4], a1[RT * 4], b1[RT * 4];
 #pragma unroll
         for (int q = 0; q < RT; ++q)
@@ -279,8 +296,8 @@ __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
         for (int r = 0; r < RT * 16; r += 2) {
-            s0 += dz[r * ld_z + o];
-            s1 += dz[(r + 1) * ld_z + o];
+            s0 += dz[r * ld_z + (o ^ fl_swz(r))];
+            s1 += dz[(r + 1) * ld_z + (o ^ fl_swz(r + 1))];
         }
         slab_store(&gb[o], s0 + s1);
     }
@@ -288,8 +305,10 @@ __device__ void wgrad_layer(int K, int N, const float* dz, int ld_z, const float
 
 template <int RT>
 __device__ void stage_rows(const float* __restrict__ X, int n_rows, int F, int row0, float* xs, int ld) {
+    const int F16 = (F + 15) & ~15;
     for (int e = threadIdx.x; e < RT * 16 * ld; e += FL_THREADS) {
-        const int r = e / ld, c = e - r * ld;
+        const int r = e / ld, cs = e - r * ld;
+        const int c = cs < F16 ? cs ^ fl_swz(r) : cs;  // logical column stored at cs
         const int row = row0 + r;
         const bool ok = row < n_rows && c < F;
         const float v = X[(size_t)(ok ? row : 0) * F + (ok ? c : 0)];  // unpredicated load
@@ -297,7 +316,8 @@ __device__ void stage_rows(const float* __restrict__ X, int n_rows, int F, int r
     }
 }
 
-// The global parameter image is bit-identical to the LDS image: one float4 copy.
+// The global parameter image is bit-identical to the LDS image (weight rows already swizzled,
+// fl_common.h): one float4 copy.
 __device__ __forceinline__ void stage_image(const MLPDesc& d, const float* __restrict__ params, float* li) {
     const float4* src = reinterpret_cast<const float4*>(params);
     float4* dst = reinterpret_cast<float4*>(li);
@@ -391,10 +411,11 @@ __device__ void eval_rows(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
         const int r = threadIdx.x, row = row0 + r;
         if (row < c.n_rows) {
             const float* zr = acts + d.act_off[d.L] + r * d.ld[d.L];
+            const int sr = fl_swz(r);
             int best = 0;
-            float bv = zr[0];
+            float bv = zr[sr];
             for (int k = 1; k < C; ++k)
-                if (zr[k] > bv) { bv = zr[k]; best = k; }
+                if (zr[k ^ sr] > bv) { bv = zr[k ^ sr]; best = k; }
             atomicAdd(&cm_s[ylab * C + best], 1);
         }
     }

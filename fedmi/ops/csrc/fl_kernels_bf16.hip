@@ -90,7 +90,8 @@ __device__ __forceinline__ void fl_pack_bf16_body(const MLPDesc& d, const MLPDes
         uint4 v = make_uint4(0u, 0u, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
         if (ok) {
             const float4* src = reinterpret_cast<const float4*>(params + d.iw_off[l] + n * fl_ldw(d.dim[l]) + 8 * ch);
-            const float4 p0 = src[0], p1 = src[1];
+            const bool sw = fl_swz(n) != 0;  // the image's swizzled rows hold the two halves swapped
+            const float4 p0 = sw ? src[1] : src[0], p1 = sw ? src[0] : src[1];
             v = make_uint4(pack_bf16x2(p0.x, p0.y), pack_bf16x2(p0.z, p0.w), pack_bf16x2(p1.x, p1.y),
                            pack_bf16x2(p1.z, p1.w));
             w = make_uint4(pack_lo_bf16x2(p0.x, p0.y), pack_lo_bf16x2(p0.z, p0.w), pack_lo_bf16x2(p1.x, p1.y),

@@ -9,8 +9,9 @@
 
 #include "fl_common.h"
 
-// Activation row stride: roundup16(dim) + 4 floats (16-byte aligned rows, 4 mod 8 so the
-// b128 / b32 MFMA operand patterns of fl_kernels.hip are bank-conflict free).
+// Activation row stride: roundup16(dim) + 4 floats (16-byte aligned rows, 4 mod 8: with the
+// chunk swizzle of fl_kernels.hip (fl_swz) the b128 / b32 MFMA operand patterns are
+// bank-conflict free).
 inline int fl_pick_ld(int dim) { return ((dim + 15) & ~15) + 4; }
 
 // dims[0..L]: features, hidden sizes, classes.  Fills the dense / image offsets and the fp32

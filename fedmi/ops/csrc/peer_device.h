@@ -109,8 +109,9 @@ __device__ __forceinline__ void peer_pack_store(const PeerPack& p, int i, float4
         if (l >= p.L || i < p.img4_w[l] || i >= p.img4_end[l]) continue;
         if (i < p.img4_b[l]) {
             const int q = i - p.img4_w[l];
-            const int n = q / p.ldw4[l], c4 = q - n * p.ldw4[l];
-            if (c4 < p.k4[l]) {  // columns [roundup16(K), ldw) are the image's zero pad
+            const int n = q / p.ldw4[l], c4s = q - n * p.ldw4[l];
+            if (c4s < p.k4[l]) {  // columns [roundup16(K), ldw) are the image's zero pad
+                const int c4 = c4s ^ (fl_swz(n) >> 2);  // logical chunk (swizzled image, fl_common.h)
                 const uint32_t hx = peer_bf16_rne(s.x), hy = peer_bf16_rne(s.y), hz = peer_bf16_rne(s.z),
                                hw = peer_bf16_rne(s.w);
                 char* dst = p.pk + p.pk_w[l] + fl_wrow(n, p.pk_lda[l], p.pk_wgap) + 16 * ((c4 >> 1) ^ fl_wswz(n, p.pk_wxor)) +

@@ -4,7 +4,10 @@ groups and bank functions of MI355X_MICROARCH.md §LDS (64 x 4 B banks; the conf
 is its worst bank's distinct-dword count - 1).  Prints each pattern's cost and instruction count per
 workgroup, so a layout change can be priced before it is built.
 
-    python tools/bank_fp32.py [--R 32] [--hidden 50 200] [--ld-pad 4]
+    python tools/bank_fp32.py [--R 32] [--hidden 50 200] [--ld-pad 4] [--no-swizzle]
+
+--no-swizzle models the layout before the chunk swizzle (fl_kernels.hip fl_swz: row r keeps
+logical column k at k ^ swz(r), swz(r) = 4 for r mod 16 in [4, 12)).
 """
 import argparse
 from collections import defaultdict
@@ -47,7 +50,11 @@ def main():
     ap.add_argument("--R", type=int, default=32)
     ap.add_argument("--hidden", type=int, nargs="+", default=[50, 200])
     ap.add_argument("--ld-pad", type=int, default=4, help="activation / weight row pad (floats) over roundup16")
+    ap.add_argument("--no-swizzle", action="store_true")
     a = ap.parse_args()
+
+    def sw(r):
+        return 0 if a.no_swizzle else ((r + 4) & 8) >> 1
     dims = [14, *a.hidden, 2]
     L = len(dims) - 1
     RT = a.R // 16
@@ -64,36 +71,36 @@ def main():
             T = 1024 // (a.R * N)
             T = 1 << (T.bit_length() - 1) if T < 64 else 64
             # wave w: gid = 64 w + lane, o = gid // T, part = gid % T
-            addrA = [((64 * 0 + ln) // T // N) * ld[l] + 4 * ((64 * 0 + ln) % T) for ln in range(64)]
-            addrW = [((64 * 0 + ln) // T % N) * ldw[l] + 4 * ((64 * 0 + ln) % T) for ln in range(64)]
+            addrA = [((ln // T) // N) * ld[l] + ((4 * (ln % T)) ^ sw((ln // T) // N)) for ln in range(64)]
+            addrW = [((ln // T) % N) * ldw[l] + ((4 * (ln % T)) ^ sw((ln // T) % N)) for ln in range(64)]
             steps = (r16(K) + 4 * T - 1) // (4 * T)
             add(f"fwd{l} head A", "read_b128", addrA, 16 * steps)
             add(f"fwd{l} head W", "read_b128", addrW, 16 * steps)
             continue
         kq = r16(K) // 16
         nt = r16(N) // 16
-        A = [(ln & 15) * ld[l] + 4 * (ln >> 4) for ln in range(64)]
-        B = [(ln & 15) * ldw[l] + 4 * (ln >> 4) for ln in range(64)]
+        A = [(ln & 15) * ld[l] + ((4 * (ln >> 4)) ^ sw(ln & 15)) for ln in range(64)]
+        B = [(ln & 15) * ldw[l] + ((4 * (ln >> 4)) ^ sw(ln & 15)) for ln in range(64)]
         add(f"fwd{l} A", "read_b128", A, nt * kq * RT)
         add(f"fwd{l} B", "read_b128", B, nt * kq)
-        O = [(4 * (ln >> 4)) * ld[l + 1] + (ln & 15) for ln in range(64)]
+        O = [(4 * (ln >> 4)) * ld[l + 1] + ((ln & 15) ^ sw(4 * (ln >> 4))) for ln in range(64)]
         add(f"fwd{l} out", "write_b32", O, nt * RT * 4)
     for l in range(L - 1, -1, -1):
         K, N = dims[l], dims[l + 1]
         ldz, lda = ld[l + 1], ld[l]
         ot, it = r16(N) // 16, r16(K) // 16
-        Az = [(4 * (ln >> 4)) * ldz + (ln & 15) for ln in range(64)]
-        Ba = [(4 * (ln >> 4)) * lda + (ln & 15) for ln in range(64)]
+        Az = [(4 * (ln >> 4)) * ldz + ((ln & 15) ^ sw(4 * (ln >> 4))) for ln in range(64)]
+        Ba = [(4 * (ln >> 4)) * lda + ((ln & 15) ^ sw(4 * (ln >> 4))) for ln in range(64)]
         add(f"wgrad{l} dZ", "read_b32", Az, ot * it * RT * 4)
         add(f"wgrad{l} act", "read_b32", Ba, ot * it * RT * 4)
         # bias column sums: thread o reads dz[r][o]
         add(f"wgrad{l} colsum", "read_b32", [ln for ln in range(64)], ((N + 63) // 64) * a.R)
         if l > 0:
-            Wc = [(4 * (ln >> 4)) * ldw[l] + (ln & 15) for ln in range(64)]
-            Ad = [(ln & 15) * ldz + 4 * (ln >> 4) for ln in range(64)]
+            Wc = [(4 * (ln >> 4)) * ldw[l] + ((ln & 15) ^ sw(4 * (ln >> 4))) for ln in range(64)]
+            Ad = [(ln & 15) * ldz + ((4 * (ln >> 4)) ^ sw(ln & 15)) for ln in range(64)]
             add(f"dgrad{l} W", "read_b32", Wc, it * ot * 4)
             add(f"dgrad{l} dZ", "read_b128", Ad, it * ot * RT)
-            Od = [(4 * (ln >> 4)) * lda + (ln & 15) for ln in range(64)]
+            Od = [(4 * (ln >> 4)) * lda + ((ln & 15) ^ sw(4 * (ln >> 4))) for ln in range(64)]
             add(f"dgrad{l} act/out", "read_b32", Od, it * RT * 4)
             add(f"dgrad{l} out", "write_b32", Od, it * RT * 4)
     tot_extra = sum(e * n for _, _, e, n in rows)
