@@ -41,8 +41,9 @@
 // logits part range of scoring wave j of a group (parts [fl_lag_w(G, j), fl_lag_w(G, j + 1)))
 __host__ __device__ inline int fl_lag_w(int G, int j) { return G - ((FL_LAG_SPR - j) * G) / FL_LAG_SPR; }
 
-// ldw = roundup16(K) + 4 (4 mod 8 floats): 16-byte aligned rows, and the 16 rows of a
-// 16-lane ds_read_b128 group land on 16 distinct 16-byte bank slots.
+// ldw = roundup16(K) + 4 (4 mod 8 floats): 16-byte aligned rows; with the chunk swizzle
+// (fl_swz below) the rows of every gfx950 ds_read_b128 lane group land on distinct 16-byte
+// bank slots.
 __host__ __device__ inline int fl_ldw(int K) { return ((K + 15) & ~15) + 4; }
 __host__ __device__ inline int fl_wrows(int N) { return (N + 15) & ~15; }
 // fp32 LDS / image chunk swizzle: row r keeps logical column k < roundup16(width) at column
