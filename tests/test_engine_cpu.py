@@ -35,6 +35,26 @@ def test_image_roundtrip(dims):
     assert abs(img.sum() - f.sum()) < 1e-3   # padding is zero
 
 
+@pytest.mark.parametrize("dims", [[14, 50, 200, 2], [5, 33, 17, 9, 4]])
+def test_image_chunk_swizzle(dims):
+    """W_l[n][k] sits at column k ^ swz(n) of image row n, swz(n) = 4 for n mod 16 in [4, 12)
+    (fl_common.h fl_swz: the fp32 kernels' bank-conflict-free LDS layout); the 4-float chunks of
+    a swizzled row trade places in pairs inside each 16-column block, and the pad columns
+    [roundup16(K), ldw) stay zero."""
+    f = init_flat(dims, 4)
+    img = dense_to_image(f, dims)
+    iw, _, _ = image_layout(dims)
+    for l, (_, (N, K), off) in enumerate(param_layout(dims)[0::2]):
+        W = f[off:off + N * K].reshape(N, K)
+        ldw = ((K + 15) & ~15) + 4
+        rows = img[iw[l]:iw[l] + ((N + 15) & ~15) * ldw].reshape(-1, ldw)
+        for n in range(N):
+            sw = 4 if 4 <= n % 16 < 12 else 0
+            for k in range(K):
+                assert rows[n, k ^ sw] == W[n, k]
+            assert not rows[n, (K + 15) & ~15:].any()
+
+
 def test_dict_flat_roundtrip():
     dims = [14, 50, 200, 2]
     f = init_flat(dims, 1)
