@@ -80,7 +80,6 @@ if nadam is not None:
         e.engine.set_debug(0)
         t = dt.view(nb, 16).cpu().numpy().astype(np.int64)
         a = da.view(-1, 16).cpu().numpy().astype(np.int64)[1:nadam]
-        tail = da.view(-1, 16).cpu().numpy().astype(np.int64)[0]
         gaps.append((a[:, 0].min() - t[:, 15].max()) * 10 / 1000)
     t0 = a[:, 0].min()
     print(f"adam: param blocks={nadam - 1} dispatch spread={(a[:,0].max()-t0)*10/1000:.2f}us "
@@ -92,7 +91,3 @@ if nadam is not None:
         d = (a[:, c] - a[:, prev]) * 10 / 1000
         print(f"   phase {prev:2d}->{c:2d}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
         prev = c
-    if tail[0] > 0 and tail[6] > 0:  # block 0: fold of the round state + the loss / metric tail
-        print(f"   tail block (0): start {(tail[0] - t0) * 10 / 1000:+.2f} us, done "
-              f"{(tail[6] - t0) * 10 / 1000:.2f} us after the first parameter block's start "
-              f"(last parameter block done {(a[:, 15].max() - t0) * 10 / 1000:.2f} us)")
