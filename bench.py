@@ -142,25 +142,6 @@ def torch_eager_anchor(X, y, dims, rounds: int = 60, warmup: int = 10) -> float:
     return (time.perf_counter() - t0) / rounds * 1e6
 
 
-def fp32_round_us(X, y, dims, a, rounds: int = 200, stream=None) -> float:
-    """Untimed companion number at the reference's precision: the same one-client round with
-    the exact-fp32 kernels (v_mfma_f32_16x16x4_f32; reference [C] trains in fp32, C:65-66),
-    graph-replayed, microseconds per round (after the bf16 timed region, one client)."""
-    from fedmi.fl.engine import EngineConfig, HipRoundEngine
-    from fedmi.models.mlp import init_flat
-    g = _pick_graph_rounds(rounds)
-    cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=rounds + 3 * g + 64, early_stop=False,
-                       graph_rounds=g, dtype="fp32")
-    eng = HipRoundEngine(X, y, 2, cfg, None, init_flat(dims, seed=0), stream=stream)
-    eng.run(32, check_every=32)
-    eng.prime_graph(g)
-    eng.stream.synchronize()
-    t0 = time.perf_counter()
-    eng._issue(rounds, close=False)
-    eng.stream.synchronize()
-    return (time.perf_counter() - t0) / rounds * 1e6
-
-
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,10 +222,9 @@ def main(argv=None):
     dev = comm.device
     dims = [14, *a.hidden, 2]
     g = a.graph_rounds or _pick_graph_rounds(a.steps)
-    # (ranks sharing one GPU: with more than two, the Adam kernels' in-kernel chunk exchange can
-    # wait on a peer whose kernel cannot become resident; classic rounds there -- the record's
-    # data_plane says so)
-    lag_off_shared = a.share_gpu and N > 2
+    # (ranks sharing one GPU: the Adam kernels' in-kernel chunk exchange needs every rank's
+    # exchanging blocks resident at once; make_peer_allreduce bounds the grid for that --
+    # fedmi.parallel.peer.shared_adam_grid -- so the N > 1 round design is the same as on N GPUs)
     max_rounds = a.warmup + a.steps + g + 16
     # the early-stop rule runs in every round; a patience above the run's length keeps every
     # timed round live (a stop would turn the remaining rounds into no-ops)
@@ -260,13 +240,13 @@ def main(argv=None):
     # a GPU, the companion run's engine on a fresh stream ran 2.3x slower)
     stream = torch.cuda.Stream(device=dev)
 
-    def timed_rounds(rows_local: int, rows_total: int):
+    def timed_rounds(rows_local: int, rows_total: int, dtype: str = a.dtype):
         """Build a client with `rows_local` rows (FedAvg weight rows_local / rows_total), warm up,
         time exactly a.steps rounds (max over ranks), close + check; returns (dt, engine, primed)."""
         X, y = synth_shard(rows_local, comm.rank, dev)
         cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=max_rounds, early_stop=a.early_stop,
                            patience=patience, rows_per_block=a.rows_per_block, graph_rounds=g,
-                           dtype=a.dtype, lagged_eval=not lag_off_shared)
+                           dtype=dtype)
         eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank), n_total=rows_total, stream=stream)
         # warm-up: the requested rounds, then (uncounted) the graph of the timed region is
         # captured, instantiated and replayed once, so the timed steps are steady-state replays
@@ -309,6 +289,7 @@ def main(argv=None):
                                "lagged-eval+late-fold" if eng.engine.late_fold else
                                "lagged-eval" if eng.engine.lagged else "classic"),
               "rows_per_block": eng.R, "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
+              "adam_grid": int(eng._peer.adam_grid) if eng._peer is not None else 0,
               "lagged_eval": eng.cfg.lagged_eval, "final_acc": float(h["global"][-1][0])}
     X, y = eng.X, eng.y
     del eng
@@ -333,7 +314,12 @@ def main(argv=None):
         barrier()
     fp32_us = None
     if N == 1 and a.dtype != "fp32" and not a.no_fp32:
-        fp32_us = fp32_round_us(X, y, dims, a, stream=stream)
+        # the reference-precision companion, timed EXACTLY like the headline: same shard, same
+        # --warmup / --steps, early-stop rule live, one graph replay of the timed steps
+        dtf, engf, _ = timed_rounds(rows_local, rows_total, dtype="fp32")
+        fp32_us = dtf / a.steps * 1e6
+        del engf
+        gc.collect()
     # rounds-to-target is measured with the same kernels (dtype) as the throughput
     rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=design["lagged_eval"])
     if comm.rank == 0:
@@ -357,9 +343,8 @@ def main(argv=None):
                        "global_batch": rows_total, "seq_len": 1,
                        "parallelism": f"fedavg{N} (1 client/{'shared ' if a.share_gpu else ''}GPU, "
                                       f"{design['aggregation']} all-reduce)",
-                       "data_plane": design["aggregation"] + (
-                           " (classic rounds: lagged evaluation disabled for > 2 ranks sharing one GPU)"
-                           if lag_off_shared else ""),
+                       "data_plane": design["aggregation"],
+                       "adam_grid": design["adam_grid"],
                        "round_design": design["round_design"],
                        "rccl_env": comm.rccl_env,
                        "rows_per_client": a.rows_per_client or reference_rows(a.total_rows, N, 0),

@@ -613,7 +613,7 @@ class HipRoundEngine(RoundEngineBase):
         self.stream.wait_stream(torch.cuda.current_stream(dev))
         self.rounds_issued = 0
         self._stopped_seen = False
-        self._native_comm = comm.native if (comm is not None and self.world > 1) else None
+        self._native_comm = None
         # one-shot xGMI all-reduce of [image | tails] (collective set-up; None -> RCCL)
         self._peer = None
         if self.world > 1 and comm_buffers is None and getattr(comm, "peer_allreduce", False):
@@ -625,6 +625,11 @@ class HipRoundEngine(RoundEngineBase):
             self._peer = make_peer_allreduce(comm, comm_len, dev, n_chunks=n_chunks)
             if self._peer is not None:
                 self.engine.attach_peer(self._peer)
+        if self.world > 1 and self._peer is None and comm_buffers is None and comm is not None \
+                and hasattr(comm, "rccl"):
+            # RCCL only when the peer plane is off or fell back (every rank agreed on that above),
+            # so this lazy, bounded bootstrap runs on every rank or on none
+            self._native_comm = comm.rccl()
         self._graph_ready = False
 
     def slab_partials(self) -> torch.Tensor:

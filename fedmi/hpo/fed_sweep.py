@@ -110,7 +110,7 @@ class FedTrialGroup:
                                                        comm_buffers=views))
             self.stream = torch.cuda.Stream(device=dev)
             self.stream.wait_stream(torch.cuda.current_stream(dev))
-            self._native = comm.native if (comm is not None and self.world > 1) else None
+            self._native = comm.rccl() if (comm is not None and self.world > 1 and hasattr(comm, "rccl")) else None
             # trial batches: same-shape engines, local steps descending (TrialBatch's order)
             self.batches = []
             if batched:

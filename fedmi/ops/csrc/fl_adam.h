@@ -51,6 +51,13 @@ __device__ __forceinline__ float adam_update(const FLConfig& c, const FLBuffers&
                                             const FLState& S, int local_step, int last_local_step, int pack, int j,
                                             int pk, bool is_bias, int wlo_delta, float (*part)[64], int lane, float p,
                                             float m, float v, float anc, float scale) {
+    if (b.undo != nullptr && local_step == 0) {
+        // a late fold may discard this round: keep the parameter's pre-round state (FLBuffers::undo)
+        b.undo[j] = p;
+        b.undo[c.tail_off + j] = m;
+        b.undo[2 * c.tail_off + j] = v;
+        if (pack) pack_store(reinterpret_cast<char*>(b.undo + 3 * c.tail_off), pk, is_bias, wlo_delta, p);
+    }
     // `scale`: this round's FedAvg weight (rtab); 0 = the client is not sampled this round: no
     // update, its local model stays the round's input (global) model and it contributes nothing
     if (scale != 0.f) {
@@ -77,6 +84,17 @@ __device__ __forceinline__ float adam_update(const FLConfig& c, const FLBuffers&
     if (pack) pack_store(b.pk_local, pk, is_bias, wlo_delta, p);
     if (last_local_step) comm[j] = p * scale;
     return p * scale;
+}
+
+// A late fold found that the round before this one ran past the stop (FLState::late): put the
+// parameter's local value, Adam moments and packed local image back to their pre-round state.
+__device__ __forceinline__ void undo_restore(const FLConfig& c, const FLBuffers& b, int pack, int j, int pk,
+                                             bool is_bias, int wlo_delta) {
+    const float p = b.undo[j];
+    b.local[j] = p;
+    b.m[j] = b.undo[c.tail_off + j];
+    b.v[j] = b.undo[2 * c.tail_off + j];
+    if (pack) pack_store(b.pk_local, pk, is_bias, wlo_delta, p);
 }
 
 // Chunk ids of the Adam-fused exchange (peer_device.h): the final metric tails, the early lag

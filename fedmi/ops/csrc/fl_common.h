@@ -233,6 +233,13 @@ struct FLBuffers {
     const float* rtab;
     float* cnt;         // FL_EVAL_LAGGED: confusion counts of the previous round's local model
     float* lbuf;        // FL_EVAL_LAGGED: the previous round's loss, published one round later
+    // Late fold (FLState::late; lagged rounds over an external all-reduce with early stopping):
+    // [local | m | v] (3 x Pimg floats) and the packed local image (undo_pk_bytes) as they were
+    // before the last live round's first optimizer step, written by adam_update; a round found
+    // to have run past the stop restores them, so the local model and the Adam moments match a
+    // run that stopped in time.  nullptr: no round can be discarded.
+    float* undo;
+    int undo_pk_bytes;
     int* sat;           // optional: set to 1 by the Adam kernel when an fp16 slab partial it reads is
                         // saturated (|x| = 65504, slab_store_h's clamp) or not finite
 };

@@ -14,12 +14,14 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
 #include <cmath>
+#include <thread>
 #include <vector>
 
 #include "fl_common.h"
@@ -54,15 +56,44 @@ static inline T* as_ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
 // ---------------------------------------------------------------------------------------
 // RCCL communicator: one per process (= one per GPU / federated client).
 // ---------------------------------------------------------------------------------------
+//
+// The communicator is NON-BLOCKING (ncclConfig_t::blocking = 0): ncclCommInitRankConfig returns at
+// once and the bootstrap (unique-id rendezvous, topology, rings) runs inside RCCL while this thread
+// polls ncclCommGetAsyncError against a deadline with the GIL released.  A peer that never calls
+// init (died before it, stuck elsewhere) therefore ends in ncclCommAbort and a Python exception
+// naming the deadline, not in a process blocked forever inside ncclCommInitRank -- the reference's
+// contract is "any failure -> comm.Abort()" (C:203-205).  Every later call on a non-blocking
+// communicator may also return ncclInProgress (e.g. the lazy connection set-up of the first
+// collective); `settle` waits those out under the same deadline.
 class RcclComm {
   public:
-    RcclComm(int nranks, int rank, py::bytes uid, int device) : nranks_(nranks), rank_(rank) {
+    RcclComm(int nranks, int rank, py::bytes uid, int device, double timeout_s)
+        : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
         std::string s = uid;
         if (s.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad RCCL unique id size");
         ncclUniqueId id;
         std::memcpy(&id, s.data(), sizeof(id));
         HIP_CHECK(hipSetDevice(device));
-        NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t r;
+        {
+            py::gil_scoped_release nogil;
+            r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
+            if (r == ncclSuccess || r == ncclInProgress) r = wait_settled();
+        }
+        if (r != ncclSuccess) {
+            if (comm_) {
+                py::gil_scoped_release nogil;
+                ncclCommAbort(comm_);
+            }
+            comm_ = nullptr;
+            if (r == ncclInProgress)
+                throw std::runtime_error("RCCL bootstrap timed out after " + std::to_string(timeout_s_) +
+                                         " s (rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                                         "): a peer never joined ncclCommInitRankConfig; communicator aborted");
+            throw std::runtime_error(std::string("RCCL bootstrap failed: ") + ncclGetErrorString(r));
+        }
     }
     ~RcclComm() { destroy(); }
 
@@ -73,24 +104,32 @@ class RcclComm {
     }
 
     void allreduce_f32(uintptr_t buf, size_t count, uintptr_t stream) {
-        NCCL_CHECK(ncclAllReduce(as_ptr<float>(buf), as_ptr<float>(buf), count, ncclFloat32, ncclSum,
-                                 comm_, as_stream(stream)));
+        settle(ncclAllReduce(as_ptr<float>(buf), as_ptr<float>(buf), count, ncclFloat32, ncclSum, live(),
+                             as_stream(stream)), "ncclAllReduce(f32)");
     }
     void allreduce_bf16(uintptr_t buf, size_t count, uintptr_t stream) {
-        NCCL_CHECK(ncclAllReduce(as_ptr<void>(buf), as_ptr<void>(buf), count, ncclBfloat16, ncclSum, comm_,
-                                 as_stream(stream)));
+        settle(ncclAllReduce(as_ptr<void>(buf), as_ptr<void>(buf), count, ncclBfloat16, ncclSum, live(),
+                             as_stream(stream)), "ncclAllReduce(bf16)");
     }
     void allreduce_f64(uintptr_t buf, size_t count, uintptr_t stream) {
-        NCCL_CHECK(ncclAllReduce(as_ptr<double>(buf), as_ptr<double>(buf), count, ncclFloat64, ncclSum,
-                                 comm_, as_stream(stream)));
+        settle(ncclAllReduce(as_ptr<double>(buf), as_ptr<double>(buf), count, ncclFloat64, ncclSum, live(),
+                             as_stream(stream)), "ncclAllReduce(f64)");
     }
     void broadcast_bytes(uintptr_t buf, size_t nbytes, int root, uintptr_t stream) {
-        NCCL_CHECK(ncclBroadcast(as_ptr<void>(buf), as_ptr<void>(buf), nbytes, ncclUint8, root, comm_,
-                                 as_stream(stream)));
+        settle(ncclBroadcast(as_ptr<void>(buf), as_ptr<void>(buf), nbytes, ncclUint8, root, live(),
+                             as_stream(stream)), "ncclBroadcast");
     }
     void allgather_f32(uintptr_t send, uintptr_t recv, size_t count, uintptr_t stream) {
-        NCCL_CHECK(ncclAllGather(as_ptr<float>(send), as_ptr<float>(recv), count, ncclFloat32, comm_,
-                                 as_stream(stream)));
+        settle(ncclAllGather(as_ptr<float>(send), as_ptr<float>(recv), count, ncclFloat32, live(),
+                             as_stream(stream)), "ncclAllGather");
+    }
+    // ncclCommGetAsyncError of a live communicator (0 = ncclSuccess); lets a watchdog see an
+    // asynchronous RCCL failure without issuing a collective.
+    int async_error() const {
+        if (!comm_) return (int)ncclInvalidArgument;
+        ncclResult_t st = ncclSuccess;
+        ncclCommGetAsyncError(comm_, &st);
+        return (int)st;
     }
     void abort() {
         if (comm_) {
@@ -109,7 +148,38 @@ class RcclComm {
     ncclComm_t handle() const { return comm_; }
 
   private:
+    ncclComm_t live() const {
+        if (!comm_) throw std::runtime_error("RCCL communicator used after abort/destroy");
+        return comm_;
+    }
+    // Poll the communicator's state until it leaves ncclInProgress or the deadline passes
+    // (returns ncclInProgress then).  Called without the GIL.
+    ncclResult_t wait_settled() const {
+        const auto t_end = std::chrono::steady_clock::now() +
+                           std::chrono::microseconds((long long)(timeout_s_ * 1e6));
+        ncclResult_t st = ncclInProgress;
+        for (;;) {
+            if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) return ncclInternalError;
+            if (st != ncclInProgress) return st;
+            if (std::chrono::steady_clock::now() >= t_end) return ncclInProgress;
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
+    void settle(ncclResult_t r, const char* what) {
+        if (r == ncclInProgress) {
+            if (PyGILState_Check()) {
+                py::gil_scoped_release nogil;
+                r = wait_settled();
+            } else {
+                r = wait_settled();
+            }
+        }
+        if (r != ncclSuccess)
+            throw std::runtime_error(std::string("RCCL error ") +
+                                     (r == ncclInProgress ? "timeout" : ncclGetErrorString(r)) + " in " + what);
+    }
     int nranks_, rank_;
+    double timeout_s_;
     ncclComm_t comm_ = nullptr;
 };
 
@@ -254,10 +324,22 @@ class FLEngine {
             b_.pk_global = pk_;
             b_.pk_local = pk_ + e_.param_bytes;
         }
+        if (lag_ok_ && c_.es_enabled) {
+            // pre-round [local | m | v | packed local image] for a round a late fold discards
+            // (FLBuffers::undo); used only while late_fold() (refresh_undo)
+            if ((e_.param_bytes & 3) != 0 || (d_.Pimg & 3) != 0)
+                throw std::runtime_error("undo buffer: image sizes must be multiples of 4");
+            const size_t bytes = 3 * (size_t)d_.Pimg * sizeof(float) + (dtype_ == 1 ? (size_t)e_.param_bytes : 0);
+            HIP_CHECK(hipMalloc(&undo_, bytes));
+            HIP_CHECK(hipMemset(undo_, 0, bytes));
+            b_.undo_pk_bytes = dtype_ == 1 ? e_.param_bytes : 0;
+        }
+        refresh_undo();
     }
 
     ~FLEngine() {
         drop_graph();
+        if (undo_) (void)hipFree(undo_);
         if (pk_) (void)hipFree(pk_);
         if (lagbuf_) (void)hipFree(lagbuf_);
     }
@@ -401,6 +483,8 @@ class FLEngine {
     // output buffer a late stop republishes from.
     bool lagged() const { return lag_ok_ && (!c_.es_enabled || xchg_ || peer_ == nullptr); }
     bool late_fold() const { return lagged() && c_.es_enabled && !xchg_; }
+    // The kernels keep / restore the pre-round state only where a round can be discarded.
+    void refresh_undo() { b_.undo = (late_fold() && undo_ != nullptr) ? undo_ : nullptr; }
     bool adam_exchange() const { return xchg_; }
     bool fused() const { return fused_; }
 
@@ -444,6 +528,7 @@ class FLEngine {
         // table for every Adam block (+ the tail block); one local step per round
         // (chunks: every Adam block, the tail block and the early lag-region chunk)
         xchg_ = lag_ok_ && c_.local_steps == 1 && p.n_chunks() >= (d_.P + 63) / 64 + 2;
+        refresh_undo();
         std::memset(&pp_, 0, sizeof(pp_));
         if (dtype_ == 1) {
             pp_.pk = b_.pk_global;
@@ -735,6 +820,7 @@ class FLEngine {
     bool prev_afold_ = false;  // ... and its Adam kernel folded that predecessor (exchanged in-kernel)
     bool need_pack_ = true;  // host changed the global weights: repack before the next round
     PeerAllReduce* peer_ = nullptr;  // one-shot xGMI all-reduce (nullptr: RCCL)
+    float* undo_ = nullptr;          // FLBuffers::undo storage (lagged engines with early stopping)
     PeerPack pp_;                    // its bf16 pack epilogue (bf16 mode)
     bool eval_fedavg_ = true;  // world > 1 with peer: evaluation + all-reduce in one kernel
     bool fused_ = false;       // rounds evaluate the previous round inside the train kernel
@@ -987,9 +1073,10 @@ static py::dict device_info(int dev) {
 PYBIND11_MODULE(_fedmi_hip, m) {
     m.doc() = "fedmi native runtime: fused FL round kernels (gfx950), HIP graphs, RCCL";
     py::class_<RcclComm>(m, "RcclComm")
-        .def(py::init<int, int, py::bytes, int>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
-             py::arg("device"))
+        .def(py::init<int, int, py::bytes, int, double>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
+             py::arg("device"), py::arg("timeout_s") = 120.0)
         .def_static("unique_id", &RcclComm::unique_id)
+        .def("async_error", &RcclComm::async_error)
         .def("allreduce_f32", &RcclComm::allreduce_f32)
         .def("allreduce_f64", &RcclComm::allreduce_f64)
         .def("allreduce_bf16", &RcclComm::allreduce_bf16)

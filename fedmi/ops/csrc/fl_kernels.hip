@@ -464,6 +464,18 @@ __global__ void fl_finalize_kernel(MLPDesc d, FLConfig c, FLBuffers b, float* __
     if (late && prev_out != nullptr)
         for (int i = threadIdx.x * 4; i < d.Pimg; i += 64 * 4)
             *reinterpret_cast<float4*>(pg + i) = *reinterpret_cast<const float4*>(prev_out + i);
+    if (late && b.undo != nullptr) {
+        // ... and the local model, Adam moments and packed local image of that round too
+        float* const dst[3] = {b.local, b.m, b.v};
+        for (int a = 0; a < 3; ++a)
+            for (int i = threadIdx.x * 4; i < d.Pimg; i += 64 * 4)
+                *reinterpret_cast<float4*>(dst[a] + i) = *reinterpret_cast<const float4*>(b.undo + a * d.Pimg + i);
+        if (b.pk_local != nullptr) {
+            const char* src = reinterpret_cast<const char*>(b.undo + 3 * d.Pimg);
+            for (int i = threadIdx.x * 4; i < b.undo_pk_bytes; i += 64 * 4)
+                *reinterpret_cast<uint32_t*>(b.pk_local + i) = *reinterpret_cast<const uint32_t*>(src + i);
+        }
+    }
     if (threadIdx.x != 0) return;
     S.live = 0;
     S.late = late;

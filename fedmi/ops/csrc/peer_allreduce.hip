@@ -107,6 +107,9 @@ PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, doubl
     // FEDMI_PEER_LL=0: weight chunks through publish / wait / pull instead (A/B)
     const char* ll_env = std::getenv("FEDMI_PEER_LL");
     use_ll_ = n_chunks_ > 0 && !(ll_env != nullptr && std::strcmp(ll_env, "0") == 0);
+    // FEDMI_ADAM_GRID=G: the LL Adam kernel on G workgroups (ranks sharing one GPU; PeerArgs)
+    const char* ag_env = std::getenv("FEDMI_ADAM_GRID");
+    if (ag_env != nullptr && *ag_env) adam_grid_ = std::max(0, std::atoi(ag_env));
     // Uncached device memory (MTYPE UC, what RCCL uses for its xGMI buffers): peers write the
     // flags and read the send buffers over xGMI, and no L2 -- this GPU's or a peer's -- may
     // hold a stale copy of either.  The send buffers are written once per round (~50 KB),
@@ -254,6 +257,7 @@ PeerArgs PeerAllReduce::args(int parity, float* out, long long n_w) const {
         }
     }
     a.rank = rank_;
+    a.adam_grid = adam_grid_;
     return a;
 }
 
@@ -299,6 +303,7 @@ void register_peer(py::module_& m) {
                  PHIP(hipGetLastError());
              })
         .def_property_readonly("uses_ll", &PeerAllReduce::uses_ll)
+        .def_property("adam_grid", &PeerAllReduce::adam_grid, &PeerAllReduce::set_adam_grid)
         .def("fill_test",
              [](const PeerAllReduce& p, int parity, unsigned salt, uintptr_t stream) {
                  const long long n = p.n_floats();

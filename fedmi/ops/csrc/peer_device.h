@@ -73,6 +73,9 @@ struct PeerArgs {
     // allocation.  nullptr: the chunks go through the publish / wait / pull protocol.
     unsigned long long* ll_dst[PEER_MAX_WORLD];  // rank j's ring (mapped)
     unsigned long long* ll;                      // my ring
+    // > 0: the LL Adam kernel runs on this many workgroups, each walking several Adam blocks
+    // (fl_adam_local.hip fl_adam_ll_grid_kernel) -- for ranks that share one GPU
+    int adam_grid;
 };
 
 // All-reduce blocks of a fused evaluation + FedAvg kernel (FL_THREADS = 512 threads each):

@@ -32,6 +32,7 @@ from __future__ import annotations
 import contextlib
 import os
 import sys
+import time
 from typing import Any, List, Optional
 
 import torch
@@ -114,13 +115,14 @@ def pin_rccl_env(proto: str) -> dict:
 
 
 class Comm:
-    """``rccl=False`` (with ``backend='xgmi'``) skips the RCCL communicator: device
+    """``rccl=False`` (with ``backend='xgmi'``) forbids the RCCL communicator: device
     all-reduces outside the round engine then go through the host.  That is the setting for
     several ranks sharing one GPU (tests), which RCCL does not support.  ``rccl_proto``: the
-    RCCL protocol pinned for this process (:func:`pin_rccl_env`; reported as ``rccl_env``)."""
+    RCCL protocol pinned for this process (:func:`pin_rccl_env`; reported as ``rccl_env``).
+    ``rccl_timeout_s`` (or ``$FEDMI_RCCL_TIMEOUT_S``) bounds the RCCL bootstrap (:meth:`rccl`)."""
 
     def __init__(self, backend: str = "auto", device: Optional[str] = None, timeout_s: float = 600.0,
-                 rccl: bool = True, rccl_proto: str = "LL"):
+                 rccl: bool = True, rccl_proto: str = "LL", rccl_timeout_s: float = 120.0):
         self.rank, self.size, self.local_rank, self.launcher = launch_env()
         if device is None or device == "auto":
             device = "cuda" if torch.cuda.is_available() else "cpu"
@@ -141,6 +143,11 @@ class Comm:
         self.rccl_env = None     # pinned NCCL_ALGO / NCCL_PROTO when an RCCL communicator exists
         self._nccl_group = None
         self._initialized_here = False
+        self.rccl_allowed = backend == "rccl" or (backend == "xgmi" and rccl)
+        self.rccl_proto = rccl_proto
+        self.rccl_timeout_s = float(os.environ.get("FEDMI_RCCL_TIMEOUT_S", "") or rccl_timeout_s)
+        self._rccl_factory = None  # tests inject a fake bootstrap (CPU); None -> native RcclComm
+        self._agree_gen = 0
         if self.size > 1:
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -152,16 +159,102 @@ class Comm:
                     dist.init_process_group("gloo", rank=self.rank, world_size=self.size,
                                             timeout=timedelta(seconds=timeout_s))
                 self._initialized_here = True
-            if backend in ("rccl", "nccl") or (backend == "xgmi" and rccl):
+            if backend in ("rccl", "nccl"):
                 self.rccl_env = pin_rccl_env(rccl_proto)
-            if backend == "rccl" or (backend == "xgmi" and rccl):
-                from ..ops import native
-                m = native()
-                uid = [m.RcclComm.unique_id() if self.rank == 0 else None]
-                dist.broadcast_object_list(uid, src=0)
-                self.native = m.RcclComm(self.size, self.rank, uid[0], self.device.index)
+            if backend == "rccl":
+                self.rccl()  # the data plane IS the communicator: bootstrap it now (bounded)
             elif backend == "nccl":
                 self._nccl_group = dist.new_group(backend="nccl")
+            # backend "xgmi": the fused engine's data plane is the peer kernel, which needs no
+            # RCCL.  The communicator is created LAZILY (rccl()) by the callers that need one:
+            # an engine whose peer set-up fell back, the wide MLP's buckets, sweeps, [S]/[H].
+
+    # ---- bounded, agreed collective set-up over the gloo store ----
+    def _store(self):
+        return dist.distributed_c10d._get_default_store()
+
+    def agree(self, tag: str, payload: str, timeout_s: float) -> List[str]:
+        """Every rank posts ``payload`` under a fresh key and waits (at most ``timeout_s``) for
+        every other rank's.  Returns the payloads in rank order; raises ``TimeoutError`` naming
+        the ranks that never posted (died, or stuck before this point) instead of blocking in a
+        gloo collective for the process group's whole timeout."""
+        if self.size == 1:
+            return [payload]
+        self._agree_gen += 1
+        base = f"fedmi/agree/{tag}/{self._agree_gen}/"
+        store = self._store()
+        store.set(base + str(self.rank), payload)
+        keys = [base + str(r) for r in range(self.size)]
+        t_end = time.monotonic() + float(timeout_s)
+        while True:
+            missing = [r for r, k in enumerate(keys) if not store.check([k])]
+            if not missing:
+                break
+            if time.monotonic() >= t_end:
+                raise TimeoutError(f"[fedmi] {tag}: rank(s) {missing} did not report within {timeout_s:g} s "
+                                   f"(died or stuck before the {tag} step)")
+            time.sleep(0.005)
+        return [store.get(k).decode() for k in keys]
+
+    def _share_bytes(self, tag: str, data: Optional[bytes], root: int, timeout_s: float) -> bytes:
+        """Root publishes ``data`` in the store; the others wait for it, bounded."""
+        self._agree_gen += 1
+        key = f"fedmi/share/{tag}/{self._agree_gen}"
+        store = self._store()
+        if self.rank == root:
+            store.set(key, data)
+            return data
+        t_end = time.monotonic() + float(timeout_s)
+        while not store.check([key]):
+            if time.monotonic() >= t_end:
+                raise TimeoutError(f"[fedmi] {tag}: rank {root} did not publish within {timeout_s:g} s")
+            time.sleep(0.005)
+        return store.get(key)
+
+    def rccl(self):
+        """The RCCL communicator of this process, created on first use.  COLLECTIVE on first use:
+        every rank must call it at the same point (SPMD).  ``None`` when RCCL is not allowed
+        (``rccl=False``, e.g. ranks sharing one GPU; the caller then goes through the host).
+
+        Set-up is bounded and agreed: the unique id travels through the gloo store with a
+        deadline, the native init is non-blocking with a deadline (``RcclComm``: abort on
+        timeout, GIL released), and every rank then posts its outcome and waits for everyone
+        else's -- so the job either has a communicator on every rank or raises on every rank
+        with the failing ranks named; never a split state, never an unbounded hang."""
+        if self.native is not None or self.size == 1 or not self.rccl_allowed:
+            return self.native
+        if self.rccl_env is None:
+            self.rccl_env = pin_rccl_env(self.rccl_proto)
+        t = self.rccl_timeout_s
+        factory = self._rccl_factory
+        if factory is None:
+            from ..ops import native
+            m = native()
+            unique_id = m.RcclComm.unique_id
+
+            def factory(uid):
+                return m.RcclComm(self.size, self.rank, uid, self.device.index, t)
+        else:
+            unique_id = factory.unique_id
+        uid = self._share_bytes("rccl-uid", unique_id() if self.rank == 0 else None, 0, t)
+        h, err = None, ""
+        try:
+            h = factory(uid)
+        except Exception as e:  # noqa: BLE001 -- agreed below, raised on every rank
+            err = str(e).replace("\n", " ") or type(e).__name__
+        try:
+            outcome = self.agree("rccl-bootstrap", "ok" if h is not None else "fail:" + err, t)
+        except TimeoutError as e:
+            if h is not None:
+                h.abort()
+            raise RuntimeError(f"RCCL bootstrap not agreed: {e}") from None
+        bad = [f"rank {r}: {o[5:]}" for r, o in enumerate(outcome) if o != "ok"]
+        if bad:
+            if h is not None:
+                h.abort()
+            raise RuntimeError("RCCL bootstrap failed on " + "; ".join(bad))
+        self.native = h
+        return h
 
     # ---- mpi4py-compatible object API (reference call sites, SURVEY §2.4) ----
     def Get_rank(self) -> int:
@@ -216,6 +309,8 @@ class Comm:
         if self.size == 1:
             return t.mul_(scale) if scale is not None else t
         if t.is_cuda:
+            if self.native is None and self.rccl_allowed:
+                self.rccl()  # collective: every rank reaches this all-reduce together
             if self.native is not None:
                 stream = torch.cuda.current_stream(t.device).cuda_stream
                 if scale is not None:

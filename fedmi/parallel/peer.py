@@ -12,6 +12,7 @@ communicator or ``None`` -- never a mix, so ranks cannot disagree about the data
 """
 from __future__ import annotations
 
+import os
 import sys
 from typing import Optional
 
@@ -76,6 +77,31 @@ def selftest(h, comm, device, calls: int = 4, timeout_s: float = 10.0) -> bool:
     return ok
 
 
+# 1024-thread Adam workgroups resident at once on one GPU with room left for the other ranks'
+# train kernels: at ~100 VGPRs one such workgroup fills a CU (256 CUs)
+SHARED_GPU_ADAM_SLOTS = 256
+
+
+def device_key(device) -> str:
+    """Identity of the physical GPU behind ``device`` (same string in every process that uses it)."""
+    p = torch.cuda.get_device_properties(torch.device(device))
+    uuid = getattr(p, "uuid", None)
+    if uuid is not None:
+        return str(uuid)
+    return f"{getattr(p, 'pci_domain_id', 0)}:{getattr(p, 'pci_bus_id', 0)}:{getattr(p, 'pci_device_id', 0)}"
+
+
+def shared_adam_grid(n_sharing: int, adam_blocks: int) -> int:
+    """Workgroups of the LL Adam kernel when ``n_sharing`` exchanging ranks sit on ONE GPU
+    (0 = the full grid of ``adam_blocks``).  Every Adam block spins until the same block of
+    every rank has pushed its chunk, so all ranks' blocks must be co-resident; when the full
+    grids cannot be, each rank walks its blocks on 128 / n_sharing workgroups
+    (fl_adam_ll_grid_kernel, bit-identical)."""
+    if n_sharing < 2 or n_sharing * adam_blocks <= SHARED_GPU_ADAM_SLOTS:
+        return 0
+    return max(1, (SHARED_GPU_ADAM_SLOTS // 2) // n_sharing)
+
+
 def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, check: bool = True,
                         n_chunks: int = 0):
     """Collective.  Returns a native ``PeerAllReduce`` of ``n_floats`` floats, open and
@@ -92,8 +118,15 @@ def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, ch
         handle = bytes(h.handle())
     except Exception as e:  # noqa: BLE001 -- reported, and every rank falls back together
         handle, why = None, f"rank {comm.rank}: {e}"
-    handles = comm.allgather(handle)
+    gathered = comm.allgather((handle, device_key(device)))
+    handles = [g[0] for g in gathered]
     ok = all(x is not None for x in handles)
+    if ok and n_chunks > 0:
+        # ranks sharing this rank's GPU (tests, bench --share-gpu): bound the spinning Adam grid
+        env = os.environ.get("FEDMI_ADAM_GRID", "")
+        if env == "":
+            mine = gathered[comm.rank][1]
+            h.adam_grid = shared_adam_grid(sum(g[1] == mine for g in gathered), n_chunks - 1)
     if ok:
         try:
             h.open(handles)

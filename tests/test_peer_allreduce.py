@@ -224,3 +224,93 @@ def test_peer_many_ranks_lagged_adam_exchange(world):
         np.testing.assert_array_equal(ca, cb)
     for r in range(1, world):
         np.testing.assert_array_equal(out[0][1][1][0], out[r][1][1][0])
+
+
+def _run_prod(comm, X, y, flat, n_total, lagged: bool, rounds: int):
+    """The bench's N > 1 round at the reference shape: MLP 14-50-200-2, bf16, early-stop rule
+    live (patience past the run), graph-replayed chunks of 16 rounds."""
+    from fedmi.fl.engine import EngineConfig, HipRoundEngine
+    cfg = EngineConfig(hidden=(50, 200), max_rounds=rounds + 40, early_stop=True, patience=rounds + 41,
+                       dtype="bf16", graph_rounds=16, lagged_eval=lagged)
+    e = HipRoundEngine(X, y, 2, cfg, comm, flat, n_total=n_total)
+    info = {"adam_exchange": bool(e.engine.adam_exchange), "lagged": bool(e.engine.lagged),
+            "adam_grid": int(e._peer.adam_grid) if e._peer is not None else -1,
+            "uses_ll": bool(e._peer.uses_ll) if e._peer is not None else False, "R": e.R}
+    e.run(rounds)
+    e.sync_history()
+    out = (e.global_flat(), e.history(), e.local_flat(), info)
+    del e
+    return out
+
+
+def _worker_prod(rank, world, port, rounds, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        import gc
+        import torch
+        from bench import reference_rows, synth_shard
+        from fedmi.models.mlp import init_flat
+        from fedmi.parallel.comm import Comm
+        # RCCL allowed: the xgmi plane must never bootstrap it while the peer plane works
+        comm = Comm(backend="xgmi", device="cuda:0", rccl=True)
+        dev = comm.device
+        rows = reference_rows(8000, world, rank)           # 1000 rows per client at world 8
+        X, y = synth_shard(rows, rank, dev)
+        flat = init_flat([14, 50, 200, 2], seed=rank)
+        res = {}
+        res["ll"] = _run_prod(comm, X, y, flat, 8000, True, rounds)
+        gc.collect()
+        os.environ["FEDMI_PEER_LL"] = "0"                   # publish / wait / pull weight chunks
+        try:
+            res["pull"] = _run_prod(comm, X, y, flat, 8000, True, rounds)
+        finally:
+            del os.environ["FEDMI_PEER_LL"]
+        gc.collect()
+        res["classic"] = _run_prod(comm, X, y, flat, 8000, False, rounds)   # standalone peer kernel
+        res["rccl_created"] = comm.native is not None
+        torch.cuda.synchronize()
+        comm.Barrier()
+        q.put((rank, res, None))
+        comm.close()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(900)
+def test_peer_world8_production_shape_adam_exchange():
+    """SCALE's default N = 8 round before any 8-GPU node runs it: 8 ranks (sharing cuda:0),
+    the reference model 14-50-200-2 on the reference's 1000-row shards, lagged evaluation with
+    FedAvg inside the Adam kernel (LL chunks, and publish / wait / pull chunks), early-stop
+    rule live, 64 graph-replayed rounds: bit-identical weights, history and per-client metrics
+    to classic rounds over the standalone peer kernel.  The shared GPU cannot hold 8 full Adam
+    grids (8 x 179 spinning 1024-thread blocks), so the exchange runs on the bounded grid
+    (peer.shared_adam_grid -> 16 workgroups per rank, fl_adam_ll_grid_kernel) -- the same
+    per-block computation.  RCCL is allowed but never bootstrapped (the xgmi plane is lazy)."""
+    world, rounds = 8, 64
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_prod, args=(r, world, port, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=800) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+    for rank, res, err in out:
+        assert err is None, f"rank {rank}:\n{err}"
+        (wl, hl, ll, il), (wp, hp, lp, ip), (wc, hc, lc, ic) = res["ll"], res["pull"], res["classic"]
+        assert il["adam_exchange"] and il["uses_ll"] and il["adam_grid"] == 16, il
+        assert ip["adam_exchange"] and not ip["uses_ll"], ip
+        assert not ic["adam_exchange"] and not ic["lagged"], ic
+        assert not res["rccl_created"]
+        assert hl["rounds_run"] == hc["rounds_run"] == rounds and hl["stop_round"] < 0
+        for name, (w, h, lo) in (("ll", (wl, hl, ll)), ("pull", (wp, hp, lp))):
+            np.testing.assert_array_equal(w, wc, err_msg=f"rank {rank} {name}: global weights")
+            np.testing.assert_array_equal(lo, lc, err_msg=f"rank {rank} {name}: local weights")
+            np.testing.assert_array_equal(h["global"], hc["global"], err_msg=f"rank {rank} {name}: metrics")
+            np.testing.assert_array_equal(h["per_rank"], hc["per_rank"])
+            np.testing.assert_array_equal(h["loss"], hc["loss"])
+    for r in range(1, world):
+        np.testing.assert_array_equal(out[0][1]["ll"][0], out[r][1]["ll"][0])

@@ -101,7 +101,8 @@ def test_lagged_rounds_with_early_stop_over_rccl(check_every, seed):
     stop is found -- by the next Adam kernel or by the finalize kernel (``check_every`` 2: every
     other round closes a host chunk) -- and is discarded.  Weights, metric history, loss and the
     stop round are bitwise equal to classic rounds (a separate evaluation per round) over the same
-    one-rank RCCL communicator."""
+    one-rank RCCL communicator -- and so are the local model, the Adam moments and the local
+    evaluation, which the discarded round's step had already changed."""
     import torch
     from fedmi.data.synthetic import make_income_like
     from fedmi.fl.engine import EngineConfig, HipRoundEngine
@@ -118,14 +119,21 @@ def test_lagged_rounds_with_early_stop_over_rccl(check_every, seed):
         assert e.engine.lagged == lag and e.engine.late_fold == lag
         e.run(300, check_every=check_every)
         h = e.history()
-        res.append((e.global_flat(), h, e.engine.eval_launches))
-    (wl, hl, ev_l), (wc, hc, ev_c) = res
+        st = e.portable_state()
+        res.append((e.global_flat(), h, e.engine.eval_launches, e.local_flat(), st, e.confusion()))
+    (wl, hl, ev_l, ll, sl, cl), (wc, hc, ev_c, lc, sc, cc) = res
     assert hc["stop_round"] > 0, "the classic run must stop early for this test to mean anything"
     assert hl["stop_round"] == hc["stop_round"] and hl["rounds_run"] == hc["rounds_run"]
     np.testing.assert_array_equal(wl, wc)
     np.testing.assert_array_equal(hl["global"], hc["global"])
     np.testing.assert_array_equal(hl["per_rank"], hc["per_rank"])
     np.testing.assert_array_equal(hl["loss"], hc["loss"])
+    # the discarded round's local step is undone too (FLBuffers::undo): local model,
+    # Adam moments and the local evaluation match the run that stopped in time
+    np.testing.assert_array_equal(ll, lc)
+    for k in ("exp_avg", "exp_avg_sq"):
+        np.testing.assert_array_equal(np.asarray(sl[k]), np.asarray(sc[k]), err_msg=k)
+    np.testing.assert_array_equal(cl, cc)
     # lagged rounds evaluate only the closing round of each host chunk
     assert ev_l < ev_c
     torch.cuda.synchronize()
@@ -186,3 +194,52 @@ class _OneRankDevComm:
         self.calls += 1
         self.scales.append(scale)
         return t
+
+
+_BOOT_CHILD = r"""
+import sys, time
+import torch
+from fedmi.ops import native
+m = native()
+torch.cuda.set_device(0)
+rank = int(sys.argv[1])
+uid = m.RcclComm.unique_id()
+t0 = time.monotonic()
+try:
+    m.RcclComm(2, rank, uid, 0, 5.0)
+    print("NO_RAISE", flush=True)
+except RuntimeError as e:
+    print(f"RAISED {time.monotonic() - t0:.2f} {e}", flush=True)
+# the process is still usable: a fresh one-rank communicator all-reduces
+rc = m.RcclComm(1, 0, m.RcclComm.unique_id(), 0)
+x = torch.arange(1000, dtype=torch.float32, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+rc.allreduce_f32(x.data_ptr(), x.numel(), s)
+torch.cuda.synchronize()
+print("AFTER_OK" if torch.equal(x.cpu(), torch.arange(1000, dtype=torch.float32)) else "AFTER_BAD", flush=True)
+rc.destroy()
+"""
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("rank", [0, 1])
+def test_rccl_bootstrap_times_out_when_peer_never_joins(rank):
+    """A world-2 RCCL bootstrap whose other rank never calls init (rank 0 = the unique-id root,
+    rank 1 = a joining rank whose root never arrives): the non-blocking ncclCommInitRankConfig is
+    polled against the 5 s deadline with the GIL released, aborted, and raises a clear error --
+    instead of blocking in ncclCommInitRank forever (reference contract: any failure ->
+    comm.Abort(), C:203-205).  Run in a child process under its own time limit, so a
+    regression shows up as a failed test, not a hung session."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _BOOT_CHILD, str(rank)], cwd=root, capture_output=True, text=True,
+                       timeout=180)
+    out = p.stdout
+    assert p.returncode == 0, (p.returncode, out, p.stderr[-3000:])
+    line = next((x for x in out.splitlines() if x.startswith(("RAISED", "NO_RAISE"))), "")
+    assert line.startswith("RAISED"), (out, p.stderr[-3000:])
+    elapsed = float(line.split()[1])
+    assert "timed out" in line and elapsed < 30.0, line
+    assert "AFTER_OK" in out, out
