@@ -341,7 +341,8 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
         "n_iter": torch.zeros(T, dtype=torch.int32, device=dev),
         "active": torch.ones(T, dtype=torch.int32, device=dev),
         "curve": torch.zeros(T, max_iter, dtype=torch.float64, device=dev),
-        "xb": torch.zeros(B, F, **f32), "yb": torch.zeros(B, dtype=torch.int32, device=dev),
+        # (the fused float64 step gathers each trial's rows into its own [B][F] slice)
+        "xb": torch.zeros(T, B, F, **f32), "yb": torch.zeros(B, dtype=torch.int32, device=dev),
         "acts": torch.zeros(L, T, B, maxw, **f32), "deltas": torch.zeros(L, T, B, maxw, **f32),
     }
     cfg = {"n_rows": n, "batch": B, "head": 1 if e0.n_outputs_ == 1 else 0, "style": 1,
@@ -351,6 +352,8 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
            "tol_stop": 0 if incremental else 1, "maxw": maxw}
     trainer = m.MLPTrainer64 if f64 else m.MLPTrainer
     tr = trainer(list(dims), T, cfg, {k: v.data_ptr() for k, v in bufs_t.items()})
+    for e in ests:
+        e._hip_fused = bool(tr.fused)   # two-kernel minibatch step (mlp_fused_f64.hip) ran
     stream = torch.cuda.Stream(device=dev)
     stream.wait_stream(torch.cuda.current_stream(dev))
     tr.run(max_iter, stream.cuda_stream, 8, True)

@@ -46,3 +46,30 @@ hipError_t xent_f64_launch(const double* z, int ldz, long long sZ, const int* y,
 hipError_t colsum_f64_launch(const double* X, int M, int N, int ld, double* out, double beta, int batch, long long sX,
                              long long sOut, const int* active, hipStream_t s);
 hipError_t adam_f64_launch(const Adam64Args& a, int T, hipStream_t s);
+
+// Fused float64 minibatch step (mlp_fused_f64.hip): two kernels per minibatch for sklearn's
+// Adam / binary-logistic or softmax head / L2 (style 1), no FedProx, at most SKF_MAXL layers.
+#define SKF_MAXL 4
+struct SkfArgs {
+    int L, T, P;
+    int dims[SKF_MAXL + 1];
+    int w_off[SKF_MAXL], b_off[SKF_MAXL];   // dense [N][K] weights, then the bias, per layer
+    const double* X;                        // [n][dims[0]]
+    const int* y;
+    const int* perms;                       // [epochs][n_perm]
+    const int* epoch_ctr;
+    long long n_perm;
+    int off, rows, Bmax, maxw, head;        // minibatch rows perm[off : off + rows]; head 1 = logistic
+    double inv_rows, alpha, beta1, beta2, eps, l2_coef;
+    double *params, *m, *v;                 // [T][P]
+    const double* lr;                       // [T]
+    long long* step;                        // [T] Adam step counter
+    double* loss_acc;                       // [T] epoch loss sum
+    const int* active;                      // [T]
+    double* xg;                             // [T][Bmax][dims[0]] gathered rows
+    double* acts;                           // [L][T][Bmax][maxw] hidden activations
+    double* deltas;                         // [L][T][Bmax][maxw]
+};
+bool skf_supported(const SkfArgs& a);
+size_t skf_lds_bytes(const SkfArgs& a);
+hipError_t skf_step_launch(const SkfArgs& a, hipStream_t s);

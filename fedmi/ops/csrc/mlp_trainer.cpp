@@ -14,8 +14,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "gemm_mfma.h"
@@ -175,13 +177,31 @@ class MLPTrainerT {
         acts_ = ptr_of<T>(bufs, "acts");    // [L][T][B][maxw]
         deltas_ = ptr_of<T>(bufs, "deltas");
         maxw_ = cfg["maxw"].cast<int>();
+        if constexpr (std::is_same<T, double>::value) {
+            // fused two-kernel minibatch step (mlp_fused_f64.hip) where it applies; the layered
+            // path otherwise, or with FEDMI_SK_FUSED=0 (A/B)
+            const char* env = std::getenv("FEDMI_SK_FUSED");
+            const bool want = !(env != nullptr && env[0] == '0') &&
+                              (!cfg.contains("fused") || cfg["fused"].cast<bool>());
+            if (want && style_ == 1 && mu_ == 0.0 && wd_ == 0.0 && L_ <= SKF_MAXL) {
+                SkfArgs a = fused_args(0, 1);
+                fused_ = skf_supported(a);
+            }
+        }
     }
     ~MLPTrainerT() { drop_graph(); }
 
     int P() const { return P_; }
+    bool fused() const { return fused_; }
 
     // One minibatch step on rows perm[epoch][off : off+rows].
     void step(int off, int rows, hipStream_t s) {
+        if constexpr (std::is_same<T, double>::value) {
+            if (fused_) {
+                TR_CHECK(skf_step_launch(fused_args(off, rows), s));
+                return;
+            }
+        }
         Ops::gather(X_, dims_[0], y_, perms_, epoch_ctr_, (long long)n_, off, rows, dims_[0], xb_, dims_[0], yb_, s);
         forward(xb_, rows, s, acts_, /*Bstride*/ B_);
         const long long sAct = (long long)B_ * maxw_;
@@ -250,6 +270,24 @@ class MLPTrainerT {
     }
 
   private:
+    // Arguments of the fused float64 step (mlp_fused_f64.hip); xb_ holds [T][B][dims[0]] there.
+    SkfArgs fused_args(int off, int rows) const {
+        SkfArgs a{};
+        a.L = L_; a.T = T_; a.P = P_;
+        for (int l = 0; l <= L_ && l <= SKF_MAXL; ++l) a.dims[l] = dims_[l];
+        for (int l = 0; l < L_ && l < SKF_MAXL; ++l) { a.w_off[l] = w_off_[l]; a.b_off[l] = b_off_[l]; }
+        a.X = reinterpret_cast<const double*>(X_); a.y = y_; a.perms = perms_; a.epoch_ctr = epoch_ctr_;
+        a.n_perm = n_; a.off = off; a.rows = rows; a.Bmax = B_; a.maxw = maxw_; a.head = head_;
+        a.inv_rows = 1.0 / (double)rows; a.alpha = alpha_; a.beta1 = beta1_; a.beta2 = beta2_; a.eps = eps_;
+        a.l2_coef = 0.5 * alpha_;
+        a.params = reinterpret_cast<double*>(params_); a.m = reinterpret_cast<double*>(m_);
+        a.v = reinterpret_cast<double*>(v_); a.lr = lr_; a.step = step_; a.loss_acc = loss_acc_;
+        a.active = active_;
+        a.xg = reinterpret_cast<double*>(xb_); a.acts = reinterpret_cast<double*>(acts_);
+        a.deltas = reinterpret_cast<double*>(deltas_);
+        return a;
+    }
+    bool fused_ = false;
     T* act(int l) const { return acts_ + (size_t)l * T_ * B_ * maxw_; }
     T* delta(int l) const { return deltas_ + (size_t)l * T_ * B_ * maxw_; }
 
@@ -445,12 +483,14 @@ void register_trainer(py::module_& m) {
         .def("run", &MLPTrainerT<float>::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
              py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
         .def("predict_logits", &MLPTrainerT<float>::predict_logits)
+        .def_property_readonly("fused", &MLPTrainerT<float>::fused)
         .def_property_readonly("P", &MLPTrainerT<float>::P);
     py::class_<MLPTrainerT<double>>(m, "MLPTrainer64")
         .def(py::init<std::vector<int>, int, py::dict, py::dict>())
         .def("run", &MLPTrainerT<double>::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
              py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
         .def("predict_logits", &MLPTrainerT<double>::predict_logits)
+        .def_property_readonly("fused", &MLPTrainerT<double>::fused)
         .def_property_readonly("P", &MLPTrainerT<double>::P);
     m.def("gemm", &gemm_py);
     m.def("colsum", &colsum_py);

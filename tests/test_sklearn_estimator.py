@@ -110,6 +110,7 @@ def test_hip_float64_matches_numpy(data, hl, binary):
     kw = dict(hidden_layer_sizes=hl, learning_rate_init=0.004, max_iter=60, random_state=42, tol=1e-3)
     a = MLPClassifier(backend="numpy", **kw).fit(X, y)
     b = MLPClassifier(backend="hip", dtype="float64", **kw).fit(X, y)
+    assert b._hip_fused            # the two-kernel minibatch step (mlp_fused_f64.hip) ran
     assert b.n_iter_ == a.n_iter_
     np.testing.assert_allclose(b.loss_curve_, a.loss_curve_, rtol=1e-9)
     for u, v in zip(a.coefs_ + a.intercepts_, b.coefs_ + b.intercepts_):
@@ -151,3 +152,24 @@ def test_hip_sweep_concurrent_groups_equal_sequential():
             assert r.hidden == tuple(hl) and r.lr == lrs[j] and r.n_iter == e.n_iter_
             for a, b in zip(r.weights, list(e.coefs_) + list(e.intercepts_)):
                 np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hl", [(50, 400), (400, 200), (12, 8, 6)])
+def test_hip_float64_fused_step_equals_layered(data, hl, monkeypatch):
+    """The fused float64 minibatch step (2 kernels: row pass + wgrad/Adam, mlp_fused_f64.hip)
+    against the layered path (~15 kernels per step, FEDMI_SK_FUSED=0): same epochs, loss curve
+    and weights to float64 reordering noise, packed trials included."""
+    X, y = data
+    lrs = [0.004, 0.02]
+    mk = lambda: [MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=12, random_state=42,
+                                backend="hip", dtype="float64") for lr in lrs]
+    fused = fit_packed(mk(), X, y)
+    monkeypatch.setenv("FEDMI_SK_FUSED", "0")
+    layered = fit_packed(mk(), X, y)
+    for f, l in zip(fused, layered):
+        assert f._hip_fused and not l._hip_fused
+        assert f.n_iter_ == l.n_iter_
+        np.testing.assert_allclose(f.loss_curve_, l.loss_curve_, rtol=1e-11)
+        for u, v in zip(f.coefs_ + f.intercepts_, l.coefs_ + l.intercepts_):
+            np.testing.assert_allclose(u, v, rtol=1e-9, atol=1e-11)

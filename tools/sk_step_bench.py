@@ -1,0 +1,43 @@
+"""Per-minibatch cost of the sklearn-compatible float64 trainer: fused two-kernel step
+(mlp_fused_f64.hip) vs the layered path (FEDMI_SK_FUSED=0), on the [S] model (hidden (50, 400),
+8000 rows, 200-row minibatches, 40 epochs = 1600 steps) and the [H] grid's largest packed job
+((400, 200) x 9 learning rates).  Prints one JSON line per case."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+
+def run(hl, T, epochs, fused, X, y):
+    from fedmi.models.sklearn_mlp import MLPClassifier, fit_packed
+    os.environ["FEDMI_SK_FUSED"] = "1" if fused else "0"
+    lrs = [0.002, 0.005, 0.004, 0.008, 0.01, 0.02, 0.05, 0.1, 0.2][:T]
+    ests = [MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=epochs, random_state=42,
+                          backend="hip", dtype="float64", tol=-1.0) for lr in lrs]
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fit_packed(ests, X, y)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = sum(e.n_iter_ for e in ests[:1]) * ((len(X) + 199) // 200)
+    return {"hidden": list(hl), "trials": T, "epochs": int(ests[0].n_iter_), "fused": bool(ests[0]._hip_fused),
+            "wall_s": dt, "us_per_step": dt / steps * 1e6, "final_loss": float(ests[0].loss_)}
+
+
+def main():
+    from fedmi.data.tabular import load_tabular
+    ds = load_tabular(with_mean=False)
+    X, y = ds.X_train, ds.y_train
+    cases = [((50, 400), 1, 40), ((400, 200), 9, 10), ((50,), 9, 40)]
+    for hl, T, ep in cases:
+        run(hl, T, 2, True, X, y)   # warm-up (build, first graph)
+        for fused in (True, False):
+            print(json.dumps(run(hl, T, ep, fused, X, y)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
