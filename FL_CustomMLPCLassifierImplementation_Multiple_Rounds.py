@@ -200,6 +200,7 @@ def main(argv=None):
                                    shard_mode=a.partition, alpha=a.alpha, presharded=a.synthetic,
                                    output_size=2 if a.synthetic else None,
                                    n_total=a.synthetic_rows * size if a.synthetic else None)
+    done = 0   # rounds restored from a checkpoint (not run by this process)
     if a.resume:
         done = resume(a.resume, trainer)
         if rank == 0:
@@ -226,7 +227,7 @@ def main(argv=None):
         # client, wall-clock throughput of the whole loop (host logging included)
         eng = trainer.engine
         h = trainer.history()
-        rounds_run = max(int(h["rounds_run"]), 1)
+        rounds_run = max(int(h["rounds_run"]) - done, 1)   # this process's rounds (not the resumed ones)
         comm_floats = int(eng.params[0].numel()) if hasattr(eng, "params") else int(eng.P + eng.world * eng.tail_stride)
         w.history(h, clients=size, script="C", timings=timings,
                   aggregation=getattr(eng, "aggregation", "host"),
@@ -236,8 +237,9 @@ def main(argv=None):
     if a.save:
         save_checkpoint(a.save, trainer)   # collective: every client writes its optimizer state
     if a.timing and rank == 0:
-        # BASELINE.md "[C] samples/s/client (e2e)": shard rows / (wall of main() / rounds run)
-        rounds_run = max(int(trainer.history()["rounds_run"]), 1)
+        # BASELINE.md "[C] samples/s/client (e2e)": shard rows / (wall of main() / rounds run) --
+        # the rounds THIS process ran: after --resume the history also counts the restored ones
+        rounds_run = max(int(trainer.history()["rounds_run"]) - done, 1)
         wall = time.perf_counter() - t_main
         print(f"main() wall {wall:.3f} s for {rounds_run} rounds ({t_train:.3f} s in train_and_evaluate): "
               f"e2e {len(trainer.X_local) * rounds_run / wall:,.0f} samples/s/client", flush=True)

@@ -611,6 +611,13 @@ def load_wide(path: str, client: WideClient) -> int:
         raise ValueError(f"{path}: not a wide checkpoint for dims {client.dims}")
     if int(meta["world"]) != client.world:
         raise ValueError(f"{path}: saved with {meta['world']} clients, this run has {client.world}")
+    # the optimizer schedule is part of the state: resuming a run saved at another lr / StepLR
+    # (e.g. under the reference's 0.004 before WIDE_LR became the default) must not silently
+    # continue at a different rate
+    for key, have in (("lr", client.lr), ("step_size", client.step_size), ("gamma", client.gamma)):
+        if key in meta and float(meta[key]) != float(have):
+            raise ValueError(f"{path}: saved with {key}={meta[key]}, this client has {key}={have}; "
+                             f"construct the client with {key}={meta[key]} to resume")
     R = int(meta["round"]) if fmt == "fedmi-wide-ckpt-2" else None
     files = meta.get("files", {"weights": "weights.safetensors", "client": "client{rank}.safetensors"})
     rank = client.comm.rank if client.comm is not None else 0

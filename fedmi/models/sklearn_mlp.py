@@ -358,6 +358,9 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
     stream.wait_stream(torch.cuda.current_stream(dev))
     tr.run(max_iter, stream.cuda_stream, 8, True)
     stream.synchronize()
+    if hasattr(tr, "stamps"):
+        for e in ests:
+            e._hip_stamps = list(tr.stamps())   # FEDMI_SK_STAMPS=1 (tools/sk_step_bench.py)
     flat = params.cpu().numpy()
     n_iter = bufs_t["n_iter"].cpu().numpy()
     curve = bufs_t["curve"].cpu().numpy()

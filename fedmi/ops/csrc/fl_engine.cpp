@@ -394,10 +394,33 @@ class FLEngine {
     // Record `n` rounds (n even, starting at an even round) into one hipGraph.  Round
     // indices live on the device, so the same graph is replayed for every chunk.  A graph
     // always starts from the steady state (see needs_eager_round).
+    //
+    // Captured graphs are cached by round count (up to kMaxGraphs): callers that alternate
+    // between graph lengths (run() at cfg.graph_rounds, the streaming console's shorter chunks
+    // of lagged engines) select the instantiated graph again instead of re-capturing it (ADVICE
+    // r4).  A graph is a pure function of the engine's configuration and buffers -- every change
+    // of those drops the cache (drop_graph) -- except a pending repack of host-written weights
+    // (need_pack_), which is captured into the graph's first round: with one pending the graph is
+    // captured afresh.
     void capture(int n, uintptr_t stream, RcclComm* comm) {
         if (n <= 0 || (n & 1)) throw std::runtime_error("capture: n must be a positive even number");
         if (needs_eager_round()) throw std::runtime_error("capture: issue one eager round first");
-        drop_graph();
+        for (size_t i = 0; i < graphs_.size(); ++i)
+            if (graphs_[i].n == n) {
+                if (!need_pack_ && graphs_[i].comm == comm) {
+                    select_graph((int)i);
+                    return;
+                }
+                destroy_rec(graphs_[i]);
+                graphs_.erase(graphs_.begin() + i);
+                break;
+            }
+        if ((int)graphs_.size() >= kMaxGraphs) {
+            destroy_rec(graphs_.front());
+            graphs_.erase(graphs_.begin());
+        }
+        graph_ = nullptr;
+        exec_ = nullptr;
         hipStream_t s = as_stream(stream);
         const bool pend = pending_cm_, tail = cm_in_tail_, plag = prev_lagged_, pscore = prev_scored_,
                    pafold = prev_afold_;
@@ -417,10 +440,15 @@ class FLEngine {
             eval_launches_ = ev0;
             throw;
         }
-        HIP_CHECK(hipStreamEndCapture(s, &graph_));
-        HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
-        graph_rounds_ = n;
-        graph_evals_ = eval_launches_ - ev0;  // counted per replay, not at capture
+        GraphRec rec{n, nullptr, nullptr, eval_launches_ - ev0 /* counted per replay, not at capture */, comm};
+        HIP_CHECK(hipStreamEndCapture(s, &rec.g));
+        if (hipGraphInstantiate(&rec.e, rec.g, nullptr, nullptr, 0) != hipSuccess) {
+            hipGraphDestroy(rec.g);
+            throw std::runtime_error("capture: hipGraphInstantiate failed");
+        }
+        graphs_.push_back(rec);
+        ++captures_;
+        select_graph((int)graphs_.size() - 1);
         eval_launches_ = ev0;
         pending_cm_ = pend;  // nothing ran yet: replay() applies the rounds' effect
         cm_in_tail_ = tail;
@@ -442,6 +470,7 @@ class FLEngine {
     }
 
     int graph_rounds() const { return graph_rounds_; }
+    long long graph_captures() const { return captures_; }
     // Stand-alone evaluation kernels issued so far (eager launches + every graph replay's):
     // a one-client fused run launches one per host-side weight change / run end, not per round.
     long long eval_launches() const { return eval_launches_; }
@@ -799,11 +828,35 @@ class FLEngine {
             HIP_CHECK(fl_launch_eval_fedavg_bf16(d_, ev_, c_, b_, b_.local, comm_buf(r), st_[(r + 1) & 1], a, pk, s));
     }
 
+    struct GraphRec {
+        int n;                 // rounds
+        hipGraph_t g;
+        hipGraphExec_t e;
+        long long evals;       // evaluation kernels per replay
+        RcclComm* comm;        // communicator the rounds were captured with
+    };
+    static constexpr int kMaxGraphs = 4;
+    static void destroy_rec(GraphRec& r) {
+        if (r.e) hipGraphExecDestroy(r.e);
+        if (r.g) hipGraphDestroy(r.g);
+        r.e = nullptr;
+        r.g = nullptr;
+    }
+    void select_graph(int i) {
+        graph_ = graphs_[i].g;
+        exec_ = graphs_[i].e;
+        graph_rounds_ = graphs_[i].n;
+        graph_evals_ = graphs_[i].evals;
+    }
     void drop_graph() {
-        if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
-        if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+        for (auto& r : graphs_) destroy_rec(r);
+        graphs_.clear();
+        exec_ = nullptr;
+        graph_ = nullptr;
         graph_rounds_ = 0;
     }
+    std::vector<GraphRec> graphs_;
+    long long captures_ = 0;   // graphs captured + instantiated (not counting cache hits)
 
     MLPDesc d_;
     MLPDescB e_;
@@ -1098,6 +1151,7 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def("flags", &FLEngine::flags)
         .def("set_flags", &FLEngine::set_flags)
         .def("graph_rounds", &FLEngine::graph_rounds)
+        .def_property_readonly("graph_captures", &FLEngine::graph_captures)
         .def_property_readonly("eval_launches", &FLEngine::eval_launches)
         .def("time_kernels", &FLEngine::time_kernels)
         .def("set_debug", &FLEngine::set_debug)

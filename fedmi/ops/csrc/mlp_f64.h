@@ -69,6 +69,8 @@ struct SkfArgs {
     double* xg;                             // [T][Bmax][dims[0]] gathered rows
     double* acts;                           // [L][T][Bmax][maxw] hidden activations
     double* deltas;                         // [L][T][Bmax][maxw]
+    unsigned long long* dbg;                // optional: s_memrealtime phase stamps of row block (0, 0)
+    const double* zero;                     // one 0.0 in device memory (branch-free masked loads)
 };
 bool skf_supported(const SkfArgs& a);
 size_t skf_lds_bytes(const SkfArgs& a);

@@ -42,11 +42,22 @@ __device__ __forceinline__ int skf_np(int n) { return (n + 15) & ~15; }
 // MFMA operand reads (16 rows x 4 consecutive columns per wave) hit distinct banks
 __host__ __device__ __forceinline__ int skf_ld(int np) { return np + 2 + ((np & 16) ? 16 : 0); }
 
+#define SKF_RED_DOUBLES (SKF_WAVES * 64 * 4)   // partial tiles of a k-split layer (skf_layer)
+// LDS of a row block (doubles): the layer buffers, the k-split partials, and the narrow output
+// layer's weights + bias when it runs on the VALU
+__host__ __device__ __forceinline__ int skf_narrow_doubles(const SkfArgs& a) {
+    const int C = a.dims[a.L];
+    return C <= SKF_NARROW ? C * a.dims[a.L - 1] + C : 0;
+}
 size_t skf_lds_bytes(const SkfArgs& a) {
     size_t d = (size_t)skf_ld((a.dims[0] + 15) & ~15);
     for (int l = 0; l < a.L; ++l) d += (size_t)skf_ld((a.dims[l + 1] + 15) & ~15);
-    return d * SKF_RB * sizeof(double);
+    return (d * SKF_RB + SKF_RED_DOUBLES + skf_narrow_doubles(a)) * sizeof(double);
 }
+
+// Workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding
+// global store (vmcnt 0), i.e. for the activations / deltas streaming out to memory
+__device__ __forceinline__ void skf_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ double skf_wave_sum(double v) {
 #pragma unroll
@@ -54,85 +65,157 @@ __device__ __forceinline__ double skf_wave_sum(double v) {
     return v;
 }
 
-// out[16][N] (ld_o) = act(in[16][K] (ld_i) . W^T + b): 16-column tiles round-robin over the
-// waves, k-steps in batches of SKF_KB whose 8-byte weight loads are all in flight together.
-__device__ __forceinline__ void skf_fwd_mfma(const double* __restrict__ in, int ld_i, double* __restrict__ out,
-                                             int ld_o, const double* __restrict__ W, const double* __restrict__ bias,
-                                             int K, int N, bool relu, int wave, int lane) {
-    const int steps = (K + 3) >> 2, nt_all = (N + 15) >> 4;
+// One layer of the row pass on the matrix cores (v_mfma_f64_16x16x4_f64):
+//   FWD  out[16][N] = act(src[16][K] . W^T + b)       tiles over n, k-steps over K
+//   BWD  dst[16][K] = (src[16][N] . W) * (dst > 0)     tiles over k, k-steps over N; dst holds the
+//        activation it masks and is overwritten in place (the lane that reads an activation for
+//        its mask is the lane that writes its delta)
+// The weight operands stream from L2 (8-byte loads, SKF_KB k-steps per chunk).  The row pass is
+// latency-bound, so the work is cut so that every wave holds at most ~2 chunks: a product with
+// fewer 16-wide tiles than waves is split along k into G groups (units = tile x group), whose
+// partial tiles meet in `red` (LDS) and are summed in group order; each wave walks its chunks
+// with the next chunk's loads in flight while the current one multiplies.
+// Branch-free by construction: every operand load is unconditional (clamped address, zero
+// selected after the load) and every MFMA runs (a zero weight operand, an in-range activation
+// column), so the compiler keeps the next chunk's loads in flight across the current chunk's
+// MFMAs -- with predicated loads / MFMAs it waited for ALL loads before every MFMA.
+template <bool FWD, int KB>
+__device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int ld_s, double* __restrict__ dst,
+                                             int ld_d, const double* __restrict__ W, const double* __restrict__ bias,
+                                             int K, int N, bool relu, double* __restrict__ red, int wave, int lane,
+                                             const double* __restrict__ zero) {
     const int lr = lane & 15, lg = lane >> 4;
-    for (int nt = wave; nt < nt_all; nt += SKF_WAVES) {
-        const int n = nt * 16 + lr;
-        skf_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int s0 = 0; s0 < steps; s0 += SKF_KB) {
-            double bw[SKF_KB];
+    const int ntiles = FWD ? (N + 15) >> 4 : (K + 15) >> 4;
+    const int steps = FWD ? (K + 3) >> 2 : (N + 3) >> 2;
+    const int nb = (steps + KB - 1) / KB;           // chunks per tile
+    const int G = ntiles < SKF_WAVES ? max(1, min(nb, SKF_WAVES / ntiles)) : 1;
+    const int units = ntiles * G;
+    const int bpg = (nb + G - 1) / G;               // chunks per unit
+    const int my_units = wave < units ? (units - 1 - wave) / SKF_WAVES + 1 : 0;
+    const int nchunks = my_units * bpg;
+    // chunk c of this wave: unit u = wave + 16 (c / bpg), its batch b = g bpg + c % bpg
+    auto load = [&](int c, double (&bw)[KB]) {
+        const int u = wave + SKF_WAVES * (c / bpg);
+        const int tile = u / G, b = (u - tile * G) * bpg + c % bpg;
+        const int col = tile * 16 + lr;   // output column of this lane
 #pragma unroll
-            for (int u = 0; u < SKF_KB; ++u) {
-                const int k = 4 * (s0 + u) + lg;
-                const bool ok = n < N && k < K;
-                bw[u] = ok ? W[(size_t)n * K + k] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < SKF_KB; ++u)
-                if (s0 + u < steps) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(in[lr * ld_i + 4 * (s0 + u) + lg], bw[u], acc, 0, 0, 0);
+        for (int i = 0; i < KB; ++i) {
+            const int kk = 4 * (b * KB + i) + lg;   // contraction index of this lane
+            const bool ok = FWD ? (col < N && kk < K) : (col < K && kk < N);
+            // out of range: read a zero from `zero` instead of selecting 0 after the load (a
+            // select would wait for the load right here, prefetch included)
+            const double* q = ok ? W + (FWD ? (size_t)col * K + kk : (size_t)kk * K + col) : zero;
+            bw[i] = *q;
         }
-        // D reg j of lane l = D[(l >> 4) + 4j][l & 15]
-        const double bv = n < N ? bias[n] : 0.0;
+    };
+    auto mult = [&](int c, const double (&bw)[KB], skf_f64x4& acc) {
+        const int u = wave + SKF_WAVES * (c / bpg);
+        const int tile = u / G, b = (u - tile * G) * bpg + c % bpg;
+        double av[KB];   // every activation operand read from LDS before the first MFMA
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            double v = acc[j] + bv;
-            if (relu) v = v > 0.0 ? v : 0.0;
-            out[(lg + 4 * j) * ld_o + n] = n < N ? v : 0.0;
+        for (int i = 0; i < KB; ++i) {
+            const int st = b * KB + i;
+            const int col = st < steps ? 4 * st + lg : lg;   // past the end: any finite column, times 0
+            av[i] = src[lr * ld_s + col];
+        }
+        // keep the reads ahead of the MFMAs (the scheduler otherwise sinks each read next to its
+        // MFMA and exposes the LDS latency per step)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < KB; ++i) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bw[i], acc, 0, 0, 0);
+    };
+    // D reg j of lane l = D[(l >> 4) + 4j][l & 15]
+    auto epilogue = [&](int tile, const skf_f64x4& acc) {
+        const int col = tile * 16 + lr;
+        if (FWD) {
+            const double bv = col < N ? bias[col] : 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double v = acc[j] + bv;
+                if (relu) v = v > 0.0 ? v : 0.0;
+                dst[(lg + 4 * j) * ld_d + col] = col < N ? v : 0.0;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double* p = dst + (lg + 4 * j) * ld_d + col;
+                const double m = *p;
+                *p = (col < K && m > 0.0) ? acc[j] : 0.0;
+            }
+        }
+    };
+    auto finish = [&](int c, const skf_f64x4& acc) {
+        const int u = wave + SKF_WAVES * (c / bpg);
+        if (G == 1) {
+            epilogue(u, acc);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) red[(u * 64 + lane) * 4 + j] = acc[j];
+        }
+    };
+    double b0[KB], b1[KB];
+    skf_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (nchunks > 0) load(0, b0);
+    for (int c = 0; c < nchunks; c += 2) {
+        if (c + 1 < nchunks) load(c + 1, b1);
+        mult(c, b0, acc);
+        if (c % bpg == bpg - 1) {
+            finish(c, acc);
+            acc = (skf_f64x4){0.0, 0.0, 0.0, 0.0};
+        }
+        if (c + 1 < nchunks) {
+            if (c + 2 < nchunks) load(c + 2, b0);
+            mult(c + 1, b1, acc);
+            if ((c + 1) % bpg == bpg - 1) {
+                finish(c + 1, acc);
+                acc = (skf_f64x4){0.0, 0.0, 0.0, 0.0};
+            }
+        }
+    }
+    if (G > 1) {
+        skf_lds_barrier();
+        for (int tile = wave; tile < ntiles; tile += SKF_WAVES) {
+            skf_f64x4 s = {0.0, 0.0, 0.0, 0.0};
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s[j] += red[((tile * G + g) * 64 + lane) * 4 + j];
+            epilogue(tile, s);
         }
     }
 }
 
-// Narrow output layer (N <= SKF_NARROW) on the VALU: wave w = row w, lanes split k, one
-// deterministic xor-tree sum per output.
+// chunk length by contraction depth: short products waste no MFMAs on padding
+template <bool FWD>
+__device__ __forceinline__ void skf_layer(const double* __restrict__ src, int ld_s, double* __restrict__ dst, int ld_d,
+                                          const double* __restrict__ W, const double* __restrict__ bias, int K, int N,
+                                          bool relu, double* __restrict__ red, int wave, int lane,
+                                          const double* __restrict__ zero) {
+    const int steps = FWD ? (K + 3) >> 2 : (N + 3) >> 2;
+    if (steps <= 4)
+        skf_layer_kb<FWD, 4>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero);
+    else if (steps <= 8)
+        skf_layer_kb<FWD, 8>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero);
+    else
+        skf_layer_kb<FWD, SKF_KB>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero);
+}
+
+// Narrow output layer (N <= SKF_NARROW) on the VALU, weights staged in LDS (Ws [N][K], bias at
+// Ws[N * K + c]): wave w = row w, lanes split k, one deterministic xor-tree sum per output.
 __device__ __forceinline__ void skf_fwd_narrow(const double* __restrict__ in, int ld_i, double* __restrict__ out,
-                                               int ld_o, const double* __restrict__ W, const double* __restrict__ bias,
-                                               int K, int N, int wave, int lane) {
+                                               int ld_o, const double* __restrict__ Ws, int K, int N, int wave,
+                                               int lane) {
     const int r = wave;  // SKF_WAVES == SKF_RB
     for (int c = 0; c < N; ++c) {
         double s = 0.0;
-        for (int k = lane; k < K; k += 64) s += in[r * ld_i + k] * W[(size_t)c * K + k];
+        for (int k = lane; k < K; k += 64) s += in[r * ld_i + k] * Ws[c * K + k];
         s = skf_wave_sum(s);
-        if (lane == 0) out[r * ld_o + c] = s + bias[c];
+        if (lane == 0) out[r * ld_o + c] = s + Ws[N * K + c];
     }
     if (lane < skf_np(N) && lane >= N) out[r * ld_o + lane] = 0.0;
 }
 
-// dIn[16][K] = (d[16][N] . W[N][K]) * (a[16][K] > 0), written over a (in place: the lane that
-// reads an activation for its mask is the lane that overwrites it).
-__device__ __forceinline__ void skf_bwd_mfma(const double* __restrict__ d, int ld_d, double* __restrict__ a, int ld_a,
-                                             const double* __restrict__ W, int K, int N, int wave, int lane) {
-    const int steps = (N + 3) >> 2, kt_all = (K + 15) >> 4;
-    const int lr = lane & 15, lg = lane >> 4;
-    for (int kt = wave; kt < kt_all; kt += SKF_WAVES) {
-        const int k = kt * 16 + lr;
-        skf_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int s0 = 0; s0 < steps; s0 += SKF_KB) {
-            double bw[SKF_KB];
-#pragma unroll
-            for (int u = 0; u < SKF_KB; ++u) {
-                const int n = 4 * (s0 + u) + lg;
-                const bool ok = n < N && k < K;
-                bw[u] = ok ? W[(size_t)n * K + k] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < SKF_KB; ++u)
-                if (s0 + u < steps) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(d[lr * ld_d + 4 * (s0 + u) + lg], bw[u], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            double* p = a + (lg + 4 * j) * ld_a + k;
-            const double m = *p;
-            *p = (k < K && m > 0.0) ? acc[j] : 0.0;
-        }
-    }
-}
-
-// Backward through a narrow layer (N <= SKF_NARROW): every thread owns (row, k) elements.
+// Backward through the narrow output layer (N <= SKF_NARROW; weights staged in LDS): every
+// thread owns (row, k) elements.
 __device__ __forceinline__ void skf_bwd_narrow(const double* __restrict__ d, int ld_d, double* __restrict__ a, int ld_a,
                                                const double* __restrict__ W, int K, int N) {
     const int kp = skf_np(K);
@@ -145,15 +228,28 @@ __device__ __forceinline__ void skf_bwd_narrow(const double* __restrict__ d, int
     }
 }
 
+// phase stamps (profiling, SkfArgs::dbg): thread 0 of row block (0, 0), 100 MHz clock
+#define SKF_STAMP(i)                                                                              \
+    do {                                                                                          \
+        if (a.dbg != nullptr && threadIdx.x == 0 && rb == 0 && blockIdx.y == 0)                   \
+            a.dbg[i] = __builtin_amdgcn_s_memrealtime();                                          \
+    } while (0)
+
 __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) {
     extern __shared__ double lds[];
     __shared__ int ys[SKF_RB];
     const int t = blockIdx.y;
     if (a.active[t] == 0) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r0 = blockIdx.x * SKF_RB;
+    // (the wave index in a scalar register: the layer loops' control flow stays scalar)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // (measured: placing a trial's row blocks and wgrad tiles on one XCD, so the weights its Adam
+    // wrote are L2-resident, changed nothing -- profiles/sk_step_bench_r5e.jsonl; the row pass is
+    // bound per CU, the same with 1 or 9 trials)
+    const int rb = blockIdx.x;
+    const int r0 = rb * SKF_RB;
     const int nr = min(SKF_RB, a.rows - r0);
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.step[t] += 1;  // this minibatch's Adam step t
+    SKF_STAMP(0);
+    if (rb == 0 && threadIdx.x == 0) a.step[t] += 1;  // this minibatch's Adam step t
     const double* P = a.params + (size_t)t * a.P;
     // LDS: buffer 0 = the rows' inputs, buffer l + 1 = layer l's output (then its delta); offsets
     // recomputed from the (uniform) dims instead of a dynamically indexed array (scratch)
@@ -163,6 +259,15 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
         for (int i = 0; i < l; ++i) o += ldof(i) * SKF_RB;
         return lds + o;
     };
+    double* red = bufp(a.L + 1);
+    double* wnar = red + SKF_RED_DOUBLES;
+    const bool narrow = a.dims[a.L] <= SKF_NARROW;
+    if (narrow) {
+        // the narrow output layer's weights + bias -> LDS, in flight with the gather
+        const int nw = skf_narrow_doubles(a), C = a.dims[a.L], Kl = a.dims[a.L - 1];
+        for (int e = threadIdx.x; e < nw; e += blockDim.x)
+            wnar[e] = e < C * Kl ? P[a.w_off[a.L - 1] + e] : P[a.b_off[a.L - 1] + e - C * Kl];
+    }
     // gather through the epoch permutation (sklearn: X[sample_idx[batch_slice]])
     const int F = a.dims[0], fp = skf_np(F);
     const int* perm = a.perms + (size_t)(*a.epoch_ctr) * a.n_perm + a.off + r0;
@@ -177,17 +282,19 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
         bufp(0)[r * ldof(0) + f] = v;
     }
     if (threadIdx.x < SKF_RB) ys[threadIdx.x] = threadIdx.x < nr ? a.y[perm[threadIdx.x]] : 0;
-    __syncthreads();
+    skf_lds_barrier();
+    SKF_STAMP(1);
     // forward
     for (int l = 0; l < a.L; ++l) {
         const int K = a.dims[l], N = a.dims[l + 1];
         const double* W = P + a.w_off[l];
         const double* b = P + a.b_off[l];
-        if (l == a.L - 1 && N <= SKF_NARROW)
-            skf_fwd_narrow(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), W, b, K, N, wave, lane);
+        if (l == a.L - 1 && narrow)
+            skf_fwd_narrow(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), wnar, K, N, wave, lane);
         else
-            skf_fwd_mfma(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), W, b, K, N, l + 1 < a.L, wave, lane);
-        __syncthreads();
+            skf_layer<true>(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), W, b, K, N, l + 1 < a.L, red, wave, lane, a.zero);
+        skf_lds_barrier();
+        SKF_STAMP(2 + l);
         if (l + 1 < a.L) {  // hidden activation: the next layer's wgrad operand (kernel 2)
             double* ag = a.acts + (((size_t)l * a.T + t) * a.Bmax + r0) * a.maxw;
             for (int e = threadIdx.x; e < nr * N; e += blockDim.x) {
@@ -227,7 +334,8 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
             lrow = skf_wave_sum(lrow);
             if (lane == 0) atomicAdd(&a.loss_acc[t], lrow);
         }
-        __syncthreads();
+        skf_lds_barrier();
+        SKF_STAMP(7);
         double* dg = a.deltas + (((size_t)(a.L - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
         for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
             const int r = e / C, c = e - r * C;
@@ -238,17 +346,20 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
     for (int l = a.L - 1; l >= 1; --l) {
         const int K = a.dims[l], N = a.dims[l + 1];
         const double* W = P + a.w_off[l];
-        if (N <= SKF_NARROW)
-            skf_bwd_narrow(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), W, K, N);
+        if (l == a.L - 1 && narrow)
+            skf_bwd_narrow(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), wnar, K, N);
         else
-            skf_bwd_mfma(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), W, K, N, wave, lane);
-        __syncthreads();
+            skf_layer<false>(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), W, nullptr, K, N, false, red, wave, lane, a.zero);
+        skf_lds_barrier();
+        SKF_STAMP(8 + (a.L - 1 - l));
         double* dg = a.deltas + (((size_t)(l - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
         for (int e = threadIdx.x; e < nr * K; e += blockDim.x) {
             const int r = e / K, c = e - r * K;
             dg[(size_t)r * a.maxw + c] = bufp(l)[r * ldof(l) + c];
         }
     }
+    if (a.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SKF_STAMP(12);
 }
 
 // One 16 x 16 tile of one layer's gradient [N][K + 1] (column K = bias) per workgroup; the 4
@@ -276,6 +387,23 @@ __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
     // rows of this wave
     const int rw = (((a.rows + 3) / 4) + 3) & ~3;
     const int rb = wave * rw, re = min(a.rows, rb + rw);
+    // wave 0 runs the Adam epilogue: its parameters' p, m, v are loaded now, in flight with the
+    // operand loads (D reg j of lane l = D[(l >> 4) + 4j][l & 15])
+    double* P = a.params + (size_t)t * a.P;
+    double* M = a.m + (size_t)t * a.P;
+    double* V = a.v + (size_t)t * a.P;
+    double pp[4], pm[4], pv[4];
+    size_t pidx[4];
+    bool pok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int nn = n0 + lg + 4 * j, kk = k0 + lr;
+        pok[j] = wave == 0 && nn < N && kk <= K;
+        pidx[j] = kk < K ? (size_t)a.w_off[l] + (size_t)nn * K + kk : (size_t)a.b_off[l] + nn;
+        pp[j] = pok[j] ? P[pidx[j]] : 0.0;
+        pm[j] = pok[j] ? M[pidx[j]] : 0.0;
+        pv[j] = pok[j] ? V[pidx[j]] : 0.0;
+    }
     skf_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     const int n = n0 + lr, k = k0 + lr;
     constexpr int SB = 13;  // k-steps (4 rows each) whose operands are in flight together
@@ -304,21 +432,17 @@ __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
     const double lr_t = a.lr[t] * sqrt(1.0 - pow(a.beta2, step)) / (1.0 - pow(a.beta1, step));
     const double wdec = a.alpha * a.inv_rows;
     double sq = 0.0;
-    double* P = a.params + (size_t)t * a.P;
-    double* M = a.m + (size_t)t * a.P;
-    double* V = a.v + (size_t)t * a.P;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int nn = n0 + lg + 4 * j, kk = k0 + lr;  // D reg j of lane l = D[(l >> 4) + 4j][l & 15]
-        if (nn >= N || kk > K) continue;
-        const size_t i = kk < K ? (size_t)a.w_off[l] + (size_t)nn * K + kk : (size_t)a.b_off[l] + nn;
-        double p = P[i];
+        if (!pok[j]) continue;
+        const size_t i = pidx[j];
+        double p = pp[j];
         double g = g4[j];
-        if (kk < K) {  // coefficient: L2 term, and its loss
+        if (k0 + lr < K) {  // coefficient: L2 term, and its loss
             sq += p * p;
             g += wdec * p;
         }
-        double m = M[i], v = V[i];
+        double m = pm[j], v = pv[j];
         m = a.beta1 * m + (1.0 - a.beta1) * g;
         v = a.beta2 * v + (1.0 - a.beta2) * g * g;
         p = p - lr_t * m / (sqrt(v) + a.eps);

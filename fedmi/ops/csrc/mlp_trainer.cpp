@@ -187,9 +187,32 @@ class MLPTrainerT {
                 SkfArgs a = fused_args(0, 1);
                 fused_ = skf_supported(a);
             }
+            if (fused_) {
+                TR_CHECK(hipMalloc(&zero_, 64));
+                TR_CHECK(hipMemset(zero_, 0, 64));
+            }
+            const char* st = std::getenv("FEDMI_SK_STAMPS");
+            if (fused_ && st != nullptr && st[0] == '1') {
+                TR_CHECK(hipMalloc(&dbg_, 16 * sizeof(unsigned long long)));
+                TR_CHECK(hipMemset(dbg_, 0, 16 * sizeof(unsigned long long)));
+            }
         }
     }
-    ~MLPTrainerT() { drop_graph(); }
+    ~MLPTrainerT() {
+        drop_graph();
+        if (dbg_) (void)hipFree(dbg_);
+        if (zero_) (void)hipFree(zero_);
+    }
+    // Last fused row pass's phase stamps (FEDMI_SK_STAMPS=1), microseconds since its start.
+    std::vector<double> stamps() const {
+        std::vector<double> out;
+        if (!dbg_) return out;
+        unsigned long long h[16];
+        TR_CHECK(hipDeviceSynchronize());
+        TR_CHECK(hipMemcpy(h, dbg_, sizeof(h), hipMemcpyDeviceToHost));
+        for (int i = 0; i < 16; ++i) out.push_back(h[i] ? (double)(h[i] - h[0]) / 100.0 : -1.0);
+        return out;
+    }
 
     int P() const { return P_; }
     bool fused() const { return fused_; }
@@ -285,8 +308,12 @@ class MLPTrainerT {
         a.active = active_;
         a.xg = reinterpret_cast<double*>(xb_); a.acts = reinterpret_cast<double*>(acts_);
         a.deltas = reinterpret_cast<double*>(deltas_);
+        a.dbg = dbg_;
+        a.zero = zero_;
         return a;
     }
+    unsigned long long* dbg_ = nullptr;  // FEDMI_SK_STAMPS=1: phase stamps of the fused row pass
+    double* zero_ = nullptr;             // SkfArgs::zero
     bool fused_ = false;
     T* act(int l) const { return acts_ + (size_t)l * T_ * B_ * maxw_; }
     T* delta(int l) const { return deltas_ + (size_t)l * T_ * B_ * maxw_; }
@@ -491,6 +518,7 @@ void register_trainer(py::module_& m) {
              py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
         .def("predict_logits", &MLPTrainerT<double>::predict_logits)
         .def_property_readonly("fused", &MLPTrainerT<double>::fused)
+        .def("stamps", &MLPTrainerT<double>::stamps)
         .def_property_readonly("P", &MLPTrainerT<double>::P);
     m.def("gemm", &gemm_py);
     m.def("colsum", &colsum_py);

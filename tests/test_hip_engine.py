@@ -874,3 +874,65 @@ def test_lagged_graph_captured_behind_self_evaluating_round(R, es):
         assert len(bad) == 0, (name, k, bad)
         np.testing.assert_array_equal(hl["per_rank"][:k], hc["per_rank"][:k], err_msg=name)
         np.testing.assert_array_equal(hl["loss"][:k], hc["loss"][:k], err_msg=name)
+
+
+def test_graph_cache_across_run_and_streaming():
+    """run() replays graphs of cfg.graph_rounds rounds, run_streaming (the console) shorter ones
+    for lagged engines; the engine caches instantiated graphs per round count, so alternating the
+    two APIs captures each length ONCE -- and the rounds stay bit-identical to a
+    plain run()."""
+    X, y = make_income_like(2000, seed=31)
+    flat = init_flat(DIMS, 4)
+    cfg = dict(max_rounds=260, early_stop=False, dtype="bf16", graph_rounds=16, fused_eval=False, lagged_eval=True)
+    e = HipRoundEngine(X, y, 2, EngineConfig(**cfg), None, flat, emulate_clients=True)
+    assert e.engine.lagged
+    for _ in range(3):
+        e.run(40)
+        e.run_streaming(40, chunk=16)
+    e.sync_history()
+    assert e.engine.graph_captures == 2, e.engine.graph_captures   # one per graph length
+    ref = HipRoundEngine(X, y, 2, EngineConfig(**cfg), None, flat, emulate_clients=True)
+    ref.run(240)
+    ref.sync_history()
+    assert e.rounds_issued == ref.rounds_issued
+    np.testing.assert_array_equal(e.global_flat(), ref.global_flat())
+    np.testing.assert_array_equal(e.history()["global"], ref.history()["global"])
+
+
+# relative L2 distance of the bf16 engine's global weights from the fp32 torch oracle, one
+# client, by round: measured (profiles/bf16_drift_vs_fp32_oracle_r5.jsonl, tools/bf16_drift.py)
+# split-bf16 forward 0.0017-0.0018 / 0.0024-0.0040 / 0.0064-0.0108 / 0.0145-0.0176 at rounds
+# 1 / 5 / 20 / 60; a plain-bf16 forward 0.0045 / 0.0068 / 0.0118 / 0.024-0.0285 (exact fp32: 1e-7)
+BF16_DRIFT_TOL = {1: 3e-3, 5: 5e-3, 20: 1.5e-2, 60: 2.5e-2}
+
+
+@pytest.mark.parametrize("seed,hidden", [(3, (50, 200)), (5, (50, 200)), (7, (33, 17, 9))])
+def test_bf16_weight_drift_vs_fp32_oracle(seed, hidden):
+    """Round-by-round bound on the bf16 engine's weight drift from the fp32 torch oracle
+    (nn.Linear + autograd + Adam + StepLR) at rounds 1, 5, 20 and 60 -- tight enough that a
+    one-client engine silently training with a plain-bf16 forward instead of the split-bf16 one
+    fails it (checked below on the same data: the plain forward exceeds the round-1 bound)."""
+    X, y = make_income_like(3000, seed=seed)
+    dims = [14, *hidden, 2]
+    flat = init_flat(dims, seed)
+    base = dict(hidden=hidden, max_rounds=80, early_stop=False)
+    ref = TorchRoundEngine(X, y, 2, EngineConfig(**base), None, flat)
+    hb = HipRoundEngine(X, y, 2, EngineConfig(dtype="bf16", **base), None, flat)
+    assert not hb.layout.get("plain_fwd", False)       # one client: the split forward
+    done = 0
+    for r, tol in BF16_DRIFT_TOL.items():
+        ref.run(r - done)
+        hb.run(r - done)
+        done = r
+        w, wr = hb.global_flat(), ref.global_flat()
+        d = float(np.linalg.norm(w - wr) / np.linalg.norm(wr))
+        assert d < tol, (r, d, tol)
+        if r == 1:
+            w1_ref = wr
+    if hidden == (50, 200):
+        # negative control: the same engine with a plain-bf16 training forward drifts past round 1's bound
+        hp = HipRoundEngine(X, y, 2, EngineConfig(dtype="bf16", fused_eval=False, plain_fwd=True, **base), None, flat)
+        assert hp.layout.get("plain_fwd", False)
+        hp.run(1)
+        dp = float(np.linalg.norm(hp.global_flat() - w1_ref) / np.linalg.norm(w1_ref))
+        assert dp > BF16_DRIFT_TOL[1], dp

@@ -25,17 +25,24 @@ def run(hl, T, epochs, fused, X, y):
     dt = time.perf_counter() - t0
     steps = sum(e.n_iter_ for e in ests[:1]) * ((len(X) + 199) // 200)
     return {"hidden": list(hl), "trials": T, "epochs": int(ests[0].n_iter_), "fused": bool(ests[0]._hip_fused),
-            "wall_s": dt, "us_per_step": dt / steps * 1e6, "final_loss": float(ests[0].loss_)}
+            "wall_s": dt, "us_per_step": dt / steps * 1e6, "final_loss": float(ests[0].loss_),
+            "stamps_us": [round(x, 2) for x in getattr(ests[0], "_hip_stamps", [])][:13]}
 
 
 def main():
     from fedmi.data.tabular import load_tabular
     ds = load_tabular(with_mean=False)
     X, y = ds.X_train, ds.y_train
-    cases = [((50, 400), 1, 40), ((400, 200), 9, 10), ((50,), 9, 40)]
+    cases = [((50, 400), 1, 40), ((400, 200), 9, 10), ((50,), 9, 40), ((50, 400), 9, 20)]
+    for i, arg in enumerate(sys.argv):
+        if arg == "--case":
+            cases = [cases[int(sys.argv[i + 1])]]
+    modes = (True,) if "--fused-only" in sys.argv else (True, False)
+    if "--stamps" in sys.argv:
+        os.environ["FEDMI_SK_STAMPS"] = "1"
     for hl, T, ep in cases:
         run(hl, T, 2, True, X, y)   # warm-up (build, first graph)
-        for fused in (True, False):
+        for fused in modes:
             print(json.dumps(run(hl, T, ep, fused, X, y)), flush=True)
 
 
