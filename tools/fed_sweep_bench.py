@@ -26,12 +26,19 @@ from fedmi.models.mlp import init_flat  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=100)
+    ap.add_argument("--rows", type=int, default=8000,
+                    help="rows per trial (client shard): 8000 = one client, 1000 = the 8-client shard of config 5")
+    ap.add_argument("--grids", default="mixed-fp32,mixed-bf16,same-bf16")
     a = ap.parse_args()
-    X, y = make_income_like(8000, seed=1)
+    X, y = make_income_like(a.rows, seed=1)
+    print(f"== {a.rows} rows per trial", flush=True)
     mixed = grid(((50, 200), (100, 50), (50, 100)), (0.002, 0.004), (1, 2))
     same = grid(((50, 200),), (0.001, 0.002, 0.003, 0.004, 0.006, 0.01), (1, 2))  # one shape: one batch of 12
     R = a.rounds
-    for name, trials, dtype in (("mixed", mixed, "fp32"), ("mixed", mixed, "bf16"), ("same-shape", same, "bf16")):
+    want = set(a.grids.split(","))
+    cases = [(n, t, d) for n, t, d in (("mixed", mixed, "fp32"), ("mixed", mixed, "bf16"), ("same-shape", same, "bf16"))
+             if f"{n.split('-')[0]}-{d}" in want]
+    for name, trials, dtype in cases:
         print(f"-- {name} grid: {len(trials)} trials, shapes {sorted({t.hidden for t in trials})}", flush=True)
         base = EngineConfig(max_rounds=R + 48, early_stop=False, dtype=dtype, graph_rounds=16)
         # warm-up: compile / first launches
