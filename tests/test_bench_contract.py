@@ -72,12 +72,14 @@ def test_bench_self_launch_shared_gpu():
 @pytest.mark.timeout(600)
 def test_bench_self_launch_eight_ranks_shared_gpu():
     """--gpus 8 (a whole MI355X node's world) with every rank on cuda:0: 8 self-launched ranks,
-    the peer protocol's start-up self-test at world 8, classic rounds (the record says the lagged
-    design is off for > 2 ranks sharing a GPU), and the replica check on every rank."""
+    the peer protocol's start-up self-test at world 8, and SCALE's own N = 8 round design -- lagged
+    evaluation with FedAvg inside the Adam kernel -- on the bounded Adam grid that lets 8 ranks'
+    exchanging blocks share one GPU (peer.shared_adam_grid), and the replica check on every rank."""
     rec = _run(["--gpus", "8", "--share-gpu", "--steps", "40", "--warmup", "5", "--no-convergence",
                 "--no-anchor"], n=8, timeout=540)
-    assert rec["config"]["data_plane"].startswith("xgmi-oneshot (classic rounds"), rec["config"]
-    assert rec["config"]["round_design"] == "classic"
+    assert rec["config"]["data_plane"] == "xgmi-oneshot+adam", rec["config"]
+    assert rec["config"]["round_design"] == "lagged-eval+adam-fedavg"
+    assert rec["config"]["adam_grid"] == 16
     assert rec["replicas_consistent"] is True
     _check_headline_config(rec, 8)
 
