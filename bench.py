@@ -170,6 +170,9 @@ def main(argv=None):
                          "so the N > 1 path runs on a one-GPU box")
     ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"],
                     help="MFMA operand type of the fused kernels (fp32 accumulate, fp32 master weights)")
+    ap.add_argument("--prime-replays", type=int, default=1,
+                    help="untimed replays of the timed region's graph after its capture (warm-up; 1 / 2 / 3 "
+                         "measured the same at 20 steps, profiles/prime_replays_ab_r5.log)")
     ap.add_argument("--no-convergence", action="store_true")
     ap.add_argument("--no-anchor", action="store_true", help="skip the same-box eager torch anchor")
     ap.add_argument("--no-fp32", action="store_true", help="skip the untimed fp32-kernel round (one client)")
@@ -225,7 +228,7 @@ def main(argv=None):
     # (ranks sharing one GPU: the Adam kernels' in-kernel chunk exchange needs every rank's
     # exchanging blocks resident at once; make_peer_allreduce bounds the grid for that --
     # fedmi.parallel.peer.shared_adam_grid -- so the N > 1 round design is the same as on N GPUs)
-    max_rounds = a.warmup + a.steps + g + 16
+    max_rounds = a.warmup + a.steps + max(1, a.prime_replays) * g + 16
     # the early-stop rule runs in every round; a patience above the run's length keeps every
     # timed round live (a stop would turn the remaining rounds into no-ops)
     patience = a.patience if a.patience > 0 else max_rounds + 1
@@ -251,7 +254,7 @@ def main(argv=None):
         # warm-up: the requested rounds, then (uncounted) the graph of the timed region is
         # captured, instantiated and replayed once, so the timed steps are steady-state replays
         eng.run(a.warmup, check_every=max(a.warmup, 1))
-        primed = eng.prime_graph(g)
+        primed = eng.prime_graph(g, replays=a.prime_replays)
         eng.stream.synchronize()
         barrier()
         torch.cuda.synchronize(dev)

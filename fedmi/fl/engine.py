@@ -810,11 +810,13 @@ class HipRoundEngine(RoundEngineBase):
             self.engine.capture(g, self._stream(), self._native_comm)
             self._graph_ready = True
 
-    def prime_graph(self, g: int) -> int:
+    def prime_graph(self, g: int, replays: int = 1) -> int:
         """Bring the engine to the steady state of a ``g``-round graph before a timed region:
         issue (uncounted by the caller) eager rounds until the next round is even and may start
-        a graph, capture + instantiate the graph and replay it once.  Afterwards
-        ``_issue(k * g, close=False)`` is ``k`` graph replays.  Returns the rounds issued."""
+        a graph, capture + instantiate the graph and replay it ``replays`` times (the second launch
+        of a freshly instantiated graph runs ~0.6 us per round slower than later ones,
+        profiles/short_region_r4*.log).  Afterwards ``_issue(k * g, close=False)`` is ``k`` graph
+        replays.  Returns the rounds issued."""
         if g < 2 or g % 2:
             raise ValueError("graph rounds must be an even number >= 2")
         if self.world > 1 and not self._engine_reduces():
@@ -830,8 +832,9 @@ class HipRoundEngine(RoundEngineBase):
         else:
             raise RuntimeError("prime_graph: engine did not reach a graph-capturable state")
         self._ensure_graph(g)
-        self.engine.replay(s)
-        self.rounds_issued += g
+        for _ in range(max(1, int(replays))):
+            self.engine.replay(s)
+            self.rounds_issued += g
         return self.rounds_issued - r0
 
     def _read_state(self, idx: int) -> np.ndarray:

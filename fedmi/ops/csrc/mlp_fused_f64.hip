@@ -470,12 +470,15 @@ bool skf_supported(const SkfArgs& a) {
 hipError_t skf_step_launch(const SkfArgs& a, hipStream_t s) {
     if (!skf_supported(a) || a.rows < 1 || a.rows > a.Bmax) return hipErrorInvalidValue;
     const size_t lds = skf_lds_bytes(a);
-    static size_t lds_set = 0;
-    if (lds > 64 * 1024 && lds > lds_set) {
+    // the dynamic-LDS limit is a per-device attribute of the kernel: raised once per device
+    static size_t lds_set[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (lds > 64 * 1024 && lds > lds_set[dev]) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(skf_rowpass_kernel),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        lds_set = lds;
+        lds_set[dev] = lds;
     }
     hipLaunchKernelGGL(skf_rowpass_kernel, dim3((a.rows + SKF_RB - 1) / SKF_RB, a.T), dim3(SKF_WAVES * 64), lds, s, a);
     hipError_t e = hipGetLastError();
