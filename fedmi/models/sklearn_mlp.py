@@ -27,6 +27,7 @@ sklearn to ~1e-12).  ``warm_start=True`` fixes the reference's limitation: a ``f
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -286,6 +287,16 @@ def _pack(coefs, inters, dtype=np.float32) -> np.ndarray:
     return np.concatenate(parts)
 
 
+def _pack_t(coefs, inters) -> np.ndarray:
+    """float64 flat layout of _pack with each layer's weights TRANSPOSED -- sklearn's own [in, out]
+    = [K][N] -- at the same offsets (biases unused)."""
+    parts = []
+    for W, b in zip(coefs, inters):
+        parts.append(np.asarray(W, dtype=np.float64).reshape(-1))
+        parts.append(np.zeros(np.asarray(b).size, np.float64))
+    return np.concatenate(parts)
+
+
 def _unpack(flat, dims):
     coefs, inters, off = [], [], 0
     for K, N in zip(dims[:-1], dims[1:]):
@@ -350,6 +361,11 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
            "alpha": float(e0.alpha), "weight_decay": 0.0, "mu": 0.0, "tol": float(e0.tol),
            "n_iter_no_change": int(e0.n_iter_no_change), "max_iter": max_iter,
            "tol_stop": 0 if incremental else 1, "maxw": maxw}
+    if f64 and os.environ.get("FEDMI_SK_WT", "1") != "0":
+        # each layer's weights also transposed ([K][N]): the fused step's forward reads whole cache
+        # lines of them (mlp_fused_f64.hip SkfArgs::wt); its Adam epilogue keeps them current
+        wt = np.stack([_pack_t(e.coefs_, e.intercepts_) for e in ests])
+        bufs_t["wt"] = torch.as_tensor(wt, device=dev).contiguous()
     trainer = m.MLPTrainer64 if f64 else m.MLPTrainer
     tr = trainer(list(dims), T, cfg, {k: v.data_ptr() for k, v in bufs_t.items()})
     for e in ests:

@@ -71,6 +71,8 @@ struct SkfArgs {
     double* deltas;                         // [L][T][Bmax][maxw]
     unsigned long long* dbg;                // optional: s_memrealtime phase stamps of row block (0, 0)
     const double* zero;                     // one 0.0 in device memory (branch-free masked loads)
+    double* wt;                             // optional [T][P]: each layer's weights transposed [K][N] (kept by
+                                            // the Adam epilogue; read by the forward), nullptr: none
 };
 bool skf_supported(const SkfArgs& a);
 size_t skf_lds_bytes(const SkfArgs& a);

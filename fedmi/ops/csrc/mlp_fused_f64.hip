@@ -83,8 +83,10 @@ template <bool FWD, int KB>
 __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int ld_s, double* __restrict__ dst,
                                              int ld_d, const double* __restrict__ W, const double* __restrict__ bias,
                                              int K, int N, bool relu, double* __restrict__ red, int wave, int lane,
-                                             const double* __restrict__ zero) {
+                                             const double* __restrict__ zero, const double* __restrict__ WT,
+                                             unsigned long long* dbg = nullptr) {
     const int lr = lane & 15, lg = lane >> 4;
+    if (dbg != nullptr && threadIdx.x == 0) dbg[0] = __builtin_amdgcn_s_memrealtime();
     const int ntiles = FWD ? (N + 15) >> 4 : (K + 15) >> 4;
     const int steps = FWD ? (K + 3) >> 2 : (N + 3) >> 2;
     const int nb = (steps + KB - 1) / KB;           // chunks per tile
@@ -104,7 +106,11 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
             const bool ok = FWD ? (col < N && kk < K) : (col < K && kk < N);
             // out of range: read a zero from `zero` instead of selecting 0 after the load (a
             // select would wait for the load right here, prefetch included)
-            const double* q = ok ? W + (FWD ? (size_t)col * K + kk : (size_t)kk * K + col) : zero;
+            // FWD reads the transposed copy WT [K][N] when there is one (SkfArgs::wt): 16 consecutive
+            // output columns per k-row -- whole cache lines -- instead of 16 rows x 32 bytes
+            const double* q = ok ? (FWD ? (WT != nullptr ? WT + (size_t)kk * N + col : W + (size_t)col * K + kk)
+                                        : W + (size_t)kk * K + col)
+                                 : zero;
             bw[i] = *q;
         }
     };
@@ -159,6 +165,10 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
     for (int c = 0; c < nchunks; c += 2) {
         if (c + 1 < nchunks) load(c + 1, b1);
         mult(c, b0, acc);
+        if (dbg != nullptr && threadIdx.x == 0 && c == 0) {
+            asm volatile("s_nop 0" ::"v"(acc[0]));   // after the first chunk's MFMAs issued
+            dbg[1] = __builtin_amdgcn_s_memrealtime();
+        }
         if (c % bpg == bpg - 1) {
             finish(c, acc);
             acc = (skf_f64x4){0.0, 0.0, 0.0, 0.0};
@@ -172,6 +182,7 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
             }
         }
     }
+    if (dbg != nullptr && threadIdx.x == 0) dbg[2] = __builtin_amdgcn_s_memrealtime();
     if (G > 1) {
         skf_lds_barrier();
         for (int tile = wave; tile < ntiles; tile += SKF_WAVES) {
@@ -189,14 +200,15 @@ template <bool FWD>
 __device__ __forceinline__ void skf_layer(const double* __restrict__ src, int ld_s, double* __restrict__ dst, int ld_d,
                                           const double* __restrict__ W, const double* __restrict__ bias, int K, int N,
                                           bool relu, double* __restrict__ red, int wave, int lane,
-                                          const double* __restrict__ zero) {
+                                          const double* __restrict__ zero, const double* __restrict__ WT,
+                                          unsigned long long* dbg = nullptr) {
     const int steps = FWD ? (K + 3) >> 2 : (N + 3) >> 2;
     if (steps <= 4)
-        skf_layer_kb<FWD, 4>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero);
+        skf_layer_kb<FWD, 4>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg);
     else if (steps <= 8)
-        skf_layer_kb<FWD, 8>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero);
+        skf_layer_kb<FWD, 8>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg);
     else
-        skf_layer_kb<FWD, SKF_KB>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero);
+        skf_layer_kb<FWD, SKF_KB>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg);
 }
 
 // Narrow output layer (N <= SKF_NARROW) on the VALU, weights staged in LDS (Ws [N][K], bias at
@@ -292,7 +304,9 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
         if (l == a.L - 1 && narrow)
             skf_fwd_narrow(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), wnar, K, N, wave, lane);
         else
-            skf_layer<true>(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), W, b, K, N, l + 1 < a.L, red, wave, lane, a.zero);
+            skf_layer<true>(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), W, b, K, N, l + 1 < a.L, red, wave, lane, a.zero,
+                            a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[l] : nullptr,
+                            (a.dbg != nullptr && l == 1 && rb == 0 && t == 0) ? a.dbg + 13 : nullptr);
         skf_lds_barrier();
         SKF_STAMP(2 + l);
         if (l + 1 < a.L) {  // hidden activation: the next layer's wgrad operand (kernel 2)
@@ -349,7 +363,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
         if (l == a.L - 1 && narrow)
             skf_bwd_narrow(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), wnar, K, N);
         else
-            skf_layer<false>(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), W, nullptr, K, N, false, red, wave, lane, a.zero);
+            skf_layer<false>(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), W, nullptr, K, N, false, red, wave, lane, a.zero, nullptr);
         skf_lds_barrier();
         SKF_STAMP(8 + (a.L - 1 - l));
         double* dg = a.deltas + (((size_t)(l - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
@@ -449,6 +463,8 @@ __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
         M[i] = m;
         V[i] = v;
         P[i] = p;
+        if (a.wt != nullptr && k0 + lr < K)  // the transposed copy the forward reads
+            a.wt[(size_t)t * a.P + a.w_off[l] + (size_t)(k0 + lr) * N + (n0 + lg + 4 * j)] = p;
     }
     sq = skf_wave_sum(sq);
     if (lane == 0 && a.l2_coef != 0.0) atomicAdd(&a.loss_acc[t], a.l2_coef * sq);

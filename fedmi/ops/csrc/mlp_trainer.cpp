@@ -187,6 +187,7 @@ class MLPTrainerT {
                 SkfArgs a = fused_args(0, 1);
                 fused_ = skf_supported(a);
             }
+            if (fused_ && bufs.contains("wt")) wt_ = ptr_of<double>(bufs, "wt");
             if (fused_) {
                 TR_CHECK(hipMalloc(&zero_, 64));
                 TR_CHECK(hipMemset(zero_, 0, 64));
@@ -310,10 +311,12 @@ class MLPTrainerT {
         a.deltas = reinterpret_cast<double*>(deltas_);
         a.dbg = dbg_;
         a.zero = zero_;
+        a.wt = wt_;
         return a;
     }
     unsigned long long* dbg_ = nullptr;  // FEDMI_SK_STAMPS=1: phase stamps of the fused row pass
     double* zero_ = nullptr;             // SkfArgs::zero
+    double* wt_ = nullptr;               // SkfArgs::wt (bufs["wt"], optional)
     bool fused_ = false;
     T* act(int l) const { return acts_ + (size_t)l * T_ * B_ * maxw_; }
     T* delta(int l) const { return deltas_ + (size_t)l * T_ * B_ * maxw_; }
