@@ -161,6 +161,8 @@ struct FLConfig {
     int plain_fwd;      // bf16, several clients, register scoring: the TRAINING forward pass is plain
                         // bf16 (a_hi.W_hi) and stages only the hi images -- every scoring pass is a
                         // separate split-bf16 forward there (fl_kernels_bf16.hip)
+    int split_score;    // lagged rounds score on n_slabs workgroups of their own (train kernel LAG 3)
+                        // instead of on waves of the training workgroups (LAG 2): small shards
     int local_steps;    // optimizer steps per round (reference: 1 full-batch step, C:63-73)
     // optimizer (torch.optim.Adam + StepLR, C:44-46); scalars kept in double like torch
     double lr0;

@@ -290,6 +290,19 @@ class FLEngine {
             const bool want = req < 0 ? (c_.world > 1 || emulate) : req > 0;
             c_.plain_fwd = (valid && want && !(pf != nullptr && pf[0] == '0')) ? 1 : 0;
         }
+        // split scoring: with register scoring (e_.lag_reg) and a train grid that leaves at least as
+        // many CUs idle as it occupies, lagged rounds score on workgroups of their own (the shards
+        // of 4-8 clients); FEDMI_SPLIT_SCORE=0 / 1 forces it off / on (A/B)
+        {
+            int cus = 0, dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                cus = 0;
+            const char* ss = std::getenv("FEDMI_SPLIT_SCORE");
+            const bool force_on = ss != nullptr && ss[0] == '1', force_off = ss != nullptr && ss[0] == '0';
+            c_.split_score = (lag_ok_ && dtype_ == 1 && e_.lag_reg && !force_off &&
+                              (force_on || 2 * c_.n_slabs <= cus)) ? 1 : 0;
+        }
 
         b_.X = as_ptr<const float>(bufs["X"].cast<uintptr_t>());
         b_.y = as_ptr<const int>(bufs["y"].cast<uintptr_t>());
@@ -653,6 +666,7 @@ class FLEngine {
         o["eval_lds_bytes"] = dtype_ == 0 ? d_.lds_floats * 4 : ev_.lds_bytes;
         o["lag_reg"] = dtype_ == 1 && e_.lag_reg != 0;  // lagged rounds score in registers (fl_layout.h)
         o["plain_fwd"] = c_.plain_fwd != 0;              // plain-bf16 training forward (several clients)
+        o["split_score"] = c_.split_score != 0;          // lagged scoring on workgroups of its own
         o["eval_fedavg"] = peer_ != nullptr && !fused_ && eval_fedavg_fits();
         o["dtype"] = dtype_;
         o["slab_stride"] = c_.slab_stride;

@@ -867,6 +867,61 @@ __device__ void score_out(const MLPDesc& d, const MLPDescB& e, const FLConfig& c
     if (sj == 0 && g == 0 && row < c.n_rows) atomicAdd(&cm_s[ysc * C + best], 1);
 }
 
+// A workgroup of the lagged round's SCORING blocks (train kernel LAG 3, FLConfig::split_score):
+// the previous local model is scored for the rows of training block blockIdx.x - n_slabs by the
+// same FL_LAG_SPR RT register-scoring waves, with the same wave numbering, as in the LAG 2 kernel
+// -- but on a workgroup of their own, so the training blocks keep all 16 waves (their training is
+// the non-lagged round's, bit for bit) and small shards, whose train grid leaves most CUs idle,
+// score on the idle CUs.  The other waves end at once (s_barrier counts the live ones).  Counts:
+// cm_s (LDS) -> cm_out, as the lagged training block flushes them.
+// (No stamps: the debug buffer holds n_slabs blocks' rows.)
+template <int RT>
+__device__ void score_block_bf16(const MLPDesc& d, const MLPDescB& e, const FLConfig& c, const FLBuffers& b_in,
+                                 const FLState* __restrict__ st_in, float* __restrict__ cm_out, char* lds,
+                                 f32x4* lag_parts, int* lag_ready) {
+    const int wave = threadIdx.x >> 6;
+    constexpr int SW0 = FL_WAVES - FL_LAG_SPR * RT;  // first scoring wave
+    if (wave < SW0) return;
+    FLBuffers b = b_in;
+    b.dbg = nullptr;
+    const int t = (int)threadIdx.x - SW0 * 64;
+    constexpr int NS = FL_LAG_SPR * RT * 64;      // scoring threads
+    const int R = RT * 16, row0 = ((int)blockIdx.x - c.n_slabs) * R;
+    const int C = d.dim[d.L];
+    int* cm_s = reinterpret_cast<int*>(lds + e.cm_off);
+    if (t < RT) lag_ready[t] = 0;
+    for (int i = t; i < C * C; i += NS) cm_s[i] = 0;
+    ScorePre spre;
+    score_prefetch<RT>(d, e, b, spre);
+    const int sw = wave - SW0;
+    const int ysc = b.y[min(row0 + 16 * (sw / FL_LAG_SPR) + (int)(threadIdx.x & 15), c.n_rows - 1)];
+    // the rows as split bf16 (act_0 hi / alo_0 lo), exactly as stage_params_rows_bf16 writes them
+    {
+        const int kp = e.kp[0], lda = e.lda[0], F = d.dim[0];
+        uint16_t* a = reinterpret_cast<uint16_t*>(lds + e.act_off[0]);
+        uint16_t* alo = reinterpret_cast<uint16_t*>(lds + e.alo_off[0]);
+        for (int idx = t; idx < R * kp; idx += NS) {
+            const int r = idx / kp, k = idx - r * kp;
+            const int row = row0 + r;
+            const bool ok = row < c.n_rows && k < F;
+            const float v = ok ? b.X[(size_t)row * F + k] : 0.f;
+            a[r * lda + k] = (uint16_t)bf16_bits(v);
+            alo[r * lda + k] = (uint16_t)lo_bits(v);
+        }
+    }
+    const FLState S0 = *st_in;  // the round's tentative live decision, as the training blocks take it
+    const bool live = !S0.stopped && S0.next_round < c.max_rounds;
+    lds_barrier();
+    if (!live) return;
+    ScoreIn sin;
+    score_in_lds<RT>(d, e, b, lds, sw, spre, sin);
+    score_out<RT>(d, e, c, b, cm_s, sw, row0, ysc, sin,
+                  lag_parts + (sw / FL_LAG_SPR) * (FL_LAG_SPR - 1) * FL_LAG_PARTS * 16, lag_ready + sw / FL_LAG_SPR);
+    lds_barrier();
+    for (int i = t; i < C * C; i += NS)
+        if (cm_s[i]) atomicAdd(&cm_out[i], (float)cm_s[i]);
+}
+
 // ---------------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------------
@@ -988,20 +1043,26 @@ hipError_t fl_launch_train_bf16(const MLPDesc& d, const MLPDescB& e, const FLCon
     if ((mode == FL_EVAL_FUSED || mode == FL_EVAL_LAGGED) && cm_out == nullptr) return hipErrorInvalidValue;
     const size_t lds = (size_t)e.lds_bytes;
     const bool lag = mode == FL_EVAL_LAGGED;
-#define FLB_TRAIN(RT_, LAG_, PL_)                                                                           \
-    hipLaunchKernelGGL((fl_train_bf16_kernel<RT_, LAG_, PL_>), dim3(c.n_slabs), dim3(FL_THREADS), lds, s, d, e, c, b, pg, \
-                       si, so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask)
+    // split scoring (FLConfig::split_score): the lagged round's first local step scores on
+    // n_slabs workgroups of their own, appended to the grid (LAG 3)
     const bool lreg = lag && e.lag_reg;
+    const bool split = lreg && c.split_score && ls == 0;
+    const int grid = split ? 2 * c.n_slabs : c.n_slabs;
+#define FLB_TRAIN(RT_, LAG_, PL_)                                                                           \
+    hipLaunchKernelGGL((fl_train_bf16_kernel<RT_, LAG_, PL_>), dim3(grid), dim3(FL_THREADS), lds, s, d, e, c, b, pg, \
+                       si, so, ls, stage_local ? 1 : 0, mode, cm_out, fold_mask)
     switch (c.R) {
         // plain_fwd (FLConfig): the training forward of several clients with register scoring (R <= 32)
         case 16:
-            if (lreg) { if (c.plain_fwd) FLB_TRAIN(1, 2, true); else FLB_TRAIN(1, 2, false); }
+            if (split) { if (c.plain_fwd) FLB_TRAIN(1, 3, true); else FLB_TRAIN(1, 3, false); }
+            else if (lreg) { if (c.plain_fwd) FLB_TRAIN(1, 2, true); else FLB_TRAIN(1, 2, false); }
             else if (lag) FLB_TRAIN(1, 1, false);
             else if (c.plain_fwd) FLB_TRAIN(1, 0, true);
             else FLB_TRAIN(1, 0, false);
             break;
         case 32:
-            if (lreg) { if (c.plain_fwd) FLB_TRAIN(2, 2, true); else FLB_TRAIN(2, 2, false); }
+            if (split) { if (c.plain_fwd) FLB_TRAIN(2, 3, true); else FLB_TRAIN(2, 3, false); }
+            else if (lreg) { if (c.plain_fwd) FLB_TRAIN(2, 2, true); else FLB_TRAIN(2, 2, false); }
             else if (lag) FLB_TRAIN(2, 1, false);
             else if (c.plain_fwd) FLB_TRAIN(2, 0, true);
             else FLB_TRAIN(2, 0, false);
@@ -1140,6 +1201,8 @@ hipError_t fl_set_lds_limit_bf16(size_t bytes) {
     FLB_SET((fl_train_bf16_kernel<1, 2, false>)); FLB_SET((fl_train_bf16_kernel<2, 2, false>));
     FLB_SET((fl_train_bf16_kernel<1, 2, true>)); FLB_SET((fl_train_bf16_kernel<2, 2, true>));
     FLB_SET((fl_train_bf16_kernel<1, 0, true>)); FLB_SET((fl_train_bf16_kernel<2, 0, true>));
+    FLB_SET((fl_train_bf16_kernel<1, 3, false>)); FLB_SET((fl_train_bf16_kernel<2, 3, false>));
+    FLB_SET((fl_train_bf16_kernel<1, 3, true>)); FLB_SET((fl_train_bf16_kernel<2, 3, true>));
     FLB_SET(fl_eval_bf16_kernel<1>); FLB_SET(fl_eval_bf16_kernel<2>); FLB_SET(fl_eval_bf16_kernel<4>);
     FLB_SET((fl_train_bf16_batch_kernel<1, false>)); FLB_SET((fl_train_bf16_batch_kernel<2, false>));
     FLB_SET((fl_train_bf16_batch_kernel<4, false>)); FLB_SET((fl_train_bf16_batch_kernel<1, true>));

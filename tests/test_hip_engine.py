@@ -767,12 +767,18 @@ def test_lagged_register_scoring_equals_serial_pass(hidden, C, R, monkeypatch):
     flat = init_flat([14, *hidden, C], 8)
     eligible = C <= 4
     out = {}
-    for env in (None, "0"):
+    # FEDMI_SPLIT_SCORE: register scoring on workgroups of its own (train kernel LAG 3; the
+    # default where 2 n_slabs <= #CUs -- forced here) or on the training workgroups' idle waves (LAG 2)
+    for env, split in ((None, "1"), (None, "0"), ("0", None)):
         for lagged in (True, False):
             if env is None:
                 monkeypatch.delenv("FEDMI_LAG_REG", raising=False)
             else:
                 monkeypatch.setenv("FEDMI_LAG_REG", env)
+            if split is None:
+                monkeypatch.delenv("FEDMI_SPLIT_SCORE", raising=False)
+            else:
+                monkeypatch.setenv("FEDMI_SPLIT_SCORE", split)
             cfg = EngineConfig(hidden=tuple(hidden), max_rounds=40, early_stop=False, dtype="bf16", graph_rounds=4,
                                rows_per_block=R, fused_eval=False, lagged_eval=lagged)
             e = HipRoundEngine(X, y, C, cfg, None, flat, emulate_clients=True)
@@ -780,21 +786,22 @@ def test_lagged_register_scoring_equals_serial_pass(hidden, C, R, monkeypatch):
             lay = e.engine.layout()
             assert lay["lag_reg"] == (env is None and eligible)
             assert lay["plain_fwd"] == (env is None and eligible)
+            assert lay["split_score"] == (lagged and env is None and eligible and split == "1")
             e.run(3)
             e.run(9)
             e.sync_history()
             h = e.history()
             assert h["rounds_run"] == 12
-            out[(env, lagged)] = (e.global_flat(), h)
-    for env in (None, "0"):
-        (wl, hl), (wc, hc) = out[(env, True)], out[(env, False)]
-        name = f"FEDMI_LAG_REG={env}"
+            out[(env, split, lagged)] = (e.global_flat(), h)
+    for env, split in ((None, "1"), (None, "0"), ("0", None)):
+        (wl, hl), (wc, hc) = out[(env, split, True)], out[(env, split, False)]
+        name = f"FEDMI_LAG_REG={env} FEDMI_SPLIT_SCORE={split}"
         np.testing.assert_array_equal(wl, wc, err_msg=name)
         np.testing.assert_array_equal(hl["global"], hc["global"], err_msg=name)
         np.testing.assert_array_equal(hl["per_rank"], hc["per_rank"], err_msg=name)
         np.testing.assert_array_equal(hl["loss"], hc["loss"], err_msg=name)
     if eligible:  # the plain training forward changes the trajectory, not its quality
-        a, b = out[(None, True)][1]["global"][-1], out[("0", True)][1]["global"][-1]
+        a, b = out[(None, "1", True)][1]["global"][-1], out[("0", None, True)][1]["global"][-1]
         assert abs(a[0] - b[0]) < 0.02, (a, b)
 
 
