@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "gemm_nt_bf16.h"
 #include "gemm_mfma.h"
@@ -44,6 +45,17 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // wave-uniform base + lane * 16, so the swizzle lives in the per-lane GLOBAL address.
 __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
     __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_base, 16, 0, 0);
+}
+
+// The same DMA through a buffer resource (buffer_load_dwordx4 ... lds, the form hipBLASLt's
+// MT256x256x64 kernels use): base in SGPRs, a lane VGPR offset shared by every piece of the same
+// swizzle parity, the piece / K-tile offset in an SGPR (soffset).  Bounds: the whole 32-bit range
+// from the block's base (the operands' extents are checked on the host).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t nt_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* lds_base) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_base, 16, voff, soff, 0, 0);
 }
 
 // DB = 0: one LDS buffer (32 KiB), two barriers per K-step, ~3 blocks/CU hide the DMA.
@@ -211,10 +223,15 @@ static inline int nt_epi_flags(const NTArgs& g) {
            (g.C != nullptr && g.beta != 0.f ? NT_EPI_BETA : 0) | (g.csum != nullptr ? NT_EPI_CSUM : 0);
 }
 
-template <int F>
-__device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (&acc)[8][4], int m0, int n0, int w,
-                                            int l) {
-    const int wr = w >> 2, wc = w & 3;
+// NW = 8 waves as 2 x 4 (128 x 64 outputs per wave, acc[8][4]; variants 2 / 3) or NW = 4 waves as
+// 2 x 2 (128 x 128, acc[8][8]: the four-wave loops measured in rounds 3 and 5,
+// profiles/nt_four_wave_r3_rejected.log, profiles/nt_ring_bufdma_r5.log).
+template <int F, int NW = 8>
+__device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (&acc)[8][32 / NW], int m0, int n0,
+                                            int w, int l) {
+    constexpr int YT = 32 / NW, WN = 16 * YT;  // 16-column tiles per wave, columns per wave
+    constexpr int RI = 256 / (2 * NW);          // row-pair iterations of the block-wide loops
+    const int wr = w / (NW / 2), wc = w % (NW / 2);
     const int lr = l & 15, lg = l >> 4;
     const bool hC = F < 0 ? g.C != nullptr : (F & NT_EPI_C) != 0;
     const bool hCb = F < 0 ? g.Cbf16 != nullptr : (F & NT_EPI_CB) != 0;
@@ -240,8 +257,8 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     if (hMask) {
         const __hip_bfloat16* Mk = reinterpret_cast<const __hip_bfloat16*>(g.mask);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int row = i * 16 + w * 2, rr = row + (l >> 5);
+        for (int i = 0; i < RI; ++i) {
+            const int row = i * 2 * NW + w * 2, rr = row + (l >> 5);
             glds16(Mk + (size_t)(m0 + rr) * g.ldmask + n0 + (((l & 31) ^ sw(rr)) << 3), smem + row * 512);
         }
         vm_wait<0>();
@@ -249,8 +266,8 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     }
 
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
-        const int cl = wc * 64 + 16 * y + lr, n = n0 + cl;
+    for (int y = 0; y < YT; ++y) {
+        const int cl = wc * WN + 16 * y + lr, n = n0 + cl;
         const float bv = hBias ? g.bias[n] : 0.f;
         float cs = 0.f;  // column n's sum over the lane's 32 rows of the bf16 output (hCsum)
 #pragma unroll
@@ -290,8 +307,8 @@ __device__ __forceinline__ void pp_epilogue(const NTArgs& g, char* smem, f32x4 (
     if (hCb) {
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int rr = i * 16 + w * 2 + (l >> 5), p = l & 31;
+        for (int i = 0; i < RI; ++i) {
+            const int rr = i * 2 * NW + w * 2 + (l >> 5), p = l & 31;
             const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * 512 + p * 16);
             *reinterpret_cast<uint4*>(Cb + (size_t)(m0 + rr) * g.ldcb + n0 + ((p ^ sw(rr)) << 3)) = d;
         }
@@ -446,7 +463,7 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
 // read.  Waits (before a phase's first barrier, retiring what the NEXT phase reads; pieces still
 // allowed in flight, in issue order): r = 0: 4 (B01, B23 of u+1) | r = 3: 4 (A m1 of u+1, B01 of
 // u+2) | r = 1, 2: none.
-template <int F>
+template <int F, bool BUF = false>
 __global__ void __launch_bounds__(NT2_THREADS)
 gemm_nt_bf16_fl_kernel(NTArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
@@ -483,12 +500,22 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
     const char* sbA0 = reinterpret_cast<const char*>(A + (size_t)(m0 + rm0) * g.lda);
     const char* sbA1 = reinterpret_cast<const char*>(A + (size_t)(m0 + rm0 + 64) * g.lda);
     const size_t rowB8 = (size_t)8 * g.ldb * 2, rowA8 = (size_t)8 * g.lda * 2;
+    // BUF (the default; variant 10 = without): the pieces through buffer resources (blds16), offsets in SGPRs
+    const __amdgpu_buffer_rsrc_t rsB = nt_rsrc(sbB), rsA = nt_rsrc(sbA0);
+    const uint32_t rowA64 = (uint32_t)(64 * g.lda * 2);
     auto dmaB = [&](int tile, int i) {
-        glds16(sbB + i * rowB8 + tile * 128 + voB[i & 1], smem + (tile & 1) * 65536 + 32768 + (32 * w + 8 * i) * 128);
+        char* dst = smem + (tile & 1) * 65536 + 32768 + (32 * w + 8 * i) * 128;
+        if (BUF) blds16(rsB, voB[i & 1], (uint32_t)(i * rowB8) + tile * 128, dst);
+        else glds16(sbB + i * rowB8 + tile * 128 + voB[i & 1], dst);
     };
     auto dmaA = [&](int tile, int half, int i) {
-        const char* src = (half ? sbA1 : sbA0) + i * rowA8 + tile * 128 + voA[i & 1];
-        glds16(src, smem + (tile & 1) * 65536 + (rm0 + 64 * half + 8 * i) * 128);
+        char* dst = smem + (tile & 1) * 65536 + (rm0 + 64 * half + 8 * i) * 128;
+        if (BUF) {
+            blds16(rsA, voA[i & 1], half * rowA64 + (uint32_t)(i * rowA8) + tile * 128, dst);
+        } else {
+            const char* src = (half ? sbA1 : sbA0) + i * rowA8 + tile * 128 + voA[i & 1];
+            glds16(src, dst);
+        }
     };
 
     // fragment reads: row (16-row group base) + lr, chunk 4 ks + lg swizzled by (lr >> 1) & 7
@@ -591,7 +618,14 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
 #undef NT_STAMP
 }
 
-static int g_nt_variant = 3;  // 3: full-line 256x256 loop (default), 2: half-line, 1/0: 128x128
+// 3: full-line 256x256 loop (default; buffer-resource LDS-DMAs), 10: the same loop with
+// global_load_lds DMAs (rounds 2-4), 2: half-line, 1/0: 128x128.  FEDMI_NT_VARIANT overrides the
+// default (A/B runs of whole workloads).
+static int nt_default_variant() {
+    const char* v = std::getenv("FEDMI_NT_VARIANT");
+    return v != nullptr && v[0] != '\0' ? std::atoi(v) : 3;
+}
+static int g_nt_variant = nt_default_variant();
 void gemm_nt_set_variant(int v) { g_nt_variant = v; }
 static unsigned long long* g_nt_dbg = nullptr;
 void gemm_nt_set_debug(unsigned long long* dbg) { g_nt_dbg = dbg; }
@@ -608,15 +642,18 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
         hipLaunchKernelGGL(gemm_nt_bf16_pp_kernel, dim3(blocks), dim3(NT2_THREADS), 0, s, g);
         return hipGetLastError();
     }
-    if (g_nt_variant == 3 && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
+    if ((g_nt_variant == 3 || g_nt_variant == 10) && g.M % NT2_BM == 0 && g.N % NT2_BM == 0 &&
         (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&
         (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
         (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
         // the output configurations of the wide client's GEMMs get their own instantiation
         switch (nt_epi_flags(g)) {
-#define NT_FL_CASE(F) \
-    case F: hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel<F>, dim3(blocks), dim3(NT2_THREADS), 0, s, g); break;
+#define NT_FL_CASE(F)                                                                                      \
+    case F:                                                                                                \
+        if (g_nt_variant == 10) hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<F, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g); \
+        else hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<F, true>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);    \
+        break;
             NT_FL_CASE(NT_EPI_CB)                                                  // plain bf16 output
             NT_FL_CASE(NT_EPI_CB | NT_EPI_CBT | NT_EPI_BIAS | NT_EPI_RELU)         // hidden-layer forward
             NT_FL_CASE(NT_EPI_CB | NT_EPI_BIAS | NT_EPI_RELU)                      // forward, no transposed copy
@@ -627,7 +664,10 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
             NT_FL_CASE(NT_EPI_C | NT_EPI_BETA)                                     // accumulating wgrad
             NT_FL_CASE(NT_EPI_C | NT_EPI_BIAS)                                     // fp32 logits
 #undef NT_FL_CASE
-            default: hipLaunchKernelGGL(gemm_nt_bf16_fl_kernel<-1>, dim3(blocks), dim3(NT2_THREADS), 0, s, g); break;
+            default:
+                if (g_nt_variant == 10) hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<-1, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);
+                else hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<-1, true>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);
+                break;
         }
         return hipGetLastError();
     }

@@ -286,9 +286,10 @@ def test_skinny_wgrad_bf16(C, trans, rows, splits):
                                        (2048, 1024, 4096, 8)])
 def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     """The 256x256 ping-pong main loops (variant 2: half-line DMA pieces, variant 3: whole-line
-    pieces and 128-byte LDS rows) against the 128x128 loop (variant 1): same per-element k
-    order, so bit-identical, and against an fp32 torch reference; row strides wider than K
-    exercise the DMA source addressing."""
+    pieces and 128-byte LDS rows, with buffer-resource DMAs; variant 10: the same with
+    global_load_lds DMAs) against the 128x128 loop (variant 1): same per-element k order, so
+    bit-identical, and against an fp32 torch reference; row strides wider than K exercise the
+    DMA source addressing."""
     m = native()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
@@ -298,7 +299,7 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     bias = torch.randn(N, device=dev)
     outs = []
     try:
-        for v in (1, 2, 3):
+        for v in (1, 2, 3, 10):
             m.gemm_nt_set_variant(v)
             Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             CbT = torch.empty(N, M, dtype=torch.bfloat16, device=dev)
@@ -314,7 +315,7 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
     mask = torch.randn(M, N + 8, device=dev).to(torch.bfloat16)
     mouts = []
     try:
-        for v in (1, 2, 3):
+        for v in (1, 2, 3, 10):
             m.gemm_nt_set_variant(v)
             Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             m.gemm_nt(M, N, K, A.data_ptr(), K + pad, B.data_ptr(), K + pad, 0, 0, Cb.data_ptr(), N, 0, 0, 0,
@@ -323,11 +324,11 @@ def test_gemm_nt_bf16_pingpong_matches_128_tile(M, N, K, pad):
             mouts.append(Cb)
     finally:
         m.gemm_nt_set_variant(3)
-    assert torch.equal(mouts[0], mouts[1]) and torch.equal(mouts[0], mouts[2])
+    assert all(torch.equal(mouts[0], o) for o in mouts[1:])
     mref = torch.where(mask[:, :N].float() > 0, A[:, :K].float() @ B[:, :K].float().t(), torch.zeros(M, N, device=dev))
     assert ((mouts[1].float() - mref).abs().max() / mref.abs().max()).item() < 1e-2
     ref = (A[:, :K].float() @ B[:, :K].float().t() + bias).clamp_min(0)
-    for v in (1, 2):
+    for v in range(1, len(outs)):
         assert torch.equal(outs[0][0], outs[v][0])
         assert torch.equal(outs[0][1], outs[v][1])
     assert ((outs[1][0] - ref).abs().max() / ref.abs().max()).item() < 1e-5
@@ -350,7 +351,7 @@ def test_gemm_nt_bf16_epilogue_configs(cfg):
     C0 = torch.randn(M, N, device=dev)
     outs = []
     try:
-        for v in (1, 3):
+        for v in (1, 3, 10):
             m.gemm_nt_set_variant(v)
             C = C0.clone()
             Cb = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
@@ -364,8 +365,9 @@ def test_gemm_nt_bf16_epilogue_configs(cfg):
             outs.append((C, Cb, CbT))
     finally:
         m.gemm_nt_set_variant(3)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 def test_gemm_nt_bf16_dgrad_column_sums():
@@ -399,6 +401,14 @@ def test_gemm_nt_bf16_dgrad_column_sums():
     torch.cuda.synchronize()
     assert ((gb - ref.sum(0)).abs().max() / ref.sum(0).abs().max()).item() < 1e-5
     try:
+        # the global_load_lds form of the full-line loop (variant 10): the same sums, bit for bit
+        m.gemm_nt_set_variant(10)
+        Cb9 = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        cs9 = torch.full((M // 128, N), float("nan"), device=dev)
+        m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, Cb9.data_ptr(), N, 0, 0, 0,
+                  mask.data_ptr(), N, 0, 1.0, 0.0, s, cs9.data_ptr(), N)
+        torch.cuda.synchronize()
+        assert torch.equal(Cb9, outs[1][0]) and torch.equal(cs9, cs)
         m.gemm_nt_set_variant(1)
         with pytest.raises(RuntimeError):
             m.gemm_nt(M, N, K, A.data_ptr(), K, B.data_ptr(), K, 0, 0, outs[0][0].data_ptr(), N, 0, 0, 0,
