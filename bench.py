@@ -292,6 +292,7 @@ def main(argv=None):
                                "lagged-eval+late-fold" if eng.engine.late_fold else
                                "lagged-eval" if eng.engine.lagged else "classic"),
               "rows_per_block": eng.R, "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
+              "split_score": bool(eng.layout.get("split_score", False)),
               "adam_grid": int(eng._peer.adam_grid) if eng._peer is not None else 0,
               "lagged_eval": eng.cfg.lagged_eval, "final_acc": float(h["global"][-1][0])}
     X, y = eng.X, eng.y
@@ -357,7 +358,7 @@ def main(argv=None):
                        "early_stop": {"enabled": bool(a.early_stop), "patience": patience, "atol": 1e-4,
                                       "rtol": 1e-5, "note": "rule evaluated on the device every timed round; "
                                       "patience longer than the run so every timed round is live"},
-                       "plain_fwd": design["plain_fwd"],
+                       "plain_fwd": design["plain_fwd"], "split_score": design["split_score"],
                        "graph_rounds": g, "share_gpu": bool(a.share_gpu)},
             "samples_per_sec_per_client": value / N,
             "us_per_round": dt / a.steps * 1e6,
