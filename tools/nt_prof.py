@@ -1,7 +1,8 @@
 """NT GEMM profiling driver: a few launches of one shape/variant (for rocprofv3 --pmc passes)."""
+import os
 import sys
 import torch
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedmi.ops import native
 
 M, N, K = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (16384, 4096, 4096)))
