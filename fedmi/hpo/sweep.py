@@ -21,7 +21,7 @@ import numpy as np
 
 from ..fl.metrics import confusion_matrix, metrics_from_confusion
 from ..fl.sklearn_fed import allreduce_confusion, average_estimator_weights
-from ..models.sklearn_mlp import MLPClassifier, fit_packed
+from ..models.sklearn_mlp import MLPClassifier, fit_packed, prepare_packed
 
 HIDDEN_GRID: Tuple[Tuple[int, ...], ...] = ((50,), (100,), (50, 50), (100, 50), (50, 100), (50, 200), (50, 400),
                                             (100, 400), (400, 200), (200, 400))
@@ -71,16 +71,16 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
     # GPU alone).  Averaging and pooled metrics then follow in the reference's trial order,
     # so every rank issues its collectives in the same sequence.
     if packed and groups and groups[0][0]._resolve_backend() == "hip" and len(groups) > 1:
-        import torch
         from concurrent.futures import ThreadPoolExecutor
-        dev = torch.cuda.current_device()
-
-        def fit_group(ests):
-            torch.cuda.set_device(dev)
-            return fit_packed(ests, X_local, y_local)
-
-        with ThreadPoolExecutor(max_workers=len(groups)) as ex:
-            list(ex.map(fit_group, groups))
+        # every job is built and its epoch graph captured HERE, one after another, before any
+        # thread starts: a capture overlapping another thread's allocations / copies / polling
+        # was invalidated (ranks sharing a GPU made the overlap likely); the threads then only
+        # replay graphs and poll, and the results are copied back here
+        jobs = [prepare_packed(ests, X_local, y_local) for ests in groups]
+        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+            list(ex.map(lambda j: j.run(), jobs))
+        for j in jobs:
+            j.finish()
     elif packed:
         for ests in groups:
             fit_packed(ests, X_local, y_local)

@@ -308,6 +308,10 @@ def _unpack(flat, dims):
 
 
 def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
+    _fit_hip_prepare(ests, X, codes, dims, perms, incremental).run().finish()
+
+
+def _fit_hip_prepare(ests: List[MLPClassifier], X, codes, dims, perms, incremental) -> "_HipJob":
     """Train T estimators of one architecture (same data, same permutations) at once."""
     import torch
     from ..ops import native
@@ -372,8 +376,35 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
         e._hip_fused = bool(tr.fused)   # two-kernel minibatch step (mlp_fused_f64.hip) ran
     stream = torch.cuda.Stream(device=dev)
     stream.wait_stream(torch.cuda.current_stream(dev))
-    tr.run(max_iter, stream.cuda_stream, 8, True)
-    stream.synchronize()
+    tr.prepare(stream.cuda_stream)      # the epoch graph, captured here (see _HipJob)
+    return _HipJob(ests, tr, stream, dev, max_iter, bufs_t, params, mom, vel, step, dims, n, T)
+
+
+class _HipJob:
+    """A packed device fit in three steps: built and graph-captured (:func:`_fit_hip_prepare`),
+    :meth:`run` (graph replays only: several jobs may run from several host threads at once),
+    :meth:`finish` (results back into the estimators).  Building and capturing from one thread
+    while no other thread issues HIP calls keeps every capture valid (the [H] sweep's threads)."""
+
+    def __init__(self, ests, tr, stream, dev, max_iter, bufs_t, params, mom, vel, step, dims, n, T):
+        self.ests, self.tr, self.stream, self.dev, self.max_iter = ests, tr, stream, dev, max_iter
+        self.bufs_t, self.params, self.mom, self.vel, self.step = bufs_t, params, mom, vel, step
+        self.dims, self.n, self.T = dims, n, T
+
+    def run(self):
+        import torch
+        torch.cuda.set_device(self.dev)
+        self.tr.run(self.max_iter, self.stream.cuda_stream, 8, True)
+        self.stream.synchronize()
+        return self
+
+    def finish(self):
+        ests, tr, bufs_t, params, dims, n, T = self.ests, self.tr, self.bufs_t, self.params, self.dims, self.n, self.T
+        mom, vel, step = self.mom, self.vel, self.step
+        _fit_hip_finish(ests, tr, bufs_t, params, mom, vel, step, dims, n, T)
+
+
+def _fit_hip_finish(ests, tr, bufs_t, params, mom, vel, step, dims, n, T):
     if hasattr(tr, "stamps"):
         for e in ests:
             e._hip_stamps = list(tr.stamps())   # FEDMI_SK_STAMPS=1 (tools/sk_step_bench.py)
@@ -398,6 +429,16 @@ def _fit_hip(ests: List[MLPClassifier], X, codes, dims, perms, incremental):
 def fit_packed(ests: List[MLPClassifier], X, y):
     """Fit several estimators that share architecture, data, random_state and batch size
     (e.g. the learning-rate axis of the [H] grid) as ONE packed device job."""
+    job = prepare_packed(ests, X, y)
+    if job is not None:
+        job.run().finish()
+    return ests
+
+
+def prepare_packed(ests: List[MLPClassifier], X, y) -> Optional["_HipJob"]:
+    """:func:`fit_packed` up to a built, graph-captured device job (None: a host backend, which
+    has fitted the estimators already).  ``job.run()`` may then run beside other jobs from other
+    host threads; ``job.finish()`` writes the results back."""
     X = np.asarray(X, dtype=np.float64)
     e0 = ests[0]
     sig = lambda e: (tuple(np.atleast_1d(e.hidden_layer_sizes)), e.random_state, e.batch_size, e.alpha,
@@ -407,7 +448,7 @@ def fit_packed(ests: List[MLPClassifier], X, y):
     if e0._resolve_backend() != "hip":
         for e in ests:
             e.fit(X, y)
-        return ests
+        return None
     rs = None
     for e in ests:
         codes = e._encode(y, True)
@@ -419,5 +460,4 @@ def fit_packed(ests: List[MLPClassifier], X, y):
         e._adam = None
     perms = epoch_permutations(rs, X.shape[0], e0.max_iter) if e0.shuffle else \
         np.tile(np.arange(X.shape[0], dtype=np.int32), (e0.max_iter, 1))
-    _fit_hip(ests, X, codes, e0._dims(X.shape[1]), perms, incremental=False)
-    return ests
+    return _fit_hip_prepare(ests, X, codes, e0._dims(X.shape[1]), perms, incremental=False)

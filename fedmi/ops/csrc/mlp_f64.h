@@ -76,4 +76,5 @@ struct SkfArgs {
 };
 bool skf_supported(const SkfArgs& a);
 size_t skf_lds_bytes(const SkfArgs& a);
+hipError_t skf_prepare(const SkfArgs& a);
 hipError_t skf_step_launch(const SkfArgs& a, hipStream_t s);

@@ -24,6 +24,7 @@
 // differ from the layered path and from BLAS, so results agree with the float64 numpy oracle
 // to ~1e-12 per step, not bitwise (tests/test_sklearn_estimator.py: loss curve rtol 1e-9).
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <math.h>
 #include <stdint.h>
 
@@ -483,18 +484,33 @@ bool skf_supported(const SkfArgs& a) {
     return true;
 }
 
+// The dynamic-LDS limit is a per-device attribute of the row-pass kernel, raised to the largest
+// size any trainer on the device needs.  Called by every fused trainer at construction -- not from
+// inside a stream capture, where the attribute call would invalidate the capture -- and guarded:
+// the [H] sweep builds and runs trainers from several host threads at once.
+hipError_t skf_prepare(const SkfArgs& a) {
+    static std::mutex mu;
+    static size_t lds_set[64] = {};
+    const size_t lds = skf_lds_bytes(a);
+    if (lds <= 64 * 1024) return hipSuccess;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(mu);
+    if (lds <= lds_set[dev]) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(skf_rowpass_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess) lds_set[dev] = lds;
+    return e;
+}
+
 hipError_t skf_step_launch(const SkfArgs& a, hipStream_t s) {
     if (!skf_supported(a) || a.rows < 1 || a.rows > a.Bmax) return hipErrorInvalidValue;
     const size_t lds = skf_lds_bytes(a);
-    // the dynamic-LDS limit is a per-device attribute of the kernel: raised once per device
-    static size_t lds_set[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    if (lds > 64 * 1024 && lds > lds_set[dev]) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(skf_rowpass_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    // normally a no-op: the trainer raised the limit when it was built (skf_prepare), outside
+    // any stream capture
+    if (lds > 64 * 1024) {
+        const hipError_t e = skf_prepare(a);
         if (e != hipSuccess) return e;
-        lds_set[dev] = lds;
     }
     hipLaunchKernelGGL(skf_rowpass_kernel, dim3((a.rows + SKF_RB - 1) / SKF_RB, a.T), dim3(SKF_WAVES * 64), lds, s, a);
     hipError_t e = hipGetLastError();

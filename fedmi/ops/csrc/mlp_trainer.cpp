@@ -188,6 +188,7 @@ class MLPTrainerT {
                 fused_ = skf_supported(a);
             }
             if (fused_ && bufs.contains("wt")) wt_ = ptr_of<double>(bufs, "wt");
+            if (fused_) TR_CHECK(skf_prepare(fused_args(0, 1)));
             if (fused_) {
                 TR_CHECK(hipMalloc(&zero_, 64));
                 TR_CHECK(hipMemset(zero_, 0, 64));
@@ -284,6 +285,13 @@ class MLPTrainerT {
             if (!any) break;
         }
         return done;
+    }
+
+    // Capture the epoch graph now (no launch): callers that run several trainers from several host
+    // threads capture them all first, from one thread, so no capture overlaps another thread's
+    // HIP calls (fedmi/hpo/sweep.py).
+    void prepare(uintptr_t stream) {
+        if (!exec_) capture(reinterpret_cast<hipStream_t>(stream));
     }
 
     // Forward pass of all trials over an arbitrary row block (evaluation / predict):
@@ -512,6 +520,7 @@ void register_trainer(py::module_& m) {
         .def(py::init<std::vector<int>, int, py::dict, py::dict>())
         .def("run", &MLPTrainerT<float>::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
              py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
+        .def("prepare", &MLPTrainerT<float>::prepare)
         .def("predict_logits", &MLPTrainerT<float>::predict_logits)
         .def_property_readonly("fused", &MLPTrainerT<float>::fused)
         .def_property_readonly("P", &MLPTrainerT<float>::P);
@@ -519,6 +528,7 @@ void register_trainer(py::module_& m) {
         .def(py::init<std::vector<int>, int, py::dict, py::dict>())
         .def("run", &MLPTrainerT<double>::run, py::arg("n_epochs"), py::arg("stream"), py::arg("check_every") = 8,
              py::arg("use_graph") = true, py::call_guard<py::gil_scoped_release>())
+        .def("prepare", &MLPTrainerT<double>::prepare)
         .def("predict_logits", &MLPTrainerT<double>::predict_logits)
         .def_property_readonly("fused", &MLPTrainerT<double>::fused)
         .def("stamps", &MLPTrainerT<double>::stamps)

@@ -223,9 +223,17 @@ class Comm:
         with the failing ranks named; never a split state, never an unbounded hang."""
         if self.native is not None or self.size == 1 or not self.rccl_allowed:
             return self.native
+        t = self.rccl_timeout_s
+        if self.device.type == "cuda" and self._rccl_factory is None:
+            # ranks sharing a GPU (--device cuda:0 on a one-GPU box): RCCL refuses duplicate
+            # devices, so every rank agrees to stay on the host path instead of failing the job
+            from .peer import device_key
+            keys = self.agree("rccl-devices", device_key(self.device), t)
+            if len(set(keys)) < len(keys):
+                self.rccl_allowed = False
+                return None
         if self.rccl_env is None:
             self.rccl_env = pin_rccl_env(self.rccl_proto)
-        t = self.rccl_timeout_s
         factory = self._rccl_factory
         if factory is None:
             from ..ops import native

@@ -133,6 +133,31 @@ def test_hip_packed_equals_single(data):
 
 
 @pytest.mark.gpu
+def test_hip_sweep_two_ranks_sharing_the_gpu():
+    """The [H] entrypoint with two ranks on one GPU (``--device cuda:0``): its packed jobs run from
+    several host threads per rank.  Jobs whose epoch graphs were captured inside those threads saw
+    the captures invalidated when another thread's allocations, copies or polling overlapped them
+    (two ranks on one GPU made that likely); every job is now built and captured before the threads
+    start (``prepare_packed``).  Also: RCCL, which refuses two ranks on one device, is skipped by
+    agreement and the averages go through the host."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "hyperparameters_tuning.py",
+                        "--device", "cuda:0", "--quiet", "--hidden", "[(16,), (12, 8), (20, 6)]", "--lrs", "0.004",
+                        "0.02", "--max-iter", "15"], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Best Global Hyperparameters" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
 def test_hip_sweep_concurrent_groups_equal_sequential():
     """run_sweep trains the packed jobs of all hidden configs concurrently (threads + streams):
     results equal the same jobs fitted one after another."""
