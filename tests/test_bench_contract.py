@@ -80,6 +80,8 @@ def test_bench_self_launch_eight_ranks_shared_gpu():
     assert rec["config"]["data_plane"] == "xgmi-oneshot+adam", rec["config"]
     assert rec["config"]["round_design"] == "lagged-eval+adam-fedavg"
     assert rec["config"]["adam_grid"] == 16
+    # 1000-row shards (63 workgroups of 16 rows): the lagged scoring runs on workgroups of its own
+    assert rec["config"]["split_score"] is True
     assert rec["replicas_consistent"] is True
     _check_headline_config(rec, 8)
 
