@@ -60,6 +60,18 @@ def _worker(rank, world, port, mode, q):
     comm.rccl_allowed = True
     comm._rccl_factory = _make_factory(mode, rank)
     out = {"rank": rank}
+    if mode == "shared":
+        # two ranks on one GPU (device identities equal): the native bootstrap is never reached
+        import fedmi.parallel.peer as peer
+        peer.device_key = lambda device: "gpu-0-uuid"
+        comm.device = torch.device("cuda", 0)
+        comm._rccl_factory = None
+        out["handle"] = comm.rccl()
+        out["allowed"] = comm.rccl_allowed
+        q.put(out)
+        q.close()
+        q.join_thread()
+        os._exit(0)
     absent = {"absent1": 1, "absent0": 0}.get(mode)
     t0 = time.monotonic()
     if rank == absent:
@@ -119,6 +131,14 @@ def test_bootstrap_peer_never_arrives_raises_within_deadline(mode):
     assert "err" in r, res
     assert ("rank(s) [1]" in r["err"]) if mode == "absent1" else ("rank 0 did not publish" in r["err"])
     assert r["elapsed"] < 10.0, r   # deadline 3 s (+3 s agreement), not gloo's 600 s
+
+
+def test_bootstrap_skipped_when_ranks_share_a_gpu():
+    """Ranks whose devices are the same GPU (``--device cuda:0`` on a one-GPU box) agree over the
+    store to stay on the host path: RCCL refuses duplicate devices, so no bootstrap is attempted."""
+    res = _run("shared")
+    for r in res:
+        assert r["handle"] is None and r["allowed"] is False, res
 
 
 def test_rccl_not_allowed_returns_none():
