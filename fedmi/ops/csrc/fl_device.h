@@ -52,7 +52,11 @@ __device__ __forceinline__ void slab_store(float* p, float v) {
 __device__ __forceinline__ void slab_store_h(uint16_t* p, float v) {
     const float c = v == v ? fminf(fmaxf(v, -65504.f), 65504.f) : v;
     const _Float16 h = (_Float16)c;
+#ifndef FL_SLAB_CACHED
     __builtin_nontemporal_store(*reinterpret_cast<const uint16_t*>(&h), p);
+#else
+    *p = *reinterpret_cast<const uint16_t*>(&h);
+#endif
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
