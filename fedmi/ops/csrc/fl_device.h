@@ -34,11 +34,15 @@ __device__ __forceinline__ void lds_count_wait(int* cnt, int target) {
 // once, by the next kernel: non-temporal stores stream it past the L2, so the train kernel's
 // end no longer writes back 11 MB of dirty lines (measured: fl_train 19.5 -> 14.8 us per
 // round, rocprofv3; FL_SLAB_CACHED restores plain stores for comparison).
+// write-through (`sc1`), as the fp16 slab (slab_store_h): fp32 round 27.65 -> 26.78 us steady
+// against nontemporal stores (profiles/slab_store_policy_r5.log)
 __device__ __forceinline__ void slab_store(float* p, float v) {
-#ifndef FL_SLAB_CACHED
+#if defined(FL_SLAB_CACHED)
+    *p = v;
+#elif defined(FL_SLAB_NT)
     __builtin_nontemporal_store(v, p);
 #else
-    *p = v;
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
 }
 
@@ -52,10 +56,16 @@ __device__ __forceinline__ void slab_store(float* p, float v) {
 __device__ __forceinline__ void slab_store_h(uint16_t* p, float v) {
     const float c = v == v ? fminf(fmaxf(v, -65504.f), 65504.f) : v;
     const _Float16 h = (_Float16)c;
-#ifndef FL_SLAB_CACHED
+    // write-through (`sc1`: the line leaves the XCD's L2 at once, so the next kernel's reads from
+    // other XCDs need no write-back at the kernel boundary): -0.4 us per one-client round in the
+    // driver's shape and -0.8 to -0.9 us per emulated N > 1 round against nontemporal stores
+    // (profiles/slab_store_policy_r5.log); FL_SLAB_NT / FL_SLAB_CACHED for A/B builds
+#if defined(FL_SLAB_CACHED)
+    *p = *reinterpret_cast<const uint16_t*>(&h);
+#elif defined(FL_SLAB_NT)
     __builtin_nontemporal_store(*reinterpret_cast<const uint16_t*>(&h), p);
 #else
-    *p = *reinterpret_cast<const uint16_t*>(&h);
+    __hip_atomic_store(p, *reinterpret_cast<const uint16_t*>(&h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
 }
 
