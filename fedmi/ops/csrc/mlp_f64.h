@@ -60,6 +60,7 @@ struct SkfArgs {
     const int* epoch_ctr;
     long long n_perm;
     int off, rows, Bmax, maxw, head;        // minibatch rows perm[off : off + rows]; head 1 = logistic
+    int wthru;                              // row pass writes acts / deltas / rows through (sc1): large jobs
     double inv_rows, alpha, beta1, beta2, eps, l2_coef;
     double *params, *m, *v;                 // [T][P]
     const double* lr;                       // [T]

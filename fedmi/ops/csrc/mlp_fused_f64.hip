@@ -58,6 +58,15 @@ size_t skf_lds_bytes(const SkfArgs& a) {
 
 // Workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding
 // global store (vmcnt 0), i.e. for the activations / deltas streaming out to memory
+// The row pass's outputs for the wgrad kernel (gathered rows, activations, deltas).  SkfArgs::wthru
+// (FEDMI_SK_WTHRU=1) writes them through (`sc1`) so no XCD's L2 holds them dirty at the kernel
+// boundary: (400, 200) x 9 172-191 -> 159 us per step, but (50, 400) x 1 49 -> 58 and (50, 400) x 9
+// 66 -> 76 (profiles/sk_store_policy_r5.log); default-policy stores by default.
+__device__ __forceinline__ void skf_st(double* p, double v, bool wthru) {
+    if (wthru) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 __device__ __forceinline__ void skf_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ double skf_wave_sum(double v) {
@@ -290,7 +299,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
         double v = 0.0;
         if (r < nr && f < F) {
             v = a.X[(size_t)perm[r] * F + f];
-            xg[(size_t)r * F + f] = v;
+            skf_st(&xg[(size_t)r * F + f], v, a.wthru);
         }
         bufp(0)[r * ldof(0) + f] = v;
     }
@@ -314,7 +323,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
             double* ag = a.acts + (((size_t)l * a.T + t) * a.Bmax + r0) * a.maxw;
             for (int e = threadIdx.x; e < nr * N; e += blockDim.x) {
                 const int r = e / N, c = e - r * N;
-                ag[(size_t)r * a.maxw + c] = bufp(l + 1)[r * ldof(l + 1) + c];
+                skf_st(&ag[(size_t)r * a.maxw + c], bufp(l + 1)[r * ldof(l + 1) + c], a.wthru);
             }
         }
     }
@@ -354,7 +363,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
         double* dg = a.deltas + (((size_t)(a.L - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
         for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
             const int r = e / C, c = e - r * C;
-            dg[(size_t)r * a.maxw + c] = z[r * ldz + c];
+            skf_st(&dg[(size_t)r * a.maxw + c], z[r * ldz + c], a.wthru);
         }
     }
     // backward: delta of layer l - 1 from layer l's, over the activation it masks
@@ -370,7 +379,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
         double* dg = a.deltas + (((size_t)(l - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
         for (int e = threadIdx.x; e < nr * K; e += blockDim.x) {
             const int r = e / K, c = e - r * K;
-            dg[(size_t)r * a.maxw + c] = bufp(l)[r * ldof(l) + c];
+            skf_st(&dg[(size_t)r * a.maxw + c], bufp(l)[r * ldof(l) + c], a.wthru);
         }
     }
     if (a.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -310,6 +310,10 @@ class MLPTrainerT {
         for (int l = 0; l < L_ && l < SKF_MAXL; ++l) { a.w_off[l] = w_off_[l]; a.b_off[l] = b_off_[l]; }
         a.X = reinterpret_cast<const double*>(X_); a.y = y_; a.perms = perms_; a.epoch_ctr = epoch_ctr_;
         a.n_perm = n_; a.off = off; a.rows = rows; a.Bmax = B_; a.maxw = maxw_; a.head = head_;
+        // write the row pass's hand-off buffers through (sc1): FEDMI_SK_WTHRU=1; off by default --
+        // it helped (400, 200) x 9 and hurt (50, 400) x 1 / x 9 (profiles/sk_store_policy_r5.log)
+        const char* wt_env = std::getenv("FEDMI_SK_WTHRU");
+        a.wthru = wt_env != nullptr && wt_env[0] == '1';
         a.inv_rows = 1.0 / (double)rows; a.alpha = alpha_; a.beta1 = beta1_; a.beta2 = beta2_; a.eps = eps_;
         a.l2_coef = 0.5 * alpha_;
         a.params = reinterpret_cast<double*>(params_); a.m = reinterpret_cast<double*>(m_);
