@@ -68,6 +68,14 @@ def _worker(rank, world, port, mode, q):
         comm._rccl_factory = None
         out["handle"] = comm.rccl()
         out["allowed"] = comm.rccl_allowed
+        # rank 0 hosts the store: it leaves only after the other rank has finished with it
+        store = comm._store()
+        if rank != 0:
+            store.set("test/done/1", "1")
+        else:
+            t_end = time.monotonic() + 30.0
+            while not store.check(["test/done/1"]) and time.monotonic() < t_end:
+                time.sleep(0.01)
         q.put(out)
         q.close()
         q.join_thread()
