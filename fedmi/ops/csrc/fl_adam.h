@@ -31,16 +31,23 @@ typedef float fl_float4v __attribute__((ext_vector_type(4)));
 // bf16 mode: parameter -> packed LDS-layout image(s).  A weight is stored as its bf16 hi part
 // and, `wlo_delta` bytes further, its lo part bf16(p - hi) (split-bf16 forward, fl_common.h);
 // a bias stays fp32.
+#ifdef FL_PACK_SC1  // (A/B builds: the packed image written through)
+template <typename T>
+__device__ __forceinline__ void pk_st(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+#else
+template <typename T>
+__device__ __forceinline__ void pk_st(T* p, T v) { *p = v; }
+#endif
 __device__ __forceinline__ void pack_store(char* img, int pk, bool is_bias, int wlo_delta, float p) {
     if (is_bias) {
-        *reinterpret_cast<float*>(img + pk) = p;
+        pk_st(reinterpret_cast<float*>(img + pk), p);
         return;
     }
     const uint32_t u = __float_as_uint(p);
     const uint32_t h = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
     const uint32_t r = __float_as_uint(p - __uint_as_float(h << 16));
-    *reinterpret_cast<uint16_t*>(img + pk) = (uint16_t)h;
-    *reinterpret_cast<uint16_t*>(img + pk + wlo_delta) = (uint16_t)((r + 0x7fffu + ((r >> 16) & 1u)) >> 16);
+    pk_st(reinterpret_cast<uint16_t*>(img + pk), (uint16_t)h);
+    pk_st(reinterpret_cast<uint16_t*>(img + pk + wlo_delta), (uint16_t)((r + 0x7fffu + ((r >> 16) & 1u)) >> 16));
 }
 
 // Adam step of one parameter (wave 0 lane of fl_adam_kernel) from the block's partial sums.
