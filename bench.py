@@ -173,6 +173,10 @@ def main(argv=None):
     ap.add_argument("--prime-replays", type=int, default=1,
                     help="untimed replays of the timed region's graph after its capture (warm-up; 1 / 2 / 3 "
                          "measured the same at 20 steps, profiles/prime_replays_ab_r5.log)")
+    ap.add_argument("--trace-rounds", type=int, default=8,
+                    help="after the timed region (untimed): this many rounds of the same round design issued "
+                         "eagerly with a hipEvent per launch (HipRoundEngine.trace) -> per-kernel us per round in "
+                         "the record's kernel_trace_us (0: off)")
     ap.add_argument("--no-convergence", action="store_true")
     ap.add_argument("--no-anchor", action="store_true", help="skip the same-box eager torch anchor")
     ap.add_argument("--no-fp32", action="store_true", help="skip the untimed fp32-kernel round (one client)")
@@ -228,7 +232,8 @@ def main(argv=None):
     # (ranks sharing one GPU: the Adam kernels' in-kernel chunk exchange needs every rank's
     # exchanging blocks resident at once; make_peer_allreduce bounds the grid for that --
     # fedmi.parallel.peer.shared_adam_grid -- so the N > 1 round design is the same as on N GPUs)
-    max_rounds = a.warmup + a.steps + max(1, a.prime_replays) * g + 16
+    trace_warm = 2  # untraced rounds behind the trace's gate (absorb the ranks' start skew)
+    max_rounds = a.warmup + a.steps + max(1, a.prime_replays) * g + 16 + max(0, a.trace_rounds) + trace_warm
     # the early-stop rule runs in every round; a patience above the run's length keeps every
     # timed round live (a stop would turn the remaining rounds into no-ops)
     patience = a.patience if a.patience > 0 else max_rounds + 1
@@ -243,9 +248,10 @@ def main(argv=None):
     # a GPU, the companion run's engine on a fresh stream ran 2.3x slower)
     stream = torch.cuda.Stream(device=dev)
 
-    def timed_rounds(rows_local: int, rows_total: int, dtype: str = a.dtype):
+    def timed_rounds(rows_local: int, rows_total: int, dtype: str = a.dtype, trace: int = 0):
         """Build a client with `rows_local` rows (FedAvg weight rows_local / rows_total), warm up,
-        time exactly a.steps rounds (max over ranks), close + check; returns (dt, engine, primed)."""
+        time exactly a.steps rounds (max over ranks), then (untimed) trace `trace` rounds, close +
+        check; returns (dt, engine, primed, trace record or None)."""
         X, y = synth_shard(rows_local, comm.rank, dev)
         cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=max_rounds, early_stop=a.early_stop,
                            patience=patience, rows_per_block=a.rows_per_block, graph_rounds=g,
@@ -267,17 +273,33 @@ def main(argv=None):
             t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        eng._issue(1)  # untimed closing round: scores the last timed round
+        tr, traced = None, 0
+        if trace > 0:
+            # per-kernel breakdown of the same round design (eager, events per launch); the max
+            # over ranks of each kind (at N > 1 waiting for a slower rank lands in "adam")
+            barrier()
+            tr = eng.trace(trace, close=False, warm=trace_warm)
+            traced = trace + trace_warm
+            kinds = sorted(k for k, v in tr.items() if isinstance(v, float))
+            if N > 1:
+                t = torch.tensor([tr[k] for k in kinds], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                tr.update(zip(kinds, t.tolist()))
+            tr = {**{k: round(tr[k], 3) for k in kinds}, "launches": tr["launches"], "rounds": tr["rounds"],
+                  "method": "eager rounds behind a gate kernel, hipEvent after every launch (each interval "
+                            "carries ~3 us of eager launch + marker cost over the kernel's rocprofv3 duration, "
+                            "profiles/kernel_trace_r5.log); max over ranks"}
+        eng._issue(1)  # untimed closing round: scores the last timed (or traced) round
         eng.sync_history()
         h = eng.history()
         # every timed round was live and folded (a stop would leave rounds_run short)
-        assert h["rounds_run"] == a.warmup + primed + a.steps + 1 and h["stop_round"] < 0, \
+        assert h["rounds_run"] == a.warmup + primed + a.steps + traced + 1 and h["stop_round"] < 0, \
             (h["rounds_run"], primed, h["stop_round"])
-        return dt, eng, primed
+        return dt, eng, primed, tr
 
     rows_local = a.rows_per_client or reference_rows(a.total_rows, N, comm.rank)
     rows_total = a.rows_per_client * N if a.rows_per_client else a.total_rows
-    dt, eng, primed = timed_rounds(rows_local, rows_total)
+    dt, eng, primed, ktrace = timed_rounds(rows_local, rows_total, trace=max(0, a.trace_rounds))
     h = eng.history()
     # every rank must hold the same global model and metric history (raises otherwise: no number
     # is reported for a run whose FedAvg was not FedAvg)
@@ -305,7 +327,7 @@ def main(argv=None):
         if N == 1 and rows_local == REF_TRAIN_ROWS:
             weak = {"value": value, "us_per_round": dt / a.steps * 1e6, "rows_per_client": REF_TRAIN_ROWS}
         else:
-            dtw, engw, _ = timed_rounds(REF_TRAIN_ROWS, REF_TRAIN_ROWS * N)
+            dtw, engw, _, _ = timed_rounds(REF_TRAIN_ROWS, REF_TRAIN_ROWS * N)
             weak = {"value": REF_TRAIN_ROWS * N * a.steps / dtw, "us_per_round": dtw / a.steps * 1e6,
                     "rows_per_client": REF_TRAIN_ROWS, "scaling": "weak",
                     "replicas_consistent": check_replicas(comm, [engw.global_flat()])}
@@ -320,7 +342,7 @@ def main(argv=None):
     if N == 1 and a.dtype != "fp32" and not a.no_fp32:
         # the reference-precision companion, timed EXACTLY like the headline: same shard, same
         # --warmup / --steps, early-stop rule live, one graph replay of the timed steps
-        dtf, engf, _ = timed_rounds(rows_local, rows_total, dtype="fp32")
+        dtf, engf, _, _ = timed_rounds(rows_local, rows_total, dtype="fp32")
         fp32_us = dtf / a.steps * 1e6
         del engf
         gc.collect()
@@ -362,6 +384,7 @@ def main(argv=None):
                        "graph_rounds": g, "share_gpu": bool(a.share_gpu)},
             "samples_per_sec_per_client": value / N,
             "us_per_round": dt / a.steps * 1e6,
+            "kernel_trace_us": ktrace,
             "weak_8000_rows_per_client": weak,
             "torch_eager_us_per_round_1client": anchor,
             "fp32_us_per_round": fp32_us if a.dtype != "fp32" else dt / a.steps * 1e6,

@@ -768,6 +768,27 @@ class HipRoundEngine(RoundEngineBase):
         self.sync_history()
         return {k + "_us": v / max(n, 1) for k, v in acc.items()}
 
+    def trace(self, n: int, close: bool = False, gate_us: float = 5000.0, warm: int = 0) -> Dict[str, object]:
+        """Per-kernel breakdown of ``n`` rounds of the engine's REAL round design (unlike
+        :meth:`profile`, which runs classic phases): the native engine issues them eagerly with
+        a hipEvent after every launch behind a gate kernel (FLEngine::trace), so the kernels
+        run back to back.  Returns mean us per round by kernel kind (``train``, ``adam``,
+        ``eval``, ``pack``, ``allreduce``, ``eval_fedavg``), ``round`` and launch counts.  Each
+        interval carries the eager launch + event marker cost: measured on MI355X (bench N = 1,
+        profiles/kernel_trace_r5.log) ~3 us per kernel over the rocprofv3 kernel durations.
+        Collective on multi-client engines (every rank must call it with the same ``n``);
+        ``warm`` untraced rounds run first behind the gate (they absorb the ranks' start skew)."""
+        if self.cfg.debug or (self.world > 1 and not self._engine_reduces()):
+            raise RuntimeError("trace: needs an engine that issues its own FedAvg")
+        n, warm = int(n), int(warm)
+        if n < 1 or warm < 0 or self.rounds_issued + warm + n > self.cfg.max_rounds:
+            raise RuntimeError("trace: needs n >= 1 and warm + n rounds left (max_rounds)")
+        # (pending host-side weight changes etc. are handled inside run(), like eager rounds)
+        out = dict(self.engine.trace(self.rounds_issued, n, self._stream(), self._native_comm,
+                                     close=close, gate_us=gate_us, warm=warm))
+        self.rounds_issued += warm + n
+        return out
+
     def _issue(self, n: int, close: bool = True, graph_rounds: Optional[int] = None) -> None:
         """Issue rounds [rounds_issued, rounds_issued + n) on the current stream.
 

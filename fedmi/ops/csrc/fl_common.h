@@ -384,3 +384,5 @@ hipError_t fl_launch_synth(float* X, int* y, long long n_rows, int n_features,
                            unsigned long long seed, unsigned long long row_offset,
                            const float* teacher_w1, const float* teacher_w2, int teacher_hidden,
                            hipStream_t s, float label_noise = 0.f);
+// Hold stream `s` for `us` microseconds (one sleeping wave; FLEngine::trace).
+hipError_t fl_launch_gate(double us, hipStream_t s);

@@ -639,6 +639,61 @@ class FLEngine {
         return out;
     }
 
+    // Per-kernel device time of the REAL round design (us per round, by kernel kind): rounds
+    // [r0, r0 + n) are issued eagerly exactly as run() issues them, with a hipEvent after every
+    // launch; a sleeping gate kernel holds the stream until the whole sequence is enqueued, so
+    // the kernels run back to back (host launch pace does not leak into the intervals).  The
+    // interval before a kernel's event is charged to that kernel: launch gaps on the device
+    // are included (that is what a graph replay pays too, minus the graph's own launch cost).
+    // With the Adam-fused peer exchange, waiting for slower ranks shows up under "adam".
+    // `warm` untraced rounds run first behind the gate (they absorb the ranks' start skew: the
+    // first in-kernel exchange waits for the last rank to arrive).
+    py::dict trace(int r0, int n, uintptr_t stream, RcclComm* comm, bool close, double gate_us, int warm) {
+        if (rec_ != nullptr) throw std::runtime_error("trace: not inside a trial batch");
+        if (n < 1 || warm < 0) throw std::runtime_error("trace: n >= 1, warm >= 0");
+        hipStream_t s = as_stream(stream);
+        std::vector<std::pair<int, hipEvent_t>> ev;
+        hipEvent_t e0;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(fl_launch_gate(gate_us, s));
+        if (warm > 0) run(r0, warm, stream, comm, false);
+        HIP_CHECK(hipEventRecord(e0, s));
+        tev_ = &ev;
+        try {
+            run(r0 + warm, n, stream, comm, close);
+        } catch (...) {
+            tev_ = nullptr;
+            throw;
+        }
+        tev_ = nullptr;
+        HIP_CHECK(hipStreamSynchronize(s));
+        static const char* names[TR_N] = {"pack", "train", "adam", "eval", "allreduce", "eval_fedavg"};
+        double us[TR_N] = {0};
+        int cnt[TR_N] = {0};
+        hipEvent_t prev = e0;
+        for (auto& [what, e] : ev) {
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, prev, e));
+            us[what] += 1e3 * ms;
+            ++cnt[what];
+            prev = e;
+        }
+        float total = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&total, e0, prev));
+        py::dict out, launches;
+        for (int k = 0; k < TR_N; ++k)
+            if (cnt[k]) {
+                out[names[k]] = us[k] / n;
+                launches[names[k]] = cnt[k];
+            }
+        out["round"] = 1e3 * total / n;
+        out["launches"] = launches;
+        out["rounds"] = n;
+        for (auto& pe : ev) hipEventDestroy(pe.second);
+        hipEventDestroy(e0);
+        return out;
+    }
+
     // held-out evaluation: confusion matrix of `params` on (X, y) accumulated into cm_out
     void confusion(uintptr_t X, uintptr_t y, int n_rows, uintptr_t params, uintptr_t cm_out, uintptr_t stream) {
         HIP_CHECK(fl_launch_confusion(d_, c_.R, as_ptr<const float>(X), as_ptr<const int>(y), n_rows,
@@ -689,6 +744,7 @@ class FLEngine {
                 rec_->push_back({FLLaunchRec::TRAIN, {ls, 0, mode, fold_mask}, {pg, si, so, cm_out}});
             else
                 HIP_CHECK(fl_launch_train(d_, c_, b_, pg, si, so, ls, s, mode, cm_out, fold_mask));
+            mark(TR_TRAIN, s);
             // (the fp32 kernels read the fp32 image directly: nothing to repack, but the flag
             // also tells issue_train that the host replaced the weights -- consumed here, or
             // every fused round would flush a separate evaluation)
@@ -707,9 +763,13 @@ class FLEngine {
                 need_pack_ = false;
                 return;
             }
-            if (ls == 0 && !packed) HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
+            if (ls == 0 && !packed) {
+                HIP_CHECK(fl_launch_pack_bf16(d_, e_, pg, b_.pk_global, s));
+                mark(TR_PACK, s);
+            }
             need_pack_ = false;
             HIP_CHECK(fl_launch_train_bf16(d_, e_, c_, b_, pg, si, so, ls, s, solo, mode, cm_out, fold_mask));
+            mark(TR_TRAIN, s);
         }
     }
     void launch_adam(const float* pin, const float* anchor, float* comm, const FLState* st, int ls,
@@ -722,6 +782,7 @@ class FLEngine {
         }
         HIP_CHECK(fl_launch_adam(d_, c_, b_, pin, anchor, comm, st, ls, s, dtype_ == 1 ? &e_ : nullptr, st_out,
                                  fold, tail_a, fold_mask, peer, wx, afold));
+        mark(TR_ADAM, s);
     }
     void launch_eval(const float* params, float* comm, const FLState* st, hipStream_t s) {
         ++eval_launches_;
@@ -731,6 +792,7 @@ class FLEngine {
         }
         if (dtype_ == 0) HIP_CHECK(fl_launch_eval(d_, c_, b_, params, comm, st, s));
         else HIP_CHECK(fl_launch_eval_bf16(d_, ev_, c_, b_, params, comm, st, s));
+        mark(TR_EVAL, s);
     }
     // Train/Adam pairs of round r.  Fused rounds (fl_common.h FL_EVAL_FUSED): the first train
     // kernel also scores the previous round's model from its own forward pass, and the first
@@ -796,6 +858,9 @@ class FLEngine {
             HIP_CHECK(peer_->launch((r + 1) & 1, pbuf_[(r + 1) & 1], dtype_ == 1 ? &pp_ : nullptr, s));
         else if (comm != nullptr)
             comm->allreduce_f32((uintptr_t)pbuf_[(r + 1) & 1], (size_t)comm_len_, (uintptr_t)s);
+        else
+            return;
+        mark(TR_ALLREDUCE, s);
     }
     // `lag`: a lagged round -- no evaluation; the next round's train kernel scores it.
     void issue_round(int r, hipStream_t s, RcclComm* comm, bool allow_fused, bool lag = false) {
@@ -840,6 +905,7 @@ class FLEngine {
             HIP_CHECK(fl_launch_eval_fedavg(d_, c_, b_, b_.local, comm_buf(r), st_[(r + 1) & 1], a, pk, s));
         else
             HIP_CHECK(fl_launch_eval_fedavg_bf16(d_, ev_, c_, b_, b_.local, comm_buf(r), st_[(r + 1) & 1], a, pk, s));
+        mark(TR_EVAL_FEDAVG, s);
     }
 
     struct GraphRec {
@@ -903,6 +969,16 @@ class FLEngine {
     long long eval_launches_ = 0;  // see eval_launches()
     long long graph_evals_ = 0;    // evaluation kernels inside the captured graph
     std::vector<FLLaunchRec>* rec_ = nullptr;  // TrialBatch: record launches instead of issuing them
+    // trace(): an event after every launch, tagged with what was launched
+    enum { TR_PACK, TR_TRAIN, TR_ADAM, TR_EVAL, TR_ALLREDUCE, TR_EVAL_FEDAVG, TR_N };
+    std::vector<std::pair<int, hipEvent_t>>* tev_ = nullptr;
+    void mark(int what, hipStream_t s) {
+        if (tev_ == nullptr) return;
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        tev_->emplace_back(what, e);
+        HIP_CHECK(hipEventRecord(e, s));
+    }
 };
 
 // ---------------------------------------------------------------------------------------
@@ -1168,6 +1244,8 @@ PYBIND11_MODULE(_fedmi_hip, m) {
         .def_property_readonly("graph_captures", &FLEngine::graph_captures)
         .def_property_readonly("eval_launches", &FLEngine::eval_launches)
         .def("time_kernels", &FLEngine::time_kernels)
+        .def("trace", &FLEngine::trace, py::arg("r0"), py::arg("n"), py::arg("stream"), py::arg("comm") = nullptr,
+             py::arg("close") = true, py::arg("gate_us") = 5000.0, py::arg("warm") = 0)
         .def("set_debug", &FLEngine::set_debug)
         .def("invalidate", &FLEngine::invalidate)
         .def("set_early_stop", &FLEngine::set_early_stop)

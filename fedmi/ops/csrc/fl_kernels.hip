@@ -738,6 +738,20 @@ hipError_t fl_launch_synth(float* X, int* y, long long n, int F, unsigned long l
     return hipGetLastError();
 }
 
+// One wave that sleeps for `ticks` of the 100 MHz s_memrealtime clock: holds a stream while
+// the host enqueues an eagerly traced sequence behind it (FLEngine::trace), so the traced
+// kernels run back to back instead of at the host's launch pace.  Bounded: it always exits.
+__global__ void fl_gate_kernel(long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+hipError_t fl_launch_gate(double us, hipStream_t s) {
+    if (!(us >= 0.0) || us > 1e6) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fl_gate_kernel, dim3(1), dim3(64), 0, s, (long long)(us * 100.0));
+    return hipGetLastError();
+}
+
 // Allow the LDS-resident kernels to request more than the default dynamic-LDS window
 // (gfx950 has 160 KiB per CU).
 hipError_t fl_set_lds_limit(size_t bytes) {

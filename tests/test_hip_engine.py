@@ -514,6 +514,23 @@ def test_hip_debug_mode_and_profile():
     t = f.profile(4)
     assert f.history()["rounds_run"] == 7
     assert t["train_us"] > 0 and t["eval_us"] > 0 and t["round_us"] >= t["train_us"]
+    # trace: the real (fused) round design with an event per launch; the rounds it issues are
+    # ordinary rounds (same trajectory as eager/graph rounds)
+    for dtype in ("fp32", "bf16"):
+        cfg3 = EngineConfig(max_rounds=20, early_stop=False, dtype=dtype)
+        a = HipRoundEngine(X, y, 2, cfg3, None, init_flat([14, 50, 200, 2], 1))
+        b = HipRoundEngine(X, y, 2, cfg3, None, init_flat([14, 50, 200, 2], 1))
+        a.run(2)
+        tr = a.trace(6, close=True)
+        a.sync_history()
+        b.run(8)
+        assert a.history()["rounds_run"] == 8
+        np.testing.assert_array_equal(a.global_flat(), b.global_flat())
+        np.testing.assert_array_equal(np.asarray(a.history()["global"]), np.asarray(b.history()["global"]))
+        assert tr["rounds"] == 6 and tr["launches"]["train"] == 6 and tr["launches"]["adam"] == 6
+        assert tr["train"] > 0 and tr["adam"] > 0
+        assert abs(sum(v for k, v in tr.items() if k not in ("round", "launches", "rounds")) - tr["round"]) \
+            < 1e-3 * tr["round"] + 0.01
     # non-finite weights are caught in debug mode
     bad = init_flat([14, 50, 200, 2], 1)
     bad[3] = np.nan
