@@ -36,7 +36,7 @@ def main():
     dev = torch.device("cuda", 0)
     X, y = synth_shard(a.rows, 0, dev)
     g = a.rounds
-    total = 5 + 2 * a.reps * (g + 4) + 16
+    total = 5 + a.reps * (3 * g + 8) + 16  # per rep: prime (<= g + 4 eager + g replayed) + g timed + g eager
     cfg = EngineConfig(hidden=(50, 200), max_rounds=total, early_stop=True, patience=total + 1,
                        graph_rounds=g, dtype="bf16")
     stream = torch.cuda.Stream(device=dev)
