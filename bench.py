@@ -94,6 +94,16 @@ def rounds_to_target(comm, targets=(0.80, 0.83), max_rounds=300, dtype="fp32", l
     return out
 
 
+_T_START = time.perf_counter()
+
+
+def _progress(msg: str) -> None:
+    """FEDMI_BENCH_PROGRESS=1: stage markers with elapsed seconds on stderr (long shared-GPU runs)."""
+    if os.environ.get("FEDMI_BENCH_PROGRESS") == "1":
+        print(f"[bench {os.environ.get('RANK', '0')} +{time.perf_counter() - _T_START:.1f}s] {msg}",
+              file=sys.stderr, flush=True)
+
+
 def _self_launch(a, argv) -> int:
     """``--gpus N`` (N > 1) without a torch.distributed environment: start N ranks with
     torch.distributed.run as a CHILD process (this process never touches the GPU) and exit
@@ -177,6 +187,12 @@ def main(argv=None):
                     help="after the timed region (untimed): this many rounds of the same round design issued "
                          "eagerly with a hipEvent per launch (HipRoundEngine.trace) -> per-kernel us per round in "
                          "the record's kernel_trace_us (0: off)")
+    ap.add_argument("--no-plane-companions", action="store_true",
+                    help="N > 1 on the xGMI plane: skip the untimed-for-the-headline companions that time the same "
+                         "shard with the pull protocol (FEDMI_PEER_LL=0) and with classic rounds (lagged_eval off)")
+    ap.add_argument("--companion-timeout", type=float, default=120.0,
+                    help="seconds the N > 1 plane companions may take before a watchdog prints the record and "
+                         "exits")
     ap.add_argument("--no-convergence", action="store_true")
     ap.add_argument("--no-anchor", action="store_true", help="skip the same-box eager torch anchor")
     ap.add_argument("--no-fp32", action="store_true", help="skip the untimed fp32-kernel round (one client)")
@@ -248,19 +264,22 @@ def main(argv=None):
     # a GPU, the companion run's engine on a fresh stream ran 2.3x slower)
     stream = torch.cuda.Stream(device=dev)
 
-    def timed_rounds(rows_local: int, rows_total: int, dtype: str = a.dtype, trace: int = 0):
+    def timed_rounds(rows_local: int, rows_total: int, dtype: str = a.dtype, trace: int = 0, lagged_eval: bool = True):
         """Build a client with `rows_local` rows (FedAvg weight rows_local / rows_total), warm up,
         time exactly a.steps rounds (max over ranks), then (untimed) trace `trace` rounds, close +
         check; returns (dt, engine, primed, trace record or None)."""
+        _progress(f"engine: {rows_local} rows, {dtype}, lagged_eval={lagged_eval}")
         X, y = synth_shard(rows_local, comm.rank, dev)
         cfg = EngineConfig(hidden=tuple(a.hidden), max_rounds=max_rounds, early_stop=a.early_stop,
                            patience=patience, rows_per_block=a.rows_per_block, graph_rounds=g,
-                           dtype=dtype)
+                           dtype=dtype, lagged_eval=lagged_eval)
         eng = HipRoundEngine(X, y, 2, cfg, comm, init_flat(dims, seed=comm.rank), n_total=rows_total, stream=stream)
         # warm-up: the requested rounds, then (uncounted) the graph of the timed region is
         # captured, instantiated and replayed once, so the timed steps are steady-state replays
+        _progress(f"warm-up ({eng.aggregation})")
         eng.run(a.warmup, check_every=max(a.warmup, 1))
         primed = eng.prime_graph(g, replays=a.prime_replays)
+        _progress("timed region")
         eng.stream.synchronize()
         barrier()
         torch.cuda.synchronize(dev)
@@ -278,6 +297,7 @@ def main(argv=None):
             # per-kernel breakdown of the same round design (eager, events per launch); the max
             # over ranks of each kind (at N > 1 waiting for a slower rank lands in "adam")
             barrier()
+            _progress("trace")
             tr = eng.trace(trace, close=False, warm=trace_warm)
             traced = trace + trace_warm
             kinds = sorted(k for k, v in tr.items() if isinstance(v, float))
@@ -308,11 +328,14 @@ def main(argv=None):
     value = rows_total * a.steps / dt
     # what the record needs from the timed engine; then it is released (its graph, buffers and
     # xGMI peer mappings) before any other engine of this process runs
+    def round_design(e) -> str:
+        return ("fused-eval" if N == 1 else
+                "lagged-eval+adam-fedavg" if e.engine.adam_exchange else
+                "lagged-eval+late-fold" if e.engine.late_fold else
+                "lagged-eval" if e.engine.lagged else "classic")
+
     design = {"aggregation": eng.aggregation,
-              "round_design": ("fused-eval" if N == 1 else
-                               "lagged-eval+adam-fedavg" if eng.engine.adam_exchange else
-                               "lagged-eval+late-fold" if eng.engine.late_fold else
-                               "lagged-eval" if eng.engine.lagged else "classic"),
+              "round_design": round_design(eng),
               "rows_per_block": eng.R, "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
               "split_score": bool(eng.layout.get("split_score", False)),
               "adam_grid": int(eng._peer.adam_grid) if eng._peer is not None else 0,
@@ -348,6 +371,7 @@ def main(argv=None):
         gc.collect()
     # rounds-to-target is measured with the same kernels (dtype) as the throughput
     rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=design["lagged_eval"])
+    rec = None
     if comm.rank == 0:
         rec = {
             "metric": METRIC,
@@ -385,6 +409,7 @@ def main(argv=None):
             "samples_per_sec_per_client": value / N,
             "us_per_round": dt / a.steps * 1e6,
             "kernel_trace_us": ktrace,
+            "plane_companions": None,
             "weak_8000_rows_per_client": weak,
             "torch_eager_us_per_round_1client": anchor,
             "fp32_us_per_round": fp32_us if a.dtype != "fp32" else dt / a.steps * 1e6,
@@ -392,9 +417,85 @@ def main(argv=None):
             "replicas_consistent": replicas_ok,
             "rounds_to_target": rtt,
         }
-        print(json.dumps(rec), flush=True)
+    # N > 1 on the xGMI plane: the same shard timed exactly like the headline with the other
+    # round designs the peer plane offers -- data for choosing between them on real xGMI links,
+    # which no one-GPU session can measure.  They run LAST, each its own engine, under a watchdog:
+    # whatever happens to them, rank 0 prints the headline record exactly once.
+    emit = _Emitter(rec)
+    if N > 1 and design["aggregation"].startswith("xgmi") and not a.no_plane_companions:
+        emit.arm(a.companion_timeout)
+        planes = {}
+        try:
+            for name, env, lagged in (("ll_pull", {"FEDMI_PEER_LL": "0"}, True), ("classic", {}, False)):
+                if name == "ll_pull" and a.share_gpu:
+                    # the pull exchange's Adam blocks spin until every rank's same block arrived and it
+                    # has no bounded-grid variant (peer.shared_adam_grid is LL-only): ranks sharing one
+                    # GPU cannot be guaranteed co-resident (8 shared ranks measured to stall)
+                    planes[name] = {"skipped": "ranks share one GPU (no bounded pull grid)"}
+                    continue
+                old = {k: os.environ.get(k) for k in env}
+                os.environ.update(env)
+                try:
+                    dtc, engc, _, trc = timed_rounds(rows_local, rows_total, trace=max(0, a.trace_rounds),
+                                                     lagged_eval=lagged)
+                    planes[name] = {"us_per_round": dtc / a.steps * 1e6, "value": rows_total * a.steps / dtc,
+                                    "round_design": round_design(engc), "data_plane": engc.aggregation,
+                                    "env": env, "kernel_trace_us": trc,
+                                    "replicas_consistent": check_replicas(comm, [engc.global_flat()])}
+                    del engc
+                    gc.collect()
+                finally:
+                    for k, v in old.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
+                if rec is not None:
+                    rec["plane_companions"] = dict(planes)
+        except Exception as e:  # noqa: BLE001 -- the headline stands; the companion's failure is recorded
+            if rec is not None:
+                rec["plane_companions"] = {**planes, "error": f"{type(e).__name__}: {e}"[:400]}
+            emit.emit()
+    emit.emit()
     comm.close()
+    emit.disarm()
     return 0
+
+
+class _Emitter:
+    """Rank 0's one JSON line, printed exactly once: normally after the plane companions, or by a
+    watchdog when they exceed their time budget -- then the process exits at once (every rank:
+    a companion stuck in a collective or a peer wait must not cost the headline record)."""
+
+    def __init__(self, rec):
+        import threading
+        self.rec, self.lock, self.done, self.timer = rec, threading.Lock(), False, None
+
+    def emit(self) -> None:
+        with self.lock:
+            if not self.done and self.rec is not None:
+                print(json.dumps(self.rec), flush=True)
+            self.done = True
+
+    def _expire(self) -> None:
+        with self.lock:
+            if self.rec is not None and not self.done:
+                self.rec["plane_companions"] = {**(self.rec.get("plane_companions") or {}),
+                                                "error": "watchdog: companions exceeded their time budget"}
+        self.emit()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    def arm(self, seconds: float) -> None:
+        import threading
+        self.timer = threading.Timer(seconds, self._expire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def disarm(self) -> None:
+        if self.timer is not None:
+            self.timer.cancel()
 
 
 def main_wide(a) -> None:

@@ -66,6 +66,13 @@ def test_bench_self_launch_shared_gpu():
     assert rec["replicas_consistent"] is True
     _check_headline_config(rec, 2)
     assert rec["weak_8000_rows_per_client"]["replicas_consistent"] is True
+    # per-kernel trace of the timed design; the other peer-plane designs timed the same way
+    tr = rec["kernel_trace_us"]
+    assert tr["launches"]["train"] == tr["launches"]["adam"] == tr["rounds"] and tr["train"] > 0
+    pc = rec["plane_companions"]
+    assert "skipped" in pc["ll_pull"]  # (separate GPUs only: no bounded pull grid for shared ranks)
+    assert pc["classic"]["round_design"] == "classic" and pc["classic"]["data_plane"] == "xgmi-oneshot"
+    assert pc["classic"]["replicas_consistent"] is True and pc["classic"]["us_per_round"] > 0
 
 
 @pytest.mark.gpu
@@ -76,7 +83,7 @@ def test_bench_self_launch_eight_ranks_shared_gpu():
     evaluation with FedAvg inside the Adam kernel -- on the bounded Adam grid that lets 8 ranks'
     exchanging blocks share one GPU (peer.shared_adam_grid), and the replica check on every rank."""
     rec = _run(["--gpus", "8", "--share-gpu", "--steps", "40", "--warmup", "5", "--no-convergence",
-                "--no-anchor"], n=8, timeout=540)
+                "--no-anchor", "--no-plane-companions"], n=8, timeout=540)
     assert rec["config"]["data_plane"] == "xgmi-oneshot+adam", rec["config"]
     assert rec["config"]["round_design"] == "lagged-eval+adam-fedavg"
     assert rec["config"]["adam_grid"] == 16
@@ -100,3 +107,16 @@ def test_bench_sweep_contract():
     rec = _run(["--config", "sweep", "--steps", "32", "--warmup", "16"])
     assert len(rec["config"]["trials"]) == 12 and "3 trial batches" in rec["config"]["parallelism"]
     assert rec["us_per_trial_round"] > 0 and 0.5 < rec["best_trial"]["train_acc_synthetic"] <= 1.0
+
+
+def test_record_emitter_prints_once_and_watchdog_exits():
+    """bench._Emitter: rank 0's record is printed exactly once -- after the N > 1 plane companions,
+    or by the watchdog when they overrun (which then ends the process with status 0)."""
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "e = bench._Emitter({'value': 1.0}); e.emit(); e.emit(); "
+            "w = bench._Emitter({'value': 2.0}); w.arm(0.3); time.sleep(20)") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert [x["value"] for x in lines] == [1.0, 2.0]
+    assert "watchdog" in lines[1]["plane_companions"]["error"]
