@@ -427,12 +427,6 @@ def main(argv=None):
         planes = {}
         try:
             for name, env, lagged in (("ll_pull", {"FEDMI_PEER_LL": "0"}, True), ("classic", {}, False)):
-                if name == "ll_pull" and a.share_gpu:
-                    # the pull exchange's Adam blocks spin until every rank's same block arrived and it
-                    # has no bounded-grid variant (peer.shared_adam_grid is LL-only): ranks sharing one
-                    # GPU cannot be guaranteed co-resident (8 shared ranks measured to stall)
-                    planes[name] = {"skipped": "ranks share one GPU (no bounded pull grid)"}
-                    continue
                 old = {k: os.environ.get(k) for k in env}
                 os.environ.update(env)
                 try:

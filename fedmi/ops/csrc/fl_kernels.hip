@@ -384,6 +384,35 @@ fl_adam_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin
 #undef ADAM_PA_LL
 }
 
+// The general body on a VIRTUAL grid, for the publish / wait / pull exchange (FEDMI_PEER_LL=0)
+// of ranks that SHARE a GPU: the counterpart of fl_adam_ll_grid_kernel (fl_adam_local.hip; same
+// block order, same deadlock-freedom argument, bit-identical values).  Without it a shared GPU
+// cannot hold every rank's spinning pull grid at once (8 ranks stalled, profiles/plane_companions_r5.log).
+__device__ __forceinline__ void fl_adam_vblock(const int adam_blk, const MLPDesc& d, const FLConfig& c,
+                                               const FLBuffers& b, const float* __restrict__ pin,
+                                               const float* __restrict__ anchor, float* __restrict__ comm,
+                                               const FLState* __restrict__ st, int local_step, const MLPDescB& e,
+                                               int pack, FLState* __restrict__ st_out, int fold, int tail_a,
+                                               int fold_mask, const PeerArgs& pa, int xchg, int afold) {
+#define ADAM_PA_LL (pa.ll != nullptr)
+#define ADAM_BLK adam_blk
+#include "fl_adam_body.inc"
+#undef ADAM_BLK
+#undef ADAM_PA_LL
+}
+
+__global__ void __launch_bounds__(ADAM_WAVES * 64)
+fl_adam_grid_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
+                    const float* __restrict__ anchor, float* __restrict__ comm, const FLState* __restrict__ st,
+                    int local_step, MLPDescB e, int pack, FLState* __restrict__ st_out, int fold, int tail_a,
+                    int fold_mask, PeerArgs pa, int xchg, int afold, int n_vblocks) {
+    for (int vb = blockIdx.x; vb < n_vblocks; vb += gridDim.x) {
+        fl_adam_vblock(vb, d, c, b, pin, anchor, comm, st, local_step, e, pack, st_out, fold, tail_a, fold_mask, pa,
+                       xchg, afold);
+        __syncthreads();  // the block's LDS (partials, state) is free before the next virtual block
+    }
+}
+
 // (the trial-batch Adam kernel lives in fl_adam_batch.hip: 4-wave blocks, same canonical sums)
 
 // Local evaluation of the post-step model on the local shard (C:148, C:75-91): forward,
@@ -618,6 +647,12 @@ hipError_t fl_launch_adam(const MLPDesc& d, const FLConfig& c, const FLBuffers& 
         return fl_launch_adam_ll(d, c, b, pin, anchor, comm, st, local_step, ee, e != nullptr ? 1 : 0, st_out, fold,
                                  tail_a, fold_mask, pa, wx ? 1 : 0, afold ? 1 : 0, s);
 #endif
+    if ((wx || afold) && pa.adam_grid > 0 && pa.adam_grid < blocks) {
+        hipLaunchKernelGGL(fl_adam_grid_kernel, dim3(pa.adam_grid), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor,
+                           comm, st, local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask, pa,
+                           wx ? 1 : 0, afold ? 1 : 0, blocks);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(fl_adam_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor, comm, st,
                        local_step, ee, e != nullptr ? 1 : 0, st_out, fold, tail_a, fold_mask, pa, wx ? 1 : 0,
                        afold ? 1 : 0);

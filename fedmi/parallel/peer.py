@@ -96,7 +96,8 @@ def shared_adam_grid(n_sharing: int, adam_blocks: int) -> int:
     (0 = the full grid of ``adam_blocks``).  Every Adam block spins until the same block of
     every rank has pushed its chunk, so all ranks' blocks must be co-resident; when the full
     grids cannot be, each rank walks its blocks on 128 / n_sharing workgroups
-    (fl_adam_ll_grid_kernel, bit-identical)."""
+    (fl_adam_ll_grid_kernel for LL chunks, fl_adam_grid_kernel for publish / wait / pull;
+    bit-identical)."""
     if n_sharing < 2 or n_sharing * adam_blocks <= SHARED_GPU_ADAM_SLOTS:
         return 0
     return max(1, (SHARED_GPU_ADAM_SLOTS // 2) // n_sharing)

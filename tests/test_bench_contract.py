@@ -70,9 +70,10 @@ def test_bench_self_launch_shared_gpu():
     tr = rec["kernel_trace_us"]
     assert tr["launches"]["train"] == tr["launches"]["adam"] == tr["rounds"] and tr["train"] > 0
     pc = rec["plane_companions"]
-    assert "skipped" in pc["ll_pull"]  # (separate GPUs only: no bounded pull grid for shared ranks)
+    assert pc["ll_pull"]["round_design"] == "lagged-eval+adam-fedavg"
+    assert pc["ll_pull"]["env"] == {"FEDMI_PEER_LL": "0"}
     assert pc["classic"]["round_design"] == "classic" and pc["classic"]["data_plane"] == "xgmi-oneshot"
-    assert pc["classic"]["replicas_consistent"] is True and pc["classic"]["us_per_round"] > 0
+    assert all(v["replicas_consistent"] is True and v["us_per_round"] > 0 for v in pc.values())
 
 
 @pytest.mark.gpu

@@ -302,7 +302,7 @@ def test_peer_world8_production_shape_adam_exchange():
         assert err is None, f"rank {rank}:\n{err}"
         (wl, hl, ll, il), (wp, hp, lp, ip), (wc, hc, lc, ic) = res["ll"], res["pull"], res["classic"]
         assert il["adam_exchange"] and il["uses_ll"] and il["adam_grid"] == 16, il
-        assert ip["adam_exchange"] and not ip["uses_ll"], ip
+        assert ip["adam_exchange"] and not ip["uses_ll"] and ip["adam_grid"] == 16, ip  # fl_adam_grid_kernel
         assert not ic["adam_exchange"] and not ic["lagged"], ic
         assert not res["rccl_created"]
         assert hl["rounds_run"] == hc["rounds_run"] == rounds and hl["stop_round"] < 0
