@@ -190,9 +190,9 @@ def main(argv=None):
     ap.add_argument("--no-plane-companions", action="store_true",
                     help="N > 1 on the xGMI plane: skip the untimed-for-the-headline companions that time the same "
                          "shard with the pull protocol (FEDMI_PEER_LL=0) and with classic rounds (lagged_eval off)")
-    ap.add_argument("--companion-timeout", type=float, default=120.0,
-                    help="seconds the N > 1 plane companions may take before a watchdog prints the record and "
-                         "exits")
+    ap.add_argument("--companion-timeout", type=float, default=180.0,
+                    help="seconds the untimed extras (rounds-to-target, the N > 1 plane companions) may take before "
+                         "a watchdog prints the headline record and exits")
     ap.add_argument("--no-convergence", action="store_true")
     ap.add_argument("--no-anchor", action="store_true", help="skip the same-box eager torch anchor")
     ap.add_argument("--no-fp32", action="store_true", help="skip the untimed fp32-kernel round (one client)")
@@ -369,8 +369,6 @@ def main(argv=None):
         fp32_us = dtf / a.steps * 1e6
         del engf
         gc.collect()
-    # rounds-to-target is measured with the same kernels (dtype) as the throughput
-    rtt = None if a.no_convergence else rounds_to_target(comm, dtype=a.dtype, lagged_eval=design["lagged_eval"])
     rec = None
     if comm.rank == 0:
         rec = {
@@ -415,15 +413,27 @@ def main(argv=None):
             "fp32_us_per_round": fp32_us if a.dtype != "fp32" else dt / a.steps * 1e6,
             "final_train_acc_synthetic": design["final_acc"],
             "replicas_consistent": replicas_ok,
-            "rounds_to_target": rtt,
+            "rounds_to_target": None,
         }
-    # N > 1 on the xGMI plane: the same shard timed exactly like the headline with the other
-    # round designs the peer plane offers -- data for choosing between them on real xGMI links,
-    # which no one-GPU session can measure.  They run LAST, each its own engine, under a watchdog:
-    # whatever happens to them, rank 0 prints the headline record exactly once.
+    # The untimed extras run last under a watchdog: the headline record is complete now, and rank 0
+    # prints it exactly once whatever happens to them (an extra that raises is recorded; one stuck
+    # in a collective or a peer wait ends the process when the budget runs out).
     emit = _Emitter(rec)
-    if N > 1 and design["aggregation"].startswith("xgmi") and not a.no_plane_companions:
-        emit.arm(a.companion_timeout)
+    emit.arm(a.companion_timeout)
+    if not a.no_convergence:
+        try:
+            # rounds-to-target is measured with the same kernels (dtype) as the throughput
+            rtt = rounds_to_target(comm, dtype=a.dtype, lagged_eval=design["lagged_eval"])
+            if rec is not None:
+                rec["rounds_to_target"] = rtt
+        except Exception as e:  # noqa: BLE001
+            if rec is not None:
+                rec["rounds_to_target"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+            emit.emit()
+    # N > 1 on the xGMI plane: the same shard timed exactly like the headline with the other round
+    # designs the peer plane offers -- data for choosing between them on real xGMI links, which no
+    # one-GPU session can measure (each companion is its own engine)
+    if N > 1 and design["aggregation"].startswith("xgmi") and not a.no_plane_companions and not emit.done:
         planes = {}
         try:
             for name, env, lagged in (("ll_pull", {"FEDMI_PEER_LL": "0"}, True), ("classic", {}, False)):
@@ -457,9 +467,9 @@ def main(argv=None):
 
 
 class _Emitter:
-    """Rank 0's one JSON line, printed exactly once: normally after the plane companions, or by a
+    """Rank 0's one JSON line, printed exactly once: normally after the untimed extras, or by a
     watchdog when they exceed their time budget -- then the process exits at once (every rank:
-    a companion stuck in a collective or a peer wait must not cost the headline record)."""
+    an extra stuck in a collective or a peer wait must not cost the headline record)."""
 
     def __init__(self, rec):
         import threading
