@@ -307,7 +307,7 @@ def main(argv=None):
                 tr.update(zip(kinds, t.tolist()))
             tr = {**{k: round(tr[k], 3) for k in kinds}, "launches": tr["launches"], "rounds": tr["rounds"],
                   "method": "eager rounds behind a gate kernel, hipEvent after every launch (each interval "
-                            "carries ~3 us of eager launch + marker cost over the kernel's rocprofv3 duration, "
+                            "carries ~1.5 us of eager launch + marker cost over the kernel's rocprofv3 duration, "
                             "profiles/kernel_trace_r5.log); max over ranks"}
         eng._issue(1)  # untimed closing round: scores the last timed (or traced) round
         eng.sync_history()

@@ -775,7 +775,8 @@ class HipRoundEngine(RoundEngineBase):
         run back to back.  Returns mean us per round by kernel kind (``train``, ``adam``,
         ``eval``, ``pack``, ``allreduce``, ``eval_fedavg``), ``round`` and launch counts.  Each
         interval carries the eager launch + event marker cost: measured on MI355X (bench N = 1,
-        profiles/kernel_trace_r5.log) ~3 us per kernel over the rocprofv3 kernel durations.
+        profiles/kernel_trace_r5.log) ~1.5 us per kernel over the rocprofv3 kernel durations
+        (markers without the system-scope fence; ~3.2 us with it).
         Collective on multi-client engines (every rank must call it with the same ``n``);
         ``warm`` untraced rounds run first behind the gate (they absorb the ranks' start skew)."""
         if self.cfg.debug or (self.world > 1 and not self._engine_reduces()):

@@ -654,7 +654,7 @@ class FLEngine {
         hipStream_t s = as_stream(stream);
         std::vector<std::pair<int, hipEvent_t>> ev;
         hipEvent_t e0;
-        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreateWithFlags(&e0, trace_event_flags()));
         HIP_CHECK(fl_launch_gate(gate_us, s));
         if (warm > 0) run(r0, warm, stream, comm, false);
         HIP_CHECK(hipEventRecord(e0, s));
@@ -972,10 +972,16 @@ class FLEngine {
     // trace(): an event after every launch, tagged with what was launched
     enum { TR_PACK, TR_TRAIN, TR_ADAM, TR_EVAL, TR_ALLREDUCE, TR_EVAL_FEDAVG, TR_N };
     std::vector<std::pair<int, hipEvent_t>>* tev_ = nullptr;
+    // trace markers without the system-scope release/acquire (device-side timing only needs the
+    // marker's timestamp); FEDMI_TRACE_SYSFENCE=1 restores default events (A/B)
+    static unsigned trace_event_flags() {
+        const char* v = std::getenv("FEDMI_TRACE_SYSFENCE");
+        return (v != nullptr && v[0] == '1') ? hipEventDefault : hipEventDisableSystemFence;
+    }
     void mark(int what, hipStream_t s) {
         if (tev_ == nullptr) return;
         hipEvent_t e;
-        HIP_CHECK(hipEventCreate(&e));
+        HIP_CHECK(hipEventCreateWithFlags(&e, trace_event_flags()));
         tev_->emplace_back(what, e);
         HIP_CHECK(hipEventRecord(e, s));
     }

@@ -62,7 +62,7 @@ def main(paths):
         print(f"N={n} {cfg.get('round_design', '?'):24s} {cfg.get('data_plane', '?'):18s} "
               f"{us:8.2f} us/round  value {r['value']:.4g} (x{r['value'] / v0:.2f} vs N={n0})  "
               f"vs_baseline {r.get('vs_baseline') or float('nan'):.1f}  replicas {r.get('replicas_consistent')}")
-        print(f"      kernels (eager trace, us/round, ~3 us marker cost each): {_trace(r.get('kernel_trace_us'))}")
+        print(f"      kernels (eager trace, us/round, ~1.5 us marker cost each): {_trace(r.get('kernel_trace_us'))}")
         weak = r.get("weak_8000_rows_per_client")
         if isinstance(weak, dict):
             print(f"      weak 8000 rows/client: {weak.get('us_per_round', float('nan')):.2f} us/round")
