@@ -1,5 +1,5 @@
 set -o pipefail
-D=gpurun_out/r6v
+D=gpurun_out/${VAL_TAG:-r6v}
 mkdir -p $D
 timeout -k 10 850 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $D/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $D/pytest_gpu.log; exit 1; }
 tail -3 $D/pytest_gpu.log
