@@ -17,6 +17,7 @@ or ``python FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py`` for one cl
 from __future__ import annotations
 
 import argparse
+import os
 import sys
 import time
 
@@ -73,8 +74,12 @@ def parse_args(argv=None):
     ap.add_argument("--resume", default=None, help="checkpoint directory to continue from (same clients/dims)")
     ap.add_argument("--fault-inject", default=None, metavar="RANK:ROUND[:raise|exit|hang]",
                     help="make one client fail at a round (tests the abort path)")
-    ap.add_argument("--watchdog-s", type=float, default=0.0,
-                    help="abort the job if a chunk of rounds stalls this long (0 = off)")
+    ap.add_argument("--watchdog-s", type=float, default=300.0,
+                    help="abort the job (non-zero exit on every rank) if a chunk of rounds stalls this long; 0 = off. "
+                         "The xGMI data plane fails fast by itself (--peer-timeout-s); this is the host-side backstop")
+    ap.add_argument("--peer-timeout-s", type=float, default=None,
+                    help="seconds a device wait of the xGMI data plane waits for a peer before it reports the peer "
+                         "as failed to every rank and the job aborts (default $FEDMI_PEER_TIMEOUT_S or 60)")
     ap.add_argument("--debug", action="store_true", help="synchronised phases + NaN/Inf checks every round")
     ap.add_argument("--profile", type=int, default=0, metavar="N",
                     help="time the first N rounds per phase with hipEvents (HIP engine)")
@@ -175,6 +180,8 @@ def main_clients(a, comm):
 def main(argv=None):
     t_main = time.perf_counter()
     a = parse_args(argv)
+    if a.peer_timeout_s is not None:
+        os.environ["FEDMI_PEER_TIMEOUT_S"] = str(a.peer_timeout_s)   # read by fedmi.parallel.peer
     if not 0.0 < a.participation <= 1.0:
         raise SystemExit("--participation must be in (0, 1]")
     if a.wide and a.participation < 1.0:

@@ -5,8 +5,10 @@ One process per GPU, each GPU one federated client (the reference's mpiexec rank
 (``FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:130-201``): a full-batch
 forward/backward + Adam step + StepLR step on the client's shard (MLP 14->50->200->2,
 bf16 MFMA operands with fp32 accumulation and fp32 master weights / Adam state by default, --dtype fp32 for exact-fp32 kernels), local evaluation of the post-step model on the shard (forward + argmax + weighted
-metrics), and the sample-size-weighted FedAvg of all clients' weights (one RCCL
-all-reduce; per-round metrics and the early-stop state ride in the same collective).
+metrics), and the sample-size-weighted FedAvg of all clients' weights.  At N > 1 the default
+data plane is the xGMI exchange inside the Adam kernel (every parameter block pushes its
+weighted update into every peer's LL ring over the direct links and sums its own ring in rank
+order; the per-round metric tails ride the same exchange), RCCL the fallback.
 
 Data: synthetic balanced-income-shaped rows (14 features, 2 classes) generated on the
 device, weights random-init.  Shards follow the reference's chunking of its 8000 training
@@ -278,7 +280,9 @@ def main(argv=None):
         # captured, instantiated and replayed once, so the timed steps are steady-state replays
         _progress(f"warm-up ({eng.aggregation})")
         eng.run(a.warmup, check_every=max(a.warmup, 1))
-        primed = eng.prime_graph(g, replays=a.prime_replays)
+        # host plane (peer set-up and RCCL both unavailable): rounds are aggregated from Python,
+        # eagerly -- slower, but the run still yields a number labelled data_plane 'host'
+        primed = eng.prime_graph(g, replays=a.prime_replays) if eng._engine_reduces() or N == 1 else 0
         _progress("timed region")
         eng.stream.synchronize()
         barrier()
@@ -288,12 +292,13 @@ def main(argv=None):
         torch.cuda.synchronize(dev)       # (waits for the engine's stream too: one wake-up, not two)
         barrier()
         dt = time.perf_counter() - t0
+        eng._check_peer()  # a failure reported on the xGMI plane: no number for these rounds
         if N > 1:
             t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         tr, traced = None, 0
-        if trace > 0:
+        if trace > 0 and (eng._engine_reduces() or N == 1):
             # per-kernel breakdown of the same round design (eager, events per launch); the max
             # over ranks of each kind (at N > 1 waiting for a slower rank lands in "adam")
             barrier()
@@ -339,6 +344,7 @@ def main(argv=None):
               "rows_per_block": eng.R, "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
               "split_score": bool(eng.layout.get("split_score", False)),
               "adam_grid": int(eng._peer.adam_grid) if eng._peer is not None else 0,
+              "peer_timeout_s": float(eng._peer.timeout_s) if eng._peer is not None else None,
               "lagged_eval": eng.cfg.lagged_eval, "final_acc": float(h["global"][-1][0])}
     X, y = eng.X, eng.y
     del eng
@@ -395,6 +401,7 @@ def main(argv=None):
                        "adam_grid": design["adam_grid"],
                        "round_design": design["round_design"],
                        "rccl_env": comm.rccl_env,
+                       "peer_timeout_s": design["peer_timeout_s"],
                        "rows_per_client": a.rows_per_client or reference_rows(a.total_rows, N, 0),
                        "rows_last_client": a.rows_per_client or reference_rows(a.total_rows, N, N - 1),
                        "rows_per_block": design["rows_per_block"],
@@ -415,20 +422,36 @@ def main(argv=None):
             "replicas_consistent": replicas_ok,
             "rounds_to_target": None,
         }
+        if N > 1 and design["aggregation"] == "host":
+            rec["warning"] = ("FedAvg went through the HOST plane (gloo all-gather, rank-order sums): the xGMI "
+                              "peer set-up and the RCCL bootstrap were both unavailable; this is not the device "
+                              "data plane's number")
     # The untimed extras run last under a watchdog: the headline record is complete now, and rank 0
     # prints it exactly once whatever happens to them (an extra that raises is recorded; one stuck
     # in a collective or a peer wait ends the process when the budget runs out).
     emit = _Emitter(rec)
     emit.arm(a.companion_timeout)
     if not a.no_convergence:
+        emit.stage = "rounds_to_target"
+        ok = True
         try:
             # rounds-to-target is measured with the same kernels (dtype) as the throughput
             rtt = rounds_to_target(comm, dtype=a.dtype, lagged_eval=design["lagged_eval"])
             if rec is not None:
                 rec["rounds_to_target"] = rtt
         except Exception as e:  # noqa: BLE001
+            ok = False
             if rec is not None:
                 rec["rounds_to_target"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+        # every rank learns whether rounds-to-target failed anywhere: a rank that raised must not
+        # leave the others to enter the collective companions alone
+        if N > 1:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = bool(t.item())
+        if not ok:
+            if rec is not None and "error" not in (rec.get("rounds_to_target") or {}):
+                rec["rounds_to_target"] = {"error": "failed on another rank"}
             emit.emit()
     # N > 1 on the xGMI plane: the same shard timed exactly like the headline with the other round
     # designs the peer plane offers -- data for choosing between them on real xGMI links, which no
@@ -437,6 +460,7 @@ def main(argv=None):
         planes = {}
         try:
             for name, env, lagged in (("ll_pull", {"FEDMI_PEER_LL": "0"}, True), ("classic", {}, False)):
+                emit.stage = f"plane_companions.{name}"
                 old = {k: os.environ.get(k) for k in env}
                 os.environ.update(env)
                 try:
@@ -466,14 +490,20 @@ def main(argv=None):
     return 0
 
 
+WATCHDOG_EXIT = 3  # exit status of a run whose untimed extras overran (the record is still printed)
+
+
 class _Emitter:
     """Rank 0's one JSON line, printed exactly once: normally after the untimed extras, or by a
-    watchdog when they exceed their time budget -- then the process exits at once (every rank:
-    an extra stuck in a collective or a peer wait must not cost the headline record)."""
+    watchdog when they exceed their time budget -- then the record names the extra that was
+    running (``stage``), and the process exits at once with status WATCHDOG_EXIT on every rank
+    (an extra stuck in a collective or a peer wait must not cost the headline record, and must
+    not pass for a clean run either)."""
 
     def __init__(self, rec):
         import threading
         self.rec, self.lock, self.done, self.timer = rec, threading.Lock(), False, None
+        self.stage = None   # the untimed extra running now
 
     def emit(self) -> None:
         with self.lock:
@@ -482,14 +512,21 @@ class _Emitter:
             self.done = True
 
     def _expire(self) -> None:
+        stage = self.stage or "untimed extras"
         with self.lock:
             if self.rec is not None and not self.done:
-                self.rec["plane_companions"] = {**(self.rec.get("plane_companions") or {}),
-                                                "error": "watchdog: companions exceeded their time budget"}
+                msg = f"watchdog: {stage} exceeded the extras' time budget"
+                key = "rounds_to_target" if stage == "rounds_to_target" else "plane_companions"
+                self.rec[key] = {**(self.rec.get(key) or {}), "error": msg}
+                self.rec["watchdog"] = {"fired": True, "stage": stage}
         self.emit()
+        print(f"[bench] rank {os.environ.get('RANK', '0')}: watchdog fired during {stage}", file=sys.stderr, flush=True)
+        # release this rank's spinning device waits and tell the peers (xGMI plane), then exit
+        if "fedmi.parallel.peer" in sys.modules:
+            sys.modules["fedmi.parallel.peer"].abort_all()
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(WATCHDOG_EXIT)
 
     def arm(self, seconds: float) -> None:
         import threading

@@ -628,8 +628,9 @@ class HipRoundEngine(RoundEngineBase):
         if self.world > 1 and self._peer is None and comm_buffers is None and comm is not None \
                 and hasattr(comm, "rccl"):
             # RCCL only when the peer plane is off or fell back (every rank agreed on that above),
-            # so this lazy, bounded bootstrap runs on every rank or on none
-            self._native_comm = comm.rccl()
+            # so this lazy, bounded bootstrap runs on every rank or on none; if it fails too, every
+            # rank continues on the host plane (aggregation 'host') instead of raising
+            self._native_comm = comm.rccl_or_host() if hasattr(comm, "rccl_or_host") else comm.rccl()
         self._graph_ready = False
 
     def slab_partials(self) -> torch.Tensor:
@@ -827,6 +828,12 @@ class HipRoundEngine(RoundEngineBase):
                 r += 1
         self.rounds_issued = r
 
+    def set_debug(self, ptr: int) -> None:
+        """Phase stamps (fl_device.h) into the device buffer at ``ptr`` (0: off).  A configuration
+        change: the native engine drops its cached graphs, and so does this side."""
+        self.engine.set_debug(int(ptr))
+        self._graph_ready = False
+
     def _ensure_graph(self, g: int) -> None:
         if not self._graph_ready or self.engine.graph_rounds() != g:
             self.engine.capture(g, self._stream(), self._native_comm)
@@ -861,9 +868,7 @@ class HipRoundEngine(RoundEngineBase):
 
     def _read_state(self, idx: int) -> np.ndarray:
         self.stream.synchronize()
-        if self._peer is not None:
-            from ..parallel.peer import check_peer_error
-            check_peer_error(self._peer)
+        self._check_peer()
         return self.state[idx].cpu().numpy().view(_STATE_DTYPE)[0]
 
     # -- step-by-step API (reference train_one_epoch / evaluate_local / federated_averaging)
@@ -965,17 +970,25 @@ class HipRoundEngine(RoundEngineBase):
             if pend is not None:
                 with (guard(pend[2]) if guard else contextlib.nullcontext()):
                     pend[0].synchronize()
+                # fail fast: a failure reported on the xGMI plane (a peer died / stalled, or
+                # aborted) invalidates this chunk's rounds -- raise before they are folded or printed
+                self._check_peer()
                 self._fold_mirror(mirror[pend[1]])
                 if on_history is not None:
                     on_history(self.history())
             pend = new
             if pend is None:
                 break
+        self._check_peer()
+        self._check_slab_saturation()
+        return self.hist.rounds_run - before
+
+    def _check_peer(self) -> None:
+        """Raise (fedmi.parallel.peer.PeerFailure) if any rank reported a failure of the xGMI
+        data plane; every host-visible result since then is invalid."""
         if self._peer is not None:
             from ..parallel.peer import check_peer_error
             check_peer_error(self._peer)
-        self._check_slab_saturation()
-        return self.hist.rounds_run - before
 
     def _host_mirror(self):
         """Two pinned-host copies (double-buffered by chunk) of the round state and history."""

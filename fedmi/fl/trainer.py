@@ -123,11 +123,15 @@ class FederatedMLPLearning:
             left = rounds - eng.rounds_issued
             while left > 0 and not eng.stopped:
                 n = left if stream else min(chunk, left)
-                if fault is not None and fault.applies(self.rank):
+                if fault is not None:
+                    # EVERY rank (the spec is on every command line) ends a run call at the fault
+                    # round, so the ranks' chunking -- and with it the collectives of each round --
+                    # stays identical up to the fault; only the faulting rank fails there
                     to_fault = fault.round - eng.rounds_issued
-                    if to_fault <= 0:
+                    if to_fault <= 0 and fault.applies(self.rank):
                         fault.trigger(self.rank, eng.rounds_issued)
-                    n = min(n, to_fault)
+                    if to_fault > 0:
+                        n = min(n, to_fault)
                 if stream:
                     eng.run_streaming(n, chunk=stream_chunk, on_history=on_history, guard=wd.guard)
                 else:

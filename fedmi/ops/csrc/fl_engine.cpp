@@ -594,7 +594,11 @@ class FLEngine {
     bool has_peer() const { return peer_ != nullptr; }
 
     // Enable (ptr != 0) / disable in-kernel phase stamps: [blocks, 16] uint64 buffer.
-    void set_debug(uintptr_t ptr) { b_.dbg = as_ptr<unsigned long long>(ptr); }
+    // (a configuration change like any other: cached graphs hold the old stamp buffer)
+    void set_debug(uintptr_t ptr) {
+        b_.dbg = as_ptr<unsigned long long>(ptr);
+        drop_graph();
+    }
 
     // Launch one kernel of round r on its live state (0 = train, 1 = adam, 2 = eval).
     void launch_one(int r, int which, uintptr_t stream) {

@@ -502,7 +502,7 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
     const size_t rowB8 = (size_t)8 * g.ldb * 2, rowA8 = (size_t)8 * g.lda * 2;
     // BUF (the default; variant 10 = without): the pieces through buffer resources (blds16), offsets in SGPRs
     const __amdgpu_buffer_rsrc_t rsB = nt_rsrc(sbB), rsA = nt_rsrc(sbA0);
-    const uint32_t rowA64 = (uint32_t)(64 * g.lda * 2);
+    const uint32_t rowA64 = (uint32_t)((size_t)64 * g.lda * 2);  // < 2^31: checked in gemm_nt_bf16_launch
     auto dmaB = [&](int tile, int i) {
         char* dst = smem + (tile & 1) * 65536 + 32768 + (32 * w + 8 * i) * 128;
         if (BUF) blds16(rsB, voB[i & 1], (uint32_t)(i * rowB8) + tile * 128, dst);
@@ -647,11 +647,18 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
         (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
         (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
         const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
+        // The buffer-resource DMAs address a block's operand rows with 32-bit offsets from the
+        // block's first row (num_records 0x7fffffff): an out-of-range offset would read zeros
+        // silently, so operands whose per-block span (a 256-row tile of A or B, + K) reaches 2^31
+        // bytes take the global_load_lds loop (variant 10) instead.
+        const size_t span_a = (size_t)NT2_BM * (size_t)g.lda * 2 + (size_t)g.K * 2;
+        const size_t span_b = (size_t)NT2_BM * (size_t)g.ldb * 2 + (size_t)g.K * 2;
+        const bool glds = g_nt_variant == 10 || span_a >= 0x7fffffffull || span_b >= 0x7fffffffull;
         // the output configurations of the wide client's GEMMs get their own instantiation
         switch (nt_epi_flags(g)) {
 #define NT_FL_CASE(F)                                                                                      \
     case F:                                                                                                \
-        if (g_nt_variant == 10) hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<F, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g); \
+        if (glds) hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<F, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g); \
         else hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<F, true>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);    \
         break;
             NT_FL_CASE(NT_EPI_CB)                                                  // plain bf16 output
@@ -665,7 +672,7 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
             NT_FL_CASE(NT_EPI_C | NT_EPI_BIAS)                                     // fp32 logits
 #undef NT_FL_CASE
             default:
-                if (g_nt_variant == 10) hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<-1, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);
+                if (glds) hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<-1, false>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);
                 else hipLaunchKernelGGL((gemm_nt_bf16_fl_kernel<-1, true>), dim3(blocks), dim3(NT2_THREADS), 0, s, g);
                 break;
         }

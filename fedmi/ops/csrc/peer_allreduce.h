@@ -33,7 +33,12 @@ class PeerAllReduce {
     // must read as 0).  Call only while no peer is reading: after a host barrier.
     void clear();
     void set_timeout(double seconds);
-    int error() const;                                  // sticky: a wait timed out
+    double timeout_s() const { return (double)timeout_ticks_ * 1e-8; }
+    int error() const;                                  // sticky failure word (PEER_ERR_*, peer_device.h)
+    // Fail-fast abort of the job from the host (Comm.Abort, watchdogs): sets the host abort word
+    // this rank's spinning kernels poll, and (bounded) writes the failure word of every rank, so
+    // the peers' waits end too.  Returns true when the peers' words were written in time.
+    bool abort(double wait_s);
     long long n_floats() const { return n_; }
     int world() const { return world_; }
     int rank() const { return rank_; }
@@ -61,6 +66,9 @@ class PeerAllReduce {
     bool uncached_ = true;
     unsigned* eflags_ = nullptr;       // fused calls: one completion flag per evaluation block
     int n_eval_ = 0;
+    unsigned* host_abort_ = nullptr;   // pinned host word (PeerArgs::host_abort) + its device address
+    unsigned* host_abort_dev_ = nullptr;
+    unsigned* abort_word_ = nullptr;   // pinned source of the failure word abort() writes
 };
 
 void register_peer(pybind11::module_& m);

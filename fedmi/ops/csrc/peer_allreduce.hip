@@ -21,8 +21,11 @@
 //   * send buffers alternate by round parity and flags are monotonic call counters, so no
 //     second barrier is needed: a rank rewrites buffer p (call s + 2) only after every peer
 //     entered call s + 1, i.e. finished reading call s;
-//   * every wait is bounded (s_memrealtime): on a timeout the kernel sets a sticky error word
-//     instead of hanging the GPU, and the host checks it at each synchronisation point.
+//   * every wait is bounded (s_memrealtime): on a timeout the kernel writes a sticky failure
+//     word into EVERY rank's control block instead of hanging the GPU, so every later wait of
+//     every rank ends at once and the job drains in one timeout; the host checks the word after
+//     every chunk of rounds and aborts (fedmi/parallel/peer.py check_peer_error).  A host abort
+//     word in pinned memory lets Comm.Abort / a watchdog release this rank's spinning kernels.
 //
 // The same allocation carries a chunk-flag table and an LL ring for the round engine's
 // Adam-fused exchange (peer_device.h): there the call index comes from the device round state;
@@ -35,7 +38,9 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
+#include <thread>
 #include <cstring>
 #include <stdexcept>
 #include <stdint.h>
@@ -122,6 +127,12 @@ PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, doubl
         PHIP(hipMalloc(reinterpret_cast<void**>(&base_), total_));
     }
     PHIP(hipMemset(base_, 0, total_));
+    PHIP(hipHostMalloc(reinterpret_cast<void**>(&host_abort_), 2 * sizeof(unsigned),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+    host_abort_[0] = 0u;
+    host_abort_[1] = 0u;
+    abort_word_ = host_abort_ + 1;
+    PHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&host_abort_dev_), host_abort_, 0));
     PHIP(hipDeviceSynchronize());
     set_timeout(timeout_s);
 }
@@ -146,6 +157,43 @@ void PeerAllReduce::close() {
         (void)hipFree(base_);
         base_ = nullptr;
     }
+    if (host_abort_) {
+        (void)hipHostFree(host_abort_);
+        host_abort_ = host_abort_dev_ = abort_word_ = nullptr;
+    }
+}
+
+bool PeerAllReduce::abort(double wait_s) {
+    if (host_abort_ == nullptr || base_ == nullptr) return false;
+    const unsigned word = (PEER_ERR_ABORT << 16) | ((unsigned)rank_ << 8) | PEER_MISSING_NONE;
+    // 1. this rank's kernels: they poll the pinned word (no GPU operation needed, cannot block)
+    __atomic_store_n(&host_abort_[0], 1u, __ATOMIC_SEQ_CST);
+    *abort_word_ = word;
+    if (!open_) return false;
+    // 2. every rank's failure word, copied from pinned memory on a private stream (best effort,
+    //    bounded: the caller is tearing the process down)
+    if (hipSetDevice(device_) != hipSuccess) return false;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
+    for (int j = 0; j < world_; ++j) {
+        unsigned* dst = &reinterpret_cast<PeerCtl*>(peer_base_[j] + 2 * buf_bytes_)->err;
+        (void)hipMemcpyAsync(dst, abort_word_, sizeof(unsigned), hipMemcpyHostToDevice, s);
+    }
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds((long long)(wait_s * 1e6));
+    bool done = false;
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) {
+            done = true;
+            break;
+        }
+        if (q != hipErrorNotReady || std::chrono::steady_clock::now() >= t_end) break;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    (void)hipGetLastError();
+    // (a stream still busy is leaked on purpose: destroying it would wait for the copies)
+    if (done) (void)hipStreamDestroy(s);
+    return done;
 }
 
 py::bytes PeerAllReduce::handle() const {
@@ -258,6 +306,9 @@ PeerArgs PeerAllReduce::args(int parity, float* out, long long n_w) const {
     }
     a.rank = rank_;
     a.adam_grid = adam_grid_;
+    if (open_)
+        for (int j = 0; j < world_; ++j) a.err_dst[j] = &reinterpret_cast<PeerCtl*>(peer_base_[j] + 2 * buf_bytes_)->err;
+    a.host_abort = host_abort_dev_;
     return a;
 }
 
@@ -320,7 +371,9 @@ void register_peer(py::module_& m) {
              })
         .def("clear", &PeerAllReduce::clear)
         .def("set_timeout", &PeerAllReduce::set_timeout)
+        .def_property_readonly("timeout_s", [](const PeerAllReduce& p) { return p.timeout_s(); })
         .def("error", &PeerAllReduce::error)
+        .def("abort", &PeerAllReduce::abort, py::arg("wait_s") = 1.0, py::call_guard<py::gil_scoped_release>())
         .def("close", &PeerAllReduce::close)
         .def_property_readonly("world", &PeerAllReduce::world)
         .def_property_readonly("rank", &PeerAllReduce::rank)

@@ -44,10 +44,23 @@ struct PeerCtl {
     unsigned tflags[PEER_MAX_WORLD];  // tails published, per source rank
     unsigned seq;                     // calls this rank has completed
     unsigned done;                    // blocks of the running call that have finished
-    unsigned err;                     // sticky: a wait timed out
+    unsigned err;                     // sticky failure word (PEER_ERR_*), 0 = healthy
     unsigned pad[64 - 2 * PEER_MAX_WORLD - 3];
 };
 static_assert(sizeof(PeerCtl) == 256, "PeerCtl is one 256-byte block");
+
+// The sticky failure word PeerCtl::err = (kind << 16) | (reporting rank << 8) | missing rank.
+// A failure is written into EVERY rank's word (PeerArgs::err_dst), so the whole job drains in
+// one timeout: each later wait of every rank sees the word and returns instead of waiting its
+// own full timeout (the reference's contract is "any failure -> comm.Abort()",
+// FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:129,203-205).
+#define PEER_ERR_TIMEOUT 1u        // a wait of the reporting rank timed out on `missing`
+#define PEER_ERR_ABORT 2u          // the reporting rank's host aborted the job (Comm.Abort / watchdog)
+#define PEER_MISSING_EVAL 0xfeu    // missing: one of the reporting rank's own evaluation blocks
+#define PEER_MISSING_NONE 0xffu
+// Waits look at the failure words only once they have waited this long (100 MHz ticks: 20 us).
+// A healthy round's waits end sooner, so the polling loop of the fast path is unchanged.
+#define PEER_SLOW_TICKS 2000
 
 struct PeerArgs {
     const float* src[PEER_MAX_WORLD];    // every rank's send buffer of this parity (mapped)
@@ -76,6 +89,10 @@ struct PeerArgs {
     // > 0: the LL Adam kernel runs on this many workgroups, each walking several Adam blocks
     // (fl_adam_local.hip fl_adam_ll_grid_kernel) -- for ranks that share one GPU
     int adam_grid;
+    // Fail-fast: every rank's failure word (mapped; [rank] = &ctl->err) and this rank's host
+    // abort word (pinned host memory, written by PeerAllReduce::abort; nullptr: none)
+    unsigned* err_dst[PEER_MAX_WORLD];
+    const unsigned* host_abort;
 };
 
 // All-reduce blocks of a fused evaluation + FedAvg kernel (FL_THREADS = 512 threads each):
@@ -176,16 +193,39 @@ __device__ __forceinline__ void peer_flag_store(unsigned* dst, unsigned v, int u
     }
 }
 
-// Wait until every rank has published `target` in `flags` (one polling lane per rank,
-// bounded by the timeout: on expiry the sticky error word is set and the wait ends).
+// Report a failure to every rank (this lane's vector stores; any lane may call it).
+__device__ __forceinline__ void peer_fail(const PeerArgs& a, unsigned word) {
+    __hip_atomic_store(&a.ctl->err, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int j = 0; j < a.world; ++j)
+        if (j != a.rank && a.err_dst[j] != nullptr)
+            __hip_atomic_store(a.err_dst[j], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Called by a lane whose awaited value has not arrived (after a poll): true when its wait must
+// end.  After PEER_SLOW_TICKS it ends as soon as any rank has reported a failure (the sticky
+// word is set) or this rank's host aborted; at the timeout it reports `missing` to every rank.
+__device__ __forceinline__ bool peer_give_up(const PeerArgs& a, unsigned long long t0, unsigned missing) {
+    const long long dt = (long long)(__builtin_amdgcn_s_memrealtime() - t0);
+    if (dt < PEER_SLOW_TICKS) return false;
+    if (__hip_atomic_load(&a.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return true;
+    if (a.host_abort != nullptr && __hip_atomic_load(a.host_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        peer_fail(a, (PEER_ERR_ABORT << 16) | ((unsigned)a.rank << 8) | PEER_MISSING_NONE);
+        return true;
+    }
+    if (dt > a.timeout) {
+        peer_fail(a, (PEER_ERR_TIMEOUT << 16) | ((unsigned)a.rank << 8) | (missing & 0xffu));
+        return true;
+    }
+    return false;
+}
+
+// Wait until every rank has published `target` in `flags` (one polling lane per rank; ends
+// early on a reported failure, PEER_ERR_*).
 __device__ __forceinline__ void peer_wait(const PeerArgs& a, unsigned* flags, unsigned target) {
     if (threadIdx.x < (unsigned)a.world) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while ((int)(__hip_atomic_load(&flags[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
-            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
-                __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
+            if (peer_give_up(a, t0, threadIdx.x)) break;
             __builtin_amdgcn_s_sleep(2);
         }
     }
@@ -258,27 +298,27 @@ __device__ __forceinline__ void peer_finish(const PeerArgs& a, unsigned target, 
 
 // Wait (bounded) until every evaluation block of this call has stored `target` in its flag:
 // plain per-block stores into uncached memory, so no block serialises on a shared counter.
+// Thread 0 alone decides to give up (waves read different clocks; the block leaves together).
 __device__ __forceinline__ void peer_wait_eval(const PeerArgs& a, unsigned target) {
-    __shared__ int pending_s;
+    __shared__ int state_s;  // 0: all done, 1: pending, 2: give up
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         int pend = 0;
         for (int i = threadIdx.x; i < a.n_eval; i += blockDim.x)
             pend |= (int)(__hip_atomic_load(&a.eflags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0;
-        if (threadIdx.x == 0) pending_s = 0;
+        if (threadIdx.x == 0) state_s = 0;
         __syncthreads();
-        if (pend) pending_s = 1;
+        if (pend) state_s = 1;
         __syncthreads();
-        const int any = pending_s;
+        if (threadIdx.x == 0 && state_s != 0 && peer_give_up(a, t0, PEER_MISSING_EVAL)) state_s = 2;
         __syncthreads();
-        if (!any) {
+        const int st = state_s;
+        __syncthreads();
+        if (st == 0) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with peer_eval_done's release
             break;
         }
-        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
-            if (threadIdx.x == 0) __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-        }
+        if (st == 2) break;
         __builtin_amdgcn_s_sleep(2);
     }
 }
@@ -327,10 +367,7 @@ __device__ __forceinline__ void peer_chunk_wait(const PeerArgs& a, int chunk, un
         const unsigned* f = a.cflags + lane * a.n_chunks + chunk;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
-            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
-                __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
+            if (peer_give_up(a, t0, lane)) break;
             __builtin_amdgcn_s_sleep(2);
         }
     }
@@ -378,9 +415,9 @@ __device__ __forceinline__ void peer_ll_push(const PeerArgs& a, int pos, unsigne
     for (int k = 0; k < PEER_MAX_WORLD; ++k)
         if (k < a.world) __hip_atomic_store(a.ll_dst[k] + slot, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// Sum over ranks (rank order) of ring position `pos` for call `target`, polling (bounded by the
-// timeout: on expiry the sticky error word is set and missing values count 0).  Called by the
-// whole wave; lanes with `active` false (no value at their position) return 0.
+// Sum over ranks (rank order) of ring position `pos` for call `target`, polling (ends early on a
+// reported failure, PEER_ERR_*: then missing values count 0 and the host discards the round).
+// Called by the whole wave; lanes with `active` false (no value at their position) return 0.
 __device__ __forceinline__ float peer_ll_sum(const PeerArgs& a, int pos, unsigned target, bool active) {
     if (!active) return 0.f;
     float v[PEER_MAX_WORLD];
@@ -403,10 +440,7 @@ __device__ __forceinline__ float peer_ll_sum(const PeerArgs& a, int pos, unsigne
                 }
             }
         if (pend == 0) break;
-        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
-            __hip_atomic_store(&a.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-        }
+        if (peer_give_up(a, t0, (unsigned)__builtin_ctz(pend))) break;
         __builtin_amdgcn_s_sleep(1);
     }
     float s = v[0];

@@ -147,6 +147,7 @@ class Comm:
         self.rccl_proto = rccl_proto
         self.rccl_timeout_s = float(os.environ.get("FEDMI_RCCL_TIMEOUT_S", "") or rccl_timeout_s)
         self._rccl_factory = None  # tests inject a fake bootstrap (CPU); None -> native RcclComm
+        self.rccl_error = None     # why RCCL was disabled after a failed bootstrap (rccl_or_host)
         self._agree_gen = 0
         if self.size > 1:
             if not dist.is_initialized():
@@ -247,6 +248,8 @@ class Comm:
         uid = self._share_bytes("rccl-uid", unique_id() if self.rank == 0 else None, 0, t)
         h, err = None, ""
         try:
+            if str(self.rank) in os.environ.get("FEDMI_TEST_RCCL_FAIL", "").split(","):
+                raise RuntimeError("RCCL bootstrap failed (FEDMI_TEST_RCCL_FAIL)")   # test knob
             h = factory(uid)
         except Exception as e:  # noqa: BLE001 -- agreed below, raised on every rank
             err = str(e).replace("\n", " ") or type(e).__name__
@@ -297,9 +300,13 @@ class Comm:
             dist.barrier()
 
     def Abort(self, code: int = 1) -> None:
-        """Tear the job down (reference C:203-205).  Aborting the RCCL communicator first
-        unblocks peers stuck in a collective; the launcher then kills the rest."""
+        """Tear the job down (reference C:203-205).  The xGMI data plane is told first (the
+        host abort word ends this rank's spinning kernels, every rank's failure word ends the
+        peers' waits: ``fedmi.parallel.peer.abort_all``), then the RCCL communicator is aborted,
+        which unblocks peers stuck in a collective; the launcher then kills the rest."""
         try:
+            if "fedmi.parallel.peer" in sys.modules:
+                sys.modules["fedmi.parallel.peer"].abort_all()
             if self.native is not None:
                 self.native.abort()
         finally:
@@ -336,15 +343,41 @@ class Comm:
                 t.mul_(scale)
             if self._nccl_group is not None:
                 dist.all_reduce(t, group=self._nccl_group)
-            else:  # no device communicator: through the host (gloo)
-                h = t.cpu()
-                dist.all_reduce(h)
-                t.copy_(h)
+            else:  # no device communicator: the host plane (gloo)
+                t.copy_(self._host_sum_rank_order(t))
         else:
             if scale is not None:
                 t.mul_(scale)
             dist.all_reduce(t)
         return t
+
+    def _host_sum_rank_order(self, t: torch.Tensor) -> torch.Tensor:
+        """Host plane of device all-reduces: every rank's buffer is all-gathered over gloo and
+        summed as a left fold in rank order -- the order of the xGMI peer kernels, so a job that
+        fell back to the host computes bit-identical FedAvg rounds (gloo's own reduction order
+        depends on the world size)."""
+        h = t.detach().cpu()
+        parts = [torch.empty_like(h) for _ in range(self.size)]
+        dist.all_gather(parts, h)
+        acc = parts[0].clone()
+        for p in parts[1:]:
+            acc += p
+        return acc
+
+    def rccl_or_host(self):
+        """COLLECTIVE.  The RCCL communicator (:meth:`rccl`), or ``None`` when RCCL is not
+        allowed or its bootstrap failed -- then RCCL is disabled for the rest of the job and
+        device all-reduces take the host plane.  Used by the round engine when the xGMI peer
+        set-up fell back: every rank ends on the SAME next plane (the bootstrap's outcome is
+        agreed, :meth:`rccl`), and a multi-GPU run still produces a (labelled) result."""
+        try:
+            return self.rccl()
+        except (RuntimeError, TimeoutError) as e:
+            self.rccl_allowed = False
+            self.rccl_error = str(e)
+            print(f"[fedmi] rank {self.rank}: RCCL unavailable ({e}); device all-reduces go through the host "
+                  "(gloo, rank-order sums) -- data plane 'host'", file=sys.stderr, flush=True)
+            return None
 
     def close(self) -> None:
         if self.native is not None:

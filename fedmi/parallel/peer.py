@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import os
 import sys
+import threading
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -77,9 +79,22 @@ def selftest(h, comm, device, calls: int = 4, timeout_s: float = 10.0) -> bool:
     return ok
 
 
-# 1024-thread Adam workgroups resident at once on one GPU with room left for the other ranks'
-# train kernels: at ~100 VGPRs one such workgroup fills a CU (256 CUs)
-SHARED_GPU_ADAM_SLOTS = 256
+# The exchanging Adam kernels are 1024-thread workgroups at ~125 VGPRs: one resident workgroup
+# per CU.  The spinning grids of every rank sharing a GPU must be resident together, so the slot
+# count is the device's CU count (MI355X: 256; fewer on a partitioned device or another SKU).
+ADAM_WORKGROUPS_PER_CU = 1
+SHARED_GPU_ADAM_SLOTS = 256   # MI355X default when the device cannot be queried
+
+
+def adam_slots(device=None) -> int:
+    """Adam workgroups that can be resident at once on ``device`` (CUs x workgroups per CU)."""
+    if device is not None and torch.cuda.is_available():
+        try:
+            return int(torch.cuda.get_device_properties(torch.device(device)).multi_processor_count) \
+                * ADAM_WORKGROUPS_PER_CU
+        except Exception:  # noqa: BLE001 -- fall back to the MI355X figure
+            pass
+    return SHARED_GPU_ADAM_SLOTS
 
 
 def device_key(device) -> str:
@@ -91,29 +106,75 @@ def device_key(device) -> str:
     return f"{getattr(p, 'pci_domain_id', 0)}:{getattr(p, 'pci_bus_id', 0)}:{getattr(p, 'pci_device_id', 0)}"
 
 
-def shared_adam_grid(n_sharing: int, adam_blocks: int) -> int:
+def shared_adam_grid(n_sharing: int, adam_blocks: int, slots: int = SHARED_GPU_ADAM_SLOTS) -> int:
     """Workgroups of the LL Adam kernel when ``n_sharing`` exchanging ranks sit on ONE GPU
-    (0 = the full grid of ``adam_blocks``).  Every Adam block spins until the same block of
-    every rank has pushed its chunk, so all ranks' blocks must be co-resident; when the full
-    grids cannot be, each rank walks its blocks on 128 / n_sharing workgroups
-    (fl_adam_ll_grid_kernel for LL chunks, fl_adam_grid_kernel for publish / wait / pull;
-    bit-identical)."""
-    if n_sharing < 2 or n_sharing * adam_blocks <= SHARED_GPU_ADAM_SLOTS:
+    with ``slots`` resident Adam workgroups (:func:`adam_slots`; 0 = the full grid of
+    ``adam_blocks``).  Every Adam block spins until the same block of every rank has pushed its
+    chunk, so all ranks' blocks must be co-resident; when the full grids cannot be, each rank
+    walks its blocks on (slots / 2) / n_sharing workgroups -- half the device, so the ranks'
+    train kernels keep room -- (fl_adam_ll_grid_kernel for LL chunks, fl_adam_grid_kernel for
+    publish / wait / pull; bit-identical)."""
+    if n_sharing < 2 or n_sharing * adam_blocks <= slots:
         return 0
-    return max(1, (SHARED_GPU_ADAM_SLOTS // 2) // n_sharing)
+    return max(1, (slots // 2) // n_sharing)
 
 
-def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, check: bool = True,
+DEFAULT_PEER_TIMEOUT_S = 60.0
+
+
+def peer_timeout_s(timeout_s: Optional[float] = None) -> float:
+    """Seconds a device wait of the xGMI plane waits for a peer before it reports the peer as
+    failed to every rank: ``timeout_s``, else ``$FEDMI_PEER_TIMEOUT_S``, else 60."""
+    if timeout_s is not None:
+        return float(timeout_s)
+    env = os.environ.get("FEDMI_PEER_TIMEOUT_S", "").strip()
+    return float(env) if env else DEFAULT_PEER_TIMEOUT_S
+
+
+# Live communicators of this process: Comm.Abort / watchdogs release their spinning kernels and
+# tell every peer (abort_all) before the process exits.
+_LIVE = weakref.WeakSet()
+
+
+def abort_all(wait_s: float = 1.0) -> int:
+    """Fail-fast abort of every live xGMI communicator of this process: the host abort word
+    ends this rank's device waits and every rank's failure word is written, so the peers stop
+    waiting at once (reference: any failure -> comm.Abort(),
+    FL_CustomMLPCLassifierImplementation_Multiple_Rounds.py:203-205).  Runs on a helper thread
+    bounded by ``wait_s`` per communicator (a wedged runtime must not keep the process alive).
+    Returns the number of communicators whose peers were told in time."""
+    told = []
+    for h in list(_LIVE):
+        res = []
+        t = threading.Thread(target=lambda: res.append(bool(h.abort(wait_s))), daemon=True)
+        t.start()
+        t.join(wait_s + 1.0)
+        told.append(bool(res and res[0]))
+    return sum(told)
+
+
+def _test_fail_ranks() -> set:
+    """Test knob ``FEDMI_TEST_PEER_FAIL=1,3``: the peer set-up fails on these ranks (exercises
+    the agreed fallback of every rank to the next data plane)."""
+    env = os.environ.get("FEDMI_TEST_PEER_FAIL", "").strip()
+    return {int(x) for x in env.split(",") if x.strip() != ""}
+
+
+def make_peer_allreduce(comm, n_floats: int, device, timeout_s: Optional[float] = None, check: bool = True,
                         n_chunks: int = 0):
     """Collective.  Returns a native ``PeerAllReduce`` of ``n_floats`` floats, open and
     self-tested on every rank, or ``None`` on every rank (then the caller uses RCCL).
-    ``n_chunks``: chunk-flag table for the Adam-fused exchange of the round engine."""
+    ``n_chunks``: chunk-flag table for the Adam-fused exchange of the round engine.
+    ``timeout_s``: see :func:`peer_timeout_s`."""
     from ..ops import native
     if comm is None or comm.size < 2 or comm.size > PEER_MAX_WORLD:
         return None
+    timeout_s = peer_timeout_s(timeout_s)
     m = native()
     h, why = None, ""
     try:
+        if comm.rank in _test_fail_ranks():
+            raise RuntimeError("peer set-up failed (FEDMI_TEST_PEER_FAIL)")
         h = m.PeerAllReduce(comm.size, comm.rank, torch.device(device).index or 0, int(n_floats), float(timeout_s),
                             int(n_chunks))
         handle = bytes(h.handle())
@@ -127,7 +188,7 @@ def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, ch
         env = os.environ.get("FEDMI_ADAM_GRID", "")
         if env == "":
             mine = gathered[comm.rank][1]
-            h.adam_grid = shared_adam_grid(sum(g[1] == mine for g in gathered), n_chunks - 1)
+            h.adam_grid = shared_adam_grid(sum(g[1] == mine for g in gathered), n_chunks - 1, adam_slots(device))
     if ok:
         try:
             h.open(handles)
@@ -140,9 +201,9 @@ def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, ch
     if h is not None:
         h.set_timeout(timeout_s)
     if not ok:
-        if comm.rank == 0:
-            print(f"[fedmi] one-shot xGMI all-reduce unavailable ({why or 'peer set-up failed'}); using RCCL",
-                  file=sys.stderr, flush=True)
+        # every rank prints its own reason (the failing rank knows why; the others only that it failed)
+        print(f"[fedmi] rank {comm.rank}: one-shot xGMI all-reduce unavailable ({why or 'peer set-up failed on another rank'}); "
+              "falling back to the next data plane", file=sys.stderr, flush=True)
         comm.Barrier()  # nobody still reads a buffer we are about to free
         if h is not None:
             h.close()
@@ -153,10 +214,33 @@ def make_peer_allreduce(comm, n_floats: int, device, timeout_s: float = 60.0, ch
     # before any rank's first real call.
     h.clear()
     comm.Barrier()
+    _LIVE.add(h)
     return h
 
 
+class PeerFailure(RuntimeError):
+    """A rank of the xGMI data plane failed (timed out waiting for a peer, or aborted)."""
+
+
+def describe_peer_error(word: int, timeout_s: Optional[float] = None) -> str:
+    """Human-readable form of the sticky failure word (peer_device.h PEER_ERR_*)."""
+    kind, who, missing = (word >> 16) & 0xFF, (word >> 8) & 0xFF, word & 0xFF
+    if kind == 2:
+        return f"rank {who} aborted the job"
+    if kind == 1:
+        t = f" {timeout_s:g} s" if timeout_s else " its timeout"
+        if missing == 0xFE:
+            return f"rank {who}: its own evaluation blocks did not finish within{t}"
+        return f"rank {who} waited{t} for rank {missing}, which died or stalled"
+    return f"failure word {word:#x}"
+
+
 def check_peer_error(h) -> None:
-    if h is not None and h.error():
-        raise RuntimeError("one-shot xGMI all-reduce: a peer did not arrive within the timeout "
-                           "(a client died or stalled); results since then are invalid")
+    """Raise :class:`PeerFailure` if any rank reported a failure on this communicator: the
+    rounds since then were aggregated from missing contributions and are invalid."""
+    if h is None:
+        return
+    word = int(h.error())
+    if word:
+        raise PeerFailure("xGMI data plane failed: " + describe_peer_error(word, getattr(h, "timeout_s", None))
+                          + "; rounds since then are invalid")

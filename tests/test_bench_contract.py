@@ -112,12 +112,28 @@ def test_bench_sweep_contract():
 
 def test_record_emitter_prints_once_and_watchdog_exits():
     """bench._Emitter: rank 0's record is printed exactly once -- after the N > 1 plane companions,
-    or by the watchdog when they overrun (which then ends the process with status 0)."""
+    or by the watchdog when they overrun, which names the extra that was running and ends the
+    process with a NON-zero status (a hang must not pass for a clean run)."""
     code = ("import sys, time; sys.path.insert(0, %r); import bench; "
             "e = bench._Emitter({'value': 1.0}); e.emit(); e.emit(); "
-            "w = bench._Emitter({'value': 2.0}); w.arm(0.3); time.sleep(20)") % ROOT
+            "w = bench._Emitter({'value': 2.0}); w.stage = 'plane_companions.ll_pull'; w.arm(0.3); "
+            "time.sleep(20)") % ROOT
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
     lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
     assert [x["value"] for x in lines] == [1.0, 2.0]
-    assert "watchdog" in lines[1]["plane_companions"]["error"]
+    assert "plane_companions.ll_pull" in lines[1]["plane_companions"]["error"]
+    assert lines[1]["watchdog"] == {"fired": True, "stage": "plane_companions.ll_pull"}
+    assert "watchdog fired during plane_companions.ll_pull" in p.stderr
+
+
+def test_watchdog_names_rounds_to_target():
+    """A watchdog that fires during rounds-to-target records it there (not as a companion error)."""
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "w = bench._Emitter({'value': 2.0, 'rounds_to_target': None}); w.stage = 'rounds_to_target'; "
+            "w.arm(0.3); time.sleep(20)") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3
+    rec = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][0]
+    assert "rounds_to_target" in rec["rounds_to_target"]["error"]
+    assert "plane_companions" not in rec

@@ -80,6 +80,25 @@ def _worker(rank, world, port, mode, q):
         q.close()
         q.join_thread()
         os._exit(0)
+    if mode == "fallback":
+        # FEDMI_TEST_RCCL_FAIL=1: rank 1's bootstrap fails -> EVERY rank lands on the host plane,
+        # RCCL is disabled for the rest of the job, and the next device all-reduce works (host)
+        os.environ["FEDMI_TEST_RCCL_FAIL"] = "1"
+        out["handle"] = comm.rccl_or_host()
+        out["allowed"] = comm.rccl_allowed
+        out["error"] = comm.rccl_error
+        out["again"] = comm.rccl()          # no second bootstrap
+        t = torch.full((5,), float(rank + 1))
+        comm.allreduce_(t)
+        out["sum"] = t.tolist()
+        # the host plane of device buffers sums in rank order (left fold, bit-identical to the
+        # xGMI kernels): fp32 values whose sum depends on the order
+        v = torch.tensor([1e8, 1.0, -1e8, 3.0], dtype=torch.float32)[rank:rank + 1].repeat(3)
+        out["ordered"] = comm._host_sum_rank_order(v).tolist()
+        q.put(out)
+        q.close()
+        q.join_thread()
+        os._exit(0)
     absent = {"absent1": 1, "absent0": 0}.get(mode)
     t0 = time.monotonic()
     if rank == absent:
@@ -155,3 +174,16 @@ def test_rccl_not_allowed_returns_none():
     from fedmi.parallel.comm import Comm
     c = Comm(backend="gloo", device="cpu")
     assert c.native is None and c.rccl() is None and not c.rccl_allowed
+
+
+def test_failed_bootstrap_falls_back_to_host_on_every_rank():
+    """Data-plane fallback chain, last link: when the RCCL bootstrap fails on one rank, every
+    rank gets ``None`` from ``rccl_or_host`` (the outcome is agreed), RCCL stays disabled, and
+    device all-reduces continue on the host plane with rank-order sums (world 4)."""
+    res = _run("fallback", world=4)
+    for r in res:
+        assert r["handle"] is None and r["allowed"] is False and r["again"] is None, res
+        assert "rank 1" in r["error"] and "FEDMI_TEST_RCCL_FAIL" in r["error"], r
+        assert r["sum"] == [10.0] * 5
+        # ((1e8 + 1) + -1e8) + 3 in fp32 = 3 (the 1 is lost), not 4 = any order adding 1 last
+        assert r["ordered"] == [3.0] * 3, r

@@ -33,10 +33,10 @@ nadam = 1 + (e.engine.layout()["P"] + 63) // 64 if "P" in e.engine.layout() else
 for which, name in kinds:
     for rep in range(5):
         dbg.zero_()
-        e.engine.set_debug(dbg.data_ptr())
+        e.set_debug(dbg.data_ptr())
         e.engine.launch_one(e.rounds_issued - 1, which, e._stream())
         e.stream.synchronize()
-        e.engine.set_debug(0)
+        e.set_debug(0)
     st = dbg.view(nb, 16).cpu().numpy().astype(np.int64)
     t0 = st[:, 0].min()
     print(f"{name}: blocks={nb} dispatch spread={(st[:,0].max()-t0)*10/1000:.2f}us "
@@ -72,12 +72,12 @@ if nadam is not None:
     for rep in range(5):
         dt.zero_()
         da.zero_()
-        e.engine.set_debug(dt.data_ptr())
+        e.set_debug(dt.data_ptr())
         e.engine.launch_one(e.rounds_issued - 1, 0, e._stream())
-        e.engine.set_debug(da.data_ptr())
+        e.set_debug(da.data_ptr())
         e.engine.launch_one(e.rounds_issued - 1, 1, e._stream())
         e.stream.synchronize()
-        e.engine.set_debug(0)
+        e.set_debug(0)
         t = dt.view(nb, 16).cpu().numpy().astype(np.int64)
         a = da.view(-1, 16).cpu().numpy().astype(np.int64)[1:nadam]
         gaps.append((a[:, 0].min() - t[:, 15].max()) * 10 / 1000)
