@@ -339,7 +339,15 @@ def main(argv=None):
                 "lagged-eval+late-fold" if e.engine.late_fold else
                 "lagged-eval" if e.engine.lagged else "classic")
 
-    design = {"aggregation": eng.aggregation,
+    def exchange(e) -> str:
+        """Weight-chunk protocol of the Adam-fused exchange: 'll' (every rank pushes every value to
+        every rank), 'rsag' (reduce-scatter + all-gather on the LL ring), 'pull' (publish / wait /
+        pull); 'none' without an in-kernel exchange."""
+        if e._peer is None or not e.engine.adam_exchange:
+            return "none"
+        return "rsag" if e._peer.uses_rsag else ("ll" if e._peer.uses_ll else "pull")
+
+    design = {"aggregation": eng.aggregation, "exchange": exchange(eng),
               "round_design": round_design(eng),
               "rows_per_block": eng.R, "plain_fwd": bool(eng.layout.get("plain_fwd", False)),
               "split_score": bool(eng.layout.get("split_score", False)),
@@ -400,6 +408,7 @@ def main(argv=None):
                        "data_plane": design["aggregation"],
                        "adam_grid": design["adam_grid"],
                        "round_design": design["round_design"],
+                       "exchange": design["exchange"],
                        "rccl_env": comm.rccl_env,
                        "peer_timeout_s": design["peer_timeout_s"],
                        "rows_per_client": a.rows_per_client or reference_rows(a.total_rows, N, 0),
@@ -459,7 +468,9 @@ def main(argv=None):
     if N > 1 and design["aggregation"].startswith("xgmi") and not a.no_plane_companions and not emit.done:
         planes = {}
         try:
-            for name, env, lagged in (("ll_pull", {"FEDMI_PEER_LL": "0"}, True), ("classic", {}, False)):
+            for name, env, lagged in (("ll_pull", {"FEDMI_PEER_LL": "0"}, True),
+                                      ("rsag", {"FEDMI_PEER_RSAG": "1"}, True),
+                                      ("classic", {}, False)):
                 emit.stage = f"plane_companions.{name}"
                 old = {k: os.environ.get(k) for k in env}
                 os.environ.update(env)
@@ -468,6 +479,7 @@ def main(argv=None):
                                                      lagged_eval=lagged)
                     planes[name] = {"us_per_round": dtc / a.steps * 1e6, "value": rows_total * a.steps / dtc,
                                     "round_design": round_design(engc), "data_plane": engc.aggregation,
+                                    "exchange": exchange(engc),
                                     "env": env, "kernel_trace_us": trc,
                                     "replicas_consistent": check_replicas(comm, [engc.global_flat()])}
                     del engc

@@ -68,12 +68,64 @@ fl_adam_ll_grid_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restri
     }
 }
 
+// Reduce-scatter + all-gather weight chunks (FEDMI_PEER_RSAG=1, PeerArgs::rsag): the LL kernels'
+// body with peer_rsag in place of the all-to-all push (bit-identical sums), full and virtual grid.
+__global__ void __launch_bounds__(ADAM_WAVES * 64)
+fl_adam_rsag_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
+                    const float* __restrict__ anchor, float* __restrict__ comm, const FLState* __restrict__ st,
+                    int local_step, MLPDescB e, int pack, FLState* __restrict__ st_out, int fold, int tail_a,
+                    int fold_mask, PeerArgs pa, int xchg, int afold) {
+#define ADAM_PA_LL true
+#define ADAM_PA_RSAG true
+#include "fl_adam_body.inc"
+#undef ADAM_PA_RSAG
+#undef ADAM_PA_LL
+}
+
+__device__ __forceinline__ void fl_adam_rsag_vblock(const int adam_blk, const MLPDesc& d, const FLConfig& c,
+                                                    const FLBuffers& b, const float* __restrict__ pin,
+                                                    const float* __restrict__ anchor, float* __restrict__ comm,
+                                                    const FLState* __restrict__ st, int local_step,
+                                                    const MLPDescB& e, int pack, FLState* __restrict__ st_out,
+                                                    int fold, int tail_a, int fold_mask, const PeerArgs& pa, int xchg,
+                                                    int afold) {
+#define ADAM_PA_LL true
+#define ADAM_PA_RSAG true
+#define ADAM_BLK adam_blk
+#include "fl_adam_body.inc"
+#undef ADAM_BLK
+#undef ADAM_PA_RSAG
+#undef ADAM_PA_LL
+}
+
+__global__ void __launch_bounds__(ADAM_WAVES * 64)
+fl_adam_rsag_grid_kernel(MLPDesc d, FLConfig c, FLBuffers b, const float* __restrict__ pin,
+                         const float* __restrict__ anchor, float* __restrict__ comm, const FLState* __restrict__ st,
+                         int local_step, MLPDescB e, int pack, FLState* __restrict__ st_out, int fold, int tail_a,
+                         int fold_mask, PeerArgs pa, int xchg, int afold, int n_vblocks) {
+    for (int vb = blockIdx.x; vb < n_vblocks; vb += gridDim.x) {
+        fl_adam_rsag_vblock(vb, d, c, b, pin, anchor, comm, st, local_step, e, pack, st_out, fold, tail_a, fold_mask,
+                            pa, xchg, afold);
+        __syncthreads();
+    }
+}
+
 hipError_t fl_launch_adam_ll(const MLPDesc& d, const FLConfig& c, const FLBuffers& b, const float* pin,
                              const float* anchor, float* comm, const FLState* st, int local_step, const MLPDescB& e,
                              int pack, FLState* st_out, int fold, int tail_a, int fold_mask, const PeerArgs& pa,
                              int xchg, int afold, hipStream_t s) {
     if (pa.ll == nullptr) return hipErrorInvalidValue;
     const int blocks = (d.P + 63) / 64 + 1;
+    if (pa.rsag) {
+        if (pa.adam_grid > 0 && pa.adam_grid < blocks)
+            hipLaunchKernelGGL(fl_adam_rsag_grid_kernel, dim3(pa.adam_grid), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin,
+                               anchor, comm, st, local_step, e, pack, st_out, fold, tail_a, fold_mask, pa, xchg, afold,
+                               blocks);
+        else
+            hipLaunchKernelGGL(fl_adam_rsag_kernel, dim3(blocks), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin, anchor,
+                               comm, st, local_step, e, pack, st_out, fold, tail_a, fold_mask, pa, xchg, afold);
+        return hipGetLastError();
+    }
     if (pa.adam_grid > 0 && pa.adam_grid < blocks) {
         hipLaunchKernelGGL(fl_adam_ll_grid_kernel, dim3(pa.adam_grid), dim3(ADAM_WAVES * 64), 0, s, d, c, b, pin,
                            anchor, comm, st, local_step, e, pack, st_out, fold, tail_a, fold_mask, pa, xchg, afold,

@@ -46,6 +46,7 @@ class PeerAllReduce {
     bool is_open() const { return open_; }
     bool uncached() const { return uncached_; }         // send buffers in uncached memory
     bool uses_ll() const { return use_ll_; }            // LL weight chunks (peer_device.h)
+    bool uses_rsag() const { return use_rsag_; }        // ... by reduce-scatter + all-gather (peer_rsag)
     int adam_grid() const { return adam_grid_; }        // PeerArgs::adam_grid (0 = full Adam grid)
     void set_adam_grid(int g) { adam_grid_ = g < 0 ? 0 : g; }
     void close();
@@ -57,6 +58,7 @@ class PeerAllReduce {
     size_t buf_bytes_ = 0, total_ = 0;
     size_t cf_off_ = 0, ll_off_ = 0, ll_bytes_ = 0;  // chunk-flag table, LL ring (byte offsets)
     bool use_ll_ = false;
+    bool use_rsag_ = false;
     int adam_grid_ = 0;
     char* base_ = nullptr;
     std::vector<char*> mapped_;        // peers' allocations, opened from their IPC handles

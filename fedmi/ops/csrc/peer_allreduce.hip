@@ -88,6 +88,15 @@ __global__ void __launch_bounds__(64) peer_ll_test_kernel(PeerArgs a, unsigned t
     if (valid) out[pos] = v;
 }
 
+// Self-test of the RS+AG chunk exchange (peer_device.h peer_rsag): block c reduces chunk c
+// (owner c % world) of this rank's send buffer with call index `target`.
+__global__ void __launch_bounds__(64) peer_rsag_test_kernel(PeerArgs a, unsigned target, float* out) {
+    const int pos = blockIdx.x * 64 + (int)threadIdx.x;
+    const bool valid = pos < a.n;
+    const float v = peer_rsag(a, blockIdx.x, pos, target, valid, valid ? a.src[a.rank][pos] : 0.f);
+    if (valid) out[pos] = v;
+}
+
 // Self-test payload: exact in fp32 for any summation order (multiples of 1/4 in [-256, 256)).
 __global__ void peer_fill_kernel(float* dst, long long n, int rank, unsigned salt) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -112,6 +121,9 @@ PeerAllReduce::PeerAllReduce(int world, int rank, int device, long long n, doubl
     // FEDMI_PEER_LL=0: weight chunks through publish / wait / pull instead (A/B)
     const char* ll_env = std::getenv("FEDMI_PEER_LL");
     use_ll_ = n_chunks_ > 0 && !(ll_env != nullptr && std::strcmp(ll_env, "0") == 0);
+    // FEDMI_PEER_RSAG=1: LL weight chunks by reduce-scatter + all-gather (peer_device.h peer_rsag)
+    const char* rsag_env = std::getenv("FEDMI_PEER_RSAG");
+    use_rsag_ = use_ll_ && rsag_env != nullptr && std::strcmp(rsag_env, "1") == 0;
     // FEDMI_ADAM_GRID=G: the LL Adam kernel on G workgroups (ranks sharing one GPU; PeerArgs)
     const char* ag_env = std::getenv("FEDMI_ADAM_GRID");
     if (ag_env != nullptr && *ag_env) adam_grid_ = std::max(0, std::atoi(ag_env));
@@ -309,6 +321,7 @@ PeerArgs PeerAllReduce::args(int parity, float* out, long long n_w) const {
     if (open_)
         for (int j = 0; j < world_; ++j) a.err_dst[j] = &reinterpret_cast<PeerCtl*>(peer_base_[j] + 2 * buf_bytes_)->err;
     a.host_abort = host_abort_dev_;
+    a.rsag = use_rsag_ ? 1 : 0;
     return a;
 }
 
@@ -353,7 +366,17 @@ void register_peer(py::module_& m) {
                                     reinterpret_cast<hipStream_t>(stream), a, target, reinterpret_cast<float*>(out));
                  PHIP(hipGetLastError());
              })
+        .def("rsag_test",
+             [](const PeerAllReduce& p, unsigned target, uintptr_t out, uintptr_t stream) {
+                 if (!p.uses_ll()) throw std::runtime_error("rsag_test: no LL ring");
+                 const PeerArgs a = p.args((int)(target & 1), reinterpret_cast<float*>(out));
+                 const int blocks = (int)std::min<long long>(p.n_chunks(), (p.n_floats() + 63) / 64);
+                 hipLaunchKernelGGL(peer_rsag_test_kernel, dim3(blocks), dim3(64), 0,
+                                    reinterpret_cast<hipStream_t>(stream), a, target, reinterpret_cast<float*>(out));
+                 PHIP(hipGetLastError());
+             })
         .def_property_readonly("uses_ll", &PeerAllReduce::uses_ll)
+        .def_property_readonly("uses_rsag", &PeerAllReduce::uses_rsag)
         .def_property("adam_grid", &PeerAllReduce::adam_grid, &PeerAllReduce::set_adam_grid)
         .def("fill_test",
              [](const PeerAllReduce& p, int parity, unsigned salt, uintptr_t stream) {

@@ -93,6 +93,9 @@ struct PeerArgs {
     // abort word (pinned host memory, written by PeerAllReduce::abort; nullptr: none)
     unsigned* err_dst[PEER_MAX_WORLD];
     const unsigned* host_abort;
+    // 1: the Adam-fused weight chunks go through reduce-scatter + all-gather on the LL ring
+    // (peer_rsag below) instead of every rank pushing every value to every rank
+    int rsag;
 };
 
 // All-reduce blocks of a fused evaluation + FedAvg kernel (FL_THREADS = 512 threads each):
@@ -447,5 +450,51 @@ __device__ __forceinline__ float peer_ll_sum(const PeerArgs& a, int pos, unsigne
 #pragma unroll
     for (int k = 1; k < PEER_MAX_WORLD; ++k)
         if (k < a.world) s += v[k];
+    return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// Reduce-scatter + all-gather (RS+AG) exchange of one LL chunk (FEDMI_PEER_RSAG=1).  Chunk c is
+// OWNED by rank c % world: every other rank pushes its value to the owner only (one 8-byte slot,
+// the same ring position as the LL exchange); the owner sums all ranks' values in rank order --
+// the LL exchange's sum, bit for bit -- and pushes the sum, with the call index, into every
+// other rank's slot of source `owner` (unused by the reduce-scatter there: only the owner
+// receives contributions for its chunks).  Per link and round the bytes drop from P slots to
+// 2 P / world (1/4 at world 8), for one more one-way hop: the design the bench's N > 1 runs
+// measure against the LL ring on real xGMI links (bench.py plane_companions).
+// Slot reuse is the LL ring's argument: a rank writes call t + 2 into a slot only after it
+// finished call t + 1, which needs the owner's call t + 1 sum, sent after the owner read call t.
+// ---------------------------------------------------------------------------------------
+// Poll ring slot (source `src`, `pos`) for call `target` (ends early on a reported failure).
+__device__ __forceinline__ float peer_ll_wait1(const PeerArgs& a, int src, int pos, unsigned target, bool active) {
+    if (!active) return 0.f;
+    const unsigned long long* slot = a.ll + peer_ll_slot(a, target, src, pos);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const unsigned long long w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((unsigned)(w >> 32) == target) return __uint_as_float((unsigned)w);
+        if (peer_give_up(a, t0, (unsigned)src)) return 0.f;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+__device__ __forceinline__ float peer_rsag(const PeerArgs& a, int chunk, int pos, unsigned target, bool active,
+                                           float v) {
+    const int owner = chunk % a.world;
+    const size_t slot = peer_ll_slot(a, target, a.rank, pos);
+    if (a.rank != owner) {
+        if (active)
+            __hip_atomic_store(a.ll_dst[owner] + slot, ((unsigned long long)target << 32) | __float_as_uint(v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return peer_ll_wait1(a, owner, pos, target, active);
+    }
+    if (active)
+        __hip_atomic_store(a.ll + slot, ((unsigned long long)target << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    const float s = peer_ll_sum(a, pos, target, active);
+    if (active) {
+        const unsigned long long w = ((unsigned long long)target << 32) | __float_as_uint(s);
+        for (int k = 0; k < a.world; ++k)
+            if (k != owner) __hip_atomic_store(a.ll_dst[k] + slot, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     return s;
 }

@@ -75,6 +75,17 @@ def selftest(h, comm, device, calls: int = 4, timeout_s: float = 10.0) -> bool:
                 got = out.cpu().numpy()[:m]
                 expect = sum(fill_values(n, r, salt) for r in range(comm.size)).astype(np.float32)[:m]
                 ok = ok and bool(np.array_equal(got, expect))
+            # RS+AG weight chunks (peer_device.h peer_rsag): owner sums, then pushes the sums back
+            if bool(getattr(h, "uses_rsag", False)):
+                for k in range(2):
+                    salt, target = 4000 + k, 5 + k
+                    out.zero_()
+                    h.fill_test(target & 1, salt, s.cuda_stream)
+                    comm.Barrier()
+                    h.rsag_test(target, out.data_ptr(), s.cuda_stream)
+                    got = out.cpu().numpy()[:m]
+                    expect = sum(fill_values(n, r, salt) for r in range(comm.size)).astype(np.float32)[:m]
+                    ok = ok and bool(np.array_equal(got, expect))
     ok = ok and h.error() == 0
     return ok
 

@@ -71,7 +71,8 @@ def test_bench_self_launch_shared_gpu():
     assert tr["launches"]["train"] == tr["launches"]["adam"] == tr["rounds"] and tr["train"] > 0
     pc = rec["plane_companions"]
     assert pc["ll_pull"]["round_design"] == "lagged-eval+adam-fedavg"
-    assert pc["ll_pull"]["env"] == {"FEDMI_PEER_LL": "0"}
+    assert pc["ll_pull"]["env"] == {"FEDMI_PEER_LL": "0"} and pc["ll_pull"]["exchange"] == "pull"
+    assert pc["rsag"]["exchange"] == "rsag" and rec["config"]["exchange"] == "ll"
     assert pc["classic"]["round_design"] == "classic" and pc["classic"]["data_plane"] == "xgmi-oneshot"
     assert all(v["replicas_consistent"] is True and v["us_per_round"] > 0 for v in pc.values())
 

@@ -180,12 +180,23 @@ def _worker4(rank, world, port, q):
             a0 = _run_engine(comm, True, "bf16", X, y, flat, hidden=hidden, expect_ll=False)
         finally:
             del os.environ["FEDMI_PEER_LL"]
+        # ... and by reduce-scatter + all-gather on the LL ring (FEDMI_PEER_RSAG=1)
+        os.environ["FEDMI_PEER_RSAG"] = "1"
+        try:
+            h = make_peer_allreduce(comm, 3001, dev, timeout_s=30.0, n_chunks=48)   # + the RS+AG self-test
+            ok = ok and h is not None and bool(h.uses_rsag)
+            comm.Barrier()
+            if h is not None:
+                h.close()
+            ar = _run_engine(comm, True, "bf16", X, y, flat, hidden=hidden, expect_ll=True)
+        finally:
+            del os.environ["FEDMI_PEER_RSAG"]
         # classic rounds over the standalone peer kernel: the same rank-order sums (gloo's
         # 4-rank reduction order differs, so the host path is not a bitwise reference here)
         b = _run_engine(comm, True, "bf16", X, y, flat, True, False, hidden=hidden)
         torch.cuda.synchronize()
         comm.Barrier()
-        q.put((rank, (ok, a, b, a0), None))
+        q.put((rank, (ok, a, b, a0, ar), None))
         comm.close()
     except Exception:  # noqa: BLE001
         import traceback
@@ -213,8 +224,11 @@ def test_peer_many_ranks_lagged_adam_exchange(world):
         p.join(timeout=30)
     for rank, res, err in out:
         assert err is None, f"rank {rank}:\n{err}"
-        ok, (wa, ha, ca), (wb, hb, cb), (w0, h0, c0) = res
+        ok, (wa, ha, ca), (wb, hb, cb), (w0, h0, c0), (wr, hr, cr) = res
         assert ok
+        np.testing.assert_array_equal(wr, wb)
+        np.testing.assert_array_equal(hr["global"], hb["global"])
+        np.testing.assert_array_equal(cr, cb)
         np.testing.assert_array_equal(wa, wb)
         np.testing.assert_array_equal(w0, wb)
         np.testing.assert_array_equal(h0["global"], hb["global"])
@@ -235,7 +249,8 @@ def _run_prod(comm, X, y, flat, n_total, lagged: bool, rounds: int):
     e = HipRoundEngine(X, y, 2, cfg, comm, flat, n_total=n_total)
     info = {"adam_exchange": bool(e.engine.adam_exchange), "lagged": bool(e.engine.lagged),
             "adam_grid": int(e._peer.adam_grid) if e._peer is not None else -1,
-            "uses_ll": bool(e._peer.uses_ll) if e._peer is not None else False, "R": e.R}
+            "uses_ll": bool(e._peer.uses_ll) if e._peer is not None else False,
+            "uses_rsag": bool(e._peer.uses_rsag) if e._peer is not None else False, "R": e.R}
     e.run(rounds)
     e.sync_history()
     out = (e.global_flat(), e.history(), e.local_flat(), info)
@@ -266,6 +281,12 @@ def _worker_prod(rank, world, port, rounds, q):
             res["pull"] = _run_prod(comm, X, y, flat, 8000, True, rounds)
         finally:
             del os.environ["FEDMI_PEER_LL"]
+        gc.collect()
+        os.environ["FEDMI_PEER_RSAG"] = "1"                 # reduce-scatter + all-gather weight chunks
+        try:
+            res["rsag"] = _run_prod(comm, X, y, flat, 8000, True, rounds)
+        finally:
+            del os.environ["FEDMI_PEER_RSAG"]
         gc.collect()
         res["classic"] = _run_prod(comm, X, y, flat, 8000, False, rounds)   # standalone peer kernel
         res["rccl_created"] = comm.native is not None
@@ -301,12 +322,14 @@ def test_peer_world8_production_shape_adam_exchange():
     for rank, res, err in out:
         assert err is None, f"rank {rank}:\n{err}"
         (wl, hl, ll, il), (wp, hp, lp, ip), (wc, hc, lc, ic) = res["ll"], res["pull"], res["classic"]
-        assert il["adam_exchange"] and il["uses_ll"] and il["adam_grid"] == 16, il
+        (wr, hr, lr, ir) = res["rsag"]
+        assert il["adam_exchange"] and il["uses_ll"] and not il["uses_rsag"] and il["adam_grid"] == 16, il
         assert ip["adam_exchange"] and not ip["uses_ll"] and ip["adam_grid"] == 16, ip  # fl_adam_grid_kernel
+        assert ir["adam_exchange"] and ir["uses_rsag"] and ir["adam_grid"] == 16, ir    # fl_adam_rsag_grid_kernel
         assert not ic["adam_exchange"] and not ic["lagged"], ic
         assert not res["rccl_created"]
         assert hl["rounds_run"] == hc["rounds_run"] == rounds and hl["stop_round"] < 0
-        for name, (w, h, lo) in (("ll", (wl, hl, ll)), ("pull", (wp, hp, lp))):
+        for name, (w, h, lo) in (("ll", (wl, hl, ll)), ("pull", (wp, hp, lp)), ("rsag", (wr, hr, lr))):
             np.testing.assert_array_equal(w, wc, err_msg=f"rank {rank} {name}: global weights")
             np.testing.assert_array_equal(lo, lc, err_msg=f"rank {rank} {name}: local weights")
             np.testing.assert_array_equal(h["global"], hc["global"], err_msg=f"rank {rank} {name}: metrics")
