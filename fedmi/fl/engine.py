@@ -633,6 +633,17 @@ class HipRoundEngine(RoundEngineBase):
             self._native_comm = comm.rccl_or_host() if hasattr(comm, "rccl_or_host") else comm.rccl()
         self._graph_ready = False
 
+    def __del__(self):
+        # the xGMI communicator's buffers are read by the peers: never freed with the engine, but
+        # retired until the next collective set-up (fedmi.parallel.peer.retire)
+        peer = getattr(self, "_peer", None)
+        if peer is not None:
+            try:
+                from ..parallel.peer import retire
+                retire(peer)
+            except Exception:  # noqa: BLE001 -- interpreter shutdown
+                pass
+
     def slab_partials(self) -> torch.Tensor:
         """The last train kernel's per-workgroup gradient partials as [n_slabs, P] (a copy of the
         slab rows, fp32 or fp16, in dense-parameter order).  fp16 partials are sums of the

@@ -164,6 +164,28 @@ def abort_all(wait_s: float = 1.0) -> int:
     return sum(told)
 
 
+# Communicators whose engine is gone.  A rank's send buffers, flags and ring are READ BY ITS
+# PEERS, so a rank must not free them when its own engine is dropped: a slower peer may still be
+# pulling its last round's tails (freed memory reused by the next allocation reads as zeros there).
+# retire() parks the communicator; the next collective set-up frees it once every rank has
+# arrived there with its device work drained (make_peer_allreduce), i.e. past its last read.
+_RETIRED = []
+
+
+def retire(h) -> None:
+    """Park a communicator whose owner is done with it (see _RETIRED); no collective needed."""
+    if h is not None:
+        _RETIRED.append(h)
+
+
+def _free_retired() -> None:
+    while _RETIRED:
+        try:
+            _RETIRED.pop().close()
+        except Exception:  # noqa: BLE001 -- best effort: the process keeps working either way
+            pass
+
+
 def _test_fail_ranks() -> set:
     """Test knob ``FEDMI_TEST_PEER_FAIL=1,3``: the peer set-up fails on these ranks (exercises
     the agreed fallback of every rank to the next data plane)."""
@@ -182,6 +204,9 @@ def make_peer_allreduce(comm, n_floats: int, device, timeout_s: Optional[float] 
         return None
     timeout_s = peer_timeout_s(timeout_s)
     m = native()
+    # this rank's device work (incl. reads of retired peers' buffers) is done before it reports
+    # in below; once every rank has reported, every retired communicator is past its last use
+    torch.cuda.synchronize(torch.device(device))
     h, why = None, ""
     try:
         if comm.rank in _test_fail_ranks():
@@ -192,6 +217,7 @@ def make_peer_allreduce(comm, n_floats: int, device, timeout_s: Optional[float] 
     except Exception as e:  # noqa: BLE001 -- reported, and every rank falls back together
         handle, why = None, f"rank {comm.rank}: {e}"
     gathered = comm.allgather((handle, device_key(device)))
+    _free_retired()
     handles = [g[0] for g in gathered]
     ok = all(x is not None for x in handles)
     if ok and n_chunks > 0:

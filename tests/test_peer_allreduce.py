@@ -231,7 +231,11 @@ def test_peer_many_ranks_lagged_adam_exchange(world):
         np.testing.assert_array_equal(cr, cb)
         np.testing.assert_array_equal(wa, wb)
         np.testing.assert_array_equal(w0, wb)
-        np.testing.assert_array_equal(h0["global"], hb["global"])
+        bad = np.flatnonzero((h0["global"] != hb["global"]).any(axis=1))
+        np.testing.assert_array_equal(h0["global"], hb["global"], err_msg=(
+            f"rank {rank}: pull-exchange metrics differ at rounds {bad.tolist()}: "
+            f"pull {h0['global'][bad].tolist()} classic {hb['global'][bad].tolist()}; per-rank pull "
+            f"{np.asarray(h0['per_rank'])[bad].tolist()} classic {np.asarray(hb['per_rank'])[bad].tolist()}"))
         np.testing.assert_array_equal(c0, cb)
         np.testing.assert_array_equal(ha["global"], hb["global"])
         np.testing.assert_array_equal(ha["per_rank"], hb["per_rank"])
