@@ -7,8 +7,9 @@ local contiguous shard, local metrics, uniform FedAvg of ``coefs_ + intercepts_`
 global metrics; at the end per-layer mean/std of the global weights.  Data:
 ``balanced_income_data.csv`` / ``income`` with ``StandardScaler(with_mean=False)`` (S:184).
 
-The estimator is fedmi's ``MLPClassifier`` (fp32 HIP trainer on a GPU, float64 numpy on a
-CPU).  The reference's limitation is kept by default (``fit`` re-initialises, so the
+The estimator is fedmi's ``MLPClassifier``: on a GPU the native HIP minibatch trainer in
+float64 by default (f64 MFMA, scikit-learn's numerics; ``--dtype float32`` for the fp32
+kernels), on a CPU the float64 numpy backend.  The reference's limitation is kept by default (``fit`` re-initialises, so the
 averaged weights are discarded: SURVEY Q8); ``--warm-start`` fixes it.  FedAvg is one
 in-place all-reduce of the flat parameter vector (uniform mean, S:114-117), and
 the pooled metrics come from all-reduced confusion matrices instead of gathered

@@ -27,6 +27,20 @@ static_assert(ADAM_CANON % ADAM_WAVES == 0, "ADAM_WAVES must divide 16");
 #define ADAM_WDEPTH 2
 #endif
 typedef _Float16 fl_half8 __attribute__((ext_vector_type(8)));
+#ifdef FL_SLAB_AUX
+// A/B builds: a 16-byte slab load with the cache-policy bits FL_SLAB_AUX (fl_adam_body.inc)
+template <typename VT>
+__device__ __forceinline__ VT fl_slab_ld_aux(const float* slab, const VT* p) {
+    // uniform resource (the slab base), per-lane byte offset
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(slab), (short)0, 0x7fffffff, 0x00020000);
+    const int off = (int)(reinterpret_cast<const char*>(p) - reinterpret_cast<const char*>(slab));
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, FL_SLAB_AUX);
+    VT out;
+    __builtin_memcpy(&out, &v, 16);
+    return out;
+}
+#endif
 typedef float fl_float4v __attribute__((ext_vector_type(4)));
 // bf16 mode: parameter -> packed LDS-layout image(s).  A weight is stored as its bf16 hi part
 // and, `wlo_delta` bytes further, its lo part bf16(p - hi) (split-bf16 forward, fl_common.h);
