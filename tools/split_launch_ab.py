@@ -23,7 +23,8 @@ def main():
     ap.add_argument("--rows", type=int, default=8000)
     ap.add_argument("--reps", type=int, default=12)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--splits", nargs="+", default=["20", "2,18", "4,16", "2,2,16", "6,14"])
+    ap.add_argument("--splits", nargs="+", default=["20", "e2,18", "e1,e1,18", "e4,16", "2,18"],
+                    help="comma-separated parts; 'eN' = N rounds launched eagerly (no graph)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -37,13 +38,15 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     variants = {}
     for sp in a.splits:
-        parts = [int(x) for x in sp.split(",")]
-        assert sum(parts) == a.steps and all(p % 2 == 0 for p in parts), sp
-        cfg = EngineConfig(max_rounds=total, early_stop=True, patience=total + 1, graph_rounds=parts[-1],
+        parts = sp.split(",")
+        n = [int(x.lstrip("e")) for x in parts]
+        assert sum(n) == a.steps and all(int(x) % 2 == 0 for x in parts if not x.startswith("e")), sp
+        gsz = sorted({int(x) for x in parts if not x.startswith("e")})
+        cfg = EngineConfig(max_rounds=total, early_stop=True, patience=total + 1, graph_rounds=gsz[-1],
                            dtype="bf16")
         e = HipRoundEngine(X, y, 2, cfg, None, init_flat([14, 50, 200, 2], 0), n_total=a.rows, stream=stream)
         e.run(5, check_every=5)
-        for g in sorted(set(parts)):          # capture + instantiate + one replay of every graph size
+        for g in gsz:                         # capture + instantiate + one replay of every graph size
             e.prime_graph(g)
         variants[sp] = (e, parts)
     s = stream.cuda_stream
@@ -52,9 +55,15 @@ def main():
         for sp, (e, parts) in variants.items():
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
-            for g in parts:
-                e.engine.capture(g, s, None)    # selects the cached graph (no capture)
-                e.engine.replay(s)
+            r = e.rounds_issued
+            for x in parts:
+                if x.startswith("e"):           # eager launches from C++ (no graph)
+                    e.engine.run(r, int(x[1:]), s, None, close=False)
+                    r += int(x[1:])
+                else:
+                    e.engine.capture(int(x), s, None)    # selects the cached graph (no capture)
+                    e.engine.replay(s)
+                    r += int(x)
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
             e.rounds_issued += a.steps
