@@ -374,6 +374,7 @@ def _fit_hip_prepare(ests: List[MLPClassifier], X, codes, dims, perms, increment
     tr = trainer(list(dims), T, cfg, {k: v.data_ptr() for k, v in bufs_t.items()})
     for e in ests:
         e._hip_fused = bool(tr.fused)   # two-kernel minibatch step (mlp_fused_f64.hip) ran
+        e._hip_split = int(getattr(tr, "split", 1))   # column slices of the row pass (skf_cs_*; 1 = none)
     stream = torch.cuda.Stream(device=dev)
     stream.wait_stream(torch.cuda.current_stream(dev))
     tr.prepare(stream.cuda_stream)      # the epoch graph, captured here (see _HipJob)

@@ -74,7 +74,16 @@ struct SkfArgs {
     const double* zero;                     // one 0.0 in device memory (branch-free masked loads)
     double* wt;                             // optional [T][P]: each layer's weights transposed [K][N] (kept by
                                             // the Adam epilogue; read by the forward), nullptr: none
+    // Column-split row pass (mlp_fused_f64.hip skf_cs_*): split > 1 slices the last hidden layer's
+    // output columns (cw each) over `split` workgroups per row block; zpart [T][split][Bmax][C] and
+    // bpart [T][split][Bmax][maxw] carry the slices' partial logits / input gradients
+    int split, cw;
+    double* zpart;
+    double* bpart;
+    int* arrive;                            // [T][row blocks] arrival tickets of skf_cs_bwd (zeroed; L == 3)
 };
+// Column slice width and count for the last hidden layer of a fused job (split 1: no split).
+void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw);
 bool skf_supported(const SkfArgs& a);
 size_t skf_lds_bytes(const SkfArgs& a);
 hipError_t skf_prepare(const SkfArgs& a);

@@ -24,6 +24,7 @@
 // differ from the layered path and from BLAS, so results agree with the float64 numpy oracle
 // to ~1e-12 per step, not bitwise (tests/test_sklearn_estimator.py: loss curve rtol 1e-9).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <mutex>
 #include <math.h>
 #include <stdint.h>
@@ -38,7 +39,7 @@ typedef double skf_f64x4 __attribute__((ext_vector_type(4)));
 #define SKF_NARROW 4       // output layers at most this wide run on the VALU
 static_assert(SKF_WAVES == SKF_RB, "skf_fwd_narrow: one wave per row");
 
-__device__ __forceinline__ int skf_np(int n) { return (n + 15) & ~15; }
+__host__ __device__ __forceinline__ int skf_np(int n) { return (n + 15) & ~15; }
 // LDS row stride (doubles) of a buffer with np (multiple of 16) columns: np = 2 (mod 32), so the
 // MFMA operand reads (16 rows x 4 consecutive columns per wave) hit distinct banks
 __host__ __device__ __forceinline__ int skf_ld(int np) { return np + 2 + ((np & 16) ? 16 : 0); }
@@ -89,12 +90,16 @@ __device__ __forceinline__ double skf_wave_sum(double v) {
 // selected after the load) and every MFMA runs (a zero weight operand, an in-range activation
 // column), so the compiler keeps the next chunk's loads in flight across the current chunk's
 // MFMAs -- with predicated loads / MFMAs it waited for ALL loads before every MFMA.
+// Column-split row pass (skf_cs_* below) extras: `ldwt` = row stride of WT (the full layer's N when
+// W / WT / bias point at a slice of its output columns; 0 = N); `raw` (BWD) = store the product
+// itself instead of masking the activation in dst (a partial over a slice of N, summed later).
 template <bool FWD, int KB>
 __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int ld_s, double* __restrict__ dst,
                                              int ld_d, const double* __restrict__ W, const double* __restrict__ bias,
                                              int K, int N, bool relu, double* __restrict__ red, int wave, int lane,
                                              const double* __restrict__ zero, const double* __restrict__ WT,
-                                             unsigned long long* dbg = nullptr) {
+                                             unsigned long long* dbg = nullptr, int ldwt = 0, bool raw = false) {
+    if (ldwt <= 0) ldwt = N;
     const int lr = lane & 15, lg = lane >> 4;
     if (dbg != nullptr && threadIdx.x == 0) dbg[0] = __builtin_amdgcn_s_memrealtime();
     const int ntiles = FWD ? (N + 15) >> 4 : (K + 15) >> 4;
@@ -118,7 +123,7 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
             // select would wait for the load right here, prefetch included)
             // FWD reads the transposed copy WT [K][N] when there is one (SkfArgs::wt): 16 consecutive
             // output columns per k-row -- whole cache lines -- instead of 16 rows x 32 bytes
-            const double* q = ok ? (FWD ? (WT != nullptr ? WT + (size_t)kk * N + col : W + (size_t)col * K + kk)
+            const double* q = ok ? (FWD ? (WT != nullptr ? WT + (size_t)kk * ldwt + col : W + (size_t)col * K + kk)
                                         : W + (size_t)kk * K + col)
                                  : zero;
             bw[i] = *q;
@@ -151,6 +156,9 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
                 if (relu) v = v > 0.0 ? v : 0.0;
                 dst[(lg + 4 * j) * ld_d + col] = col < N ? v : 0.0;
             }
+        } else if (raw) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dst[(lg + 4 * j) * ld_d + col] = col < K ? acc[j] : 0.0;
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -211,14 +219,14 @@ __device__ __forceinline__ void skf_layer(const double* __restrict__ src, int ld
                                           const double* __restrict__ W, const double* __restrict__ bias, int K, int N,
                                           bool relu, double* __restrict__ red, int wave, int lane,
                                           const double* __restrict__ zero, const double* __restrict__ WT,
-                                          unsigned long long* dbg = nullptr) {
+                                          unsigned long long* dbg = nullptr, int ldwt = 0, bool raw = false) {
     const int steps = FWD ? (K + 3) >> 2 : (N + 3) >> 2;
     if (steps <= 4)
-        skf_layer_kb<FWD, 4>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg);
+        skf_layer_kb<FWD, 4>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw);
     else if (steps <= 8)
-        skf_layer_kb<FWD, 8>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg);
+        skf_layer_kb<FWD, 8>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw);
     else
-        skf_layer_kb<FWD, SKF_KB>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg);
+        skf_layer_kb<FWD, SKF_KB>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw);
 }
 
 // Narrow output layer (N <= SKF_NARROW) on the VALU, weights staged in LDS (Ws [N][K], bias at
@@ -386,6 +394,395 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
     SKF_STAMP(12);
 }
 
+// ---------------------------------------------------------------------------------------
+// Column-split row pass (SkfArgs::split = S > 1).  skf_rowpass runs one 16-row block on ONE CU and
+// is bound by that CU's float64 MFMA pipes (MFMA busy 67 %): every row block streams and multiplies
+// the whole weight set alone, so a minibatch of 200 rows uses 13 CUs.  With a narrow head (binary
+// logistic / <= 4 classes, sklearn's [S] / [H] jobs) the last hidden layer's output columns are
+// sliced over S workgroups per row block -- S x more CUs for the widest products -- in three
+// kernels (no in-kernel waits across workgroups, so any number of trials can queue):
+//   skf_cs_fwd   (row block x slice x trial)  gather, the layers before the split layer (every slice
+//                recomputes them; slice 0 stores them), the split layer's forward for its columns,
+//                and the slice's partial logits = a[:, slice] . W_head[:, slice]^T -> zpart
+//   skf_cs_bwd   (row block x slice x trial)  logits = sum of the S partials in slice order + bias ->
+//                loss head -> the slice's delta (head delta . W_head, ReLU mask) -> the slice's
+//                partial input gradient of the split layer (raw product) -> bpart
+//   skf_cs_tail  (row block x trial)          delta below the split layer = sum of the S partials
+//                in slice order, masked; the remaining layers' backward as in skf_rowpass
+// Every sum is in a fixed order (deterministic); the orders differ from skf_rowpass's, so the two
+// agree to float64 rounding, not bitwise.
+// ---------------------------------------------------------------------------------------
+void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw) {
+    *split = 1;
+    *cw = 0;
+    if (a.L < 2 || a.dims[a.L] > SKF_NARROW) return;
+    const int hk = a.dims[a.L - 1];
+    // default: slices of >= 64 columns, and about one workgroup per CU over all row blocks and
+    // trials (more queue behind each other: (50, 400) x 9 trials 65 us per step at 2 slices, 100 at 7;
+    // x 1 trial 39 us at 7, 58 unsplit -- profiles/sk_split_r6.log)
+    const int nrb = (a.Bmax + SKF_RB - 1) / SKF_RB;  // row blocks of a full minibatch
+    int S = want;
+    if (S <= 0) {
+        const int by_cols = hk >= 96 ? (hk + 63) / 64 : 1;
+        const int by_cus = 256 / std::max(1, nrb * a.T);
+        S = std::min(by_cols, std::max(1, by_cus));
+    }
+    S = S < 1 ? 1 : (S > 16 ? 16 : S);
+    if (S <= 1) return;
+    const int w = (((hk + S - 1) / S) + 15) & ~15;  // slices of whole 16-column tiles
+    *cw = w;
+    *split = (hk + w - 1) / w;
+    if (*split <= 1) *cw = 0;
+}
+
+// Weights a split kernel stages in LDS at its start, in flight with its other first loads (a layer's
+// weights streamed from memory are one more dependent round trip each): skf_cs_fwd the layers
+// below the split layer + the split layer's slice (+ biases), skf_cs_bwd the split layer's slice
+// (dgrad operand).  Only when they fit beside the kernel's buffers (160 KB of LDS).
+__host__ __device__ __forceinline__ int skf_cs_fwd_stage_doubles(const SkfArgs& a) {
+    const int ls = a.L - 2;
+    int d = 0;
+    for (int l = 0; l < ls; ++l) d += a.dims[l + 1] * a.dims[l] + a.dims[l + 1];
+    return d + a.cw * a.dims[ls] + a.cw;
+}
+__host__ __device__ __forceinline__ int skf_cs_bwd_stage_doubles(const SkfArgs& a) {
+    return a.L >= 3 ? a.cw * a.dims[a.L - 2] : 0;
+}
+__host__ __device__ __forceinline__ size_t skf_cs_bwd_base_doubles(const SkfArgs& a) {
+    const int ls = a.L - 2;
+    return (size_t)SKF_RB * skf_ld(skf_np(a.cw)) + (size_t)SKF_RB * skf_ld(skf_np(a.dims[ls])) + SKF_RED_DOUBLES +
+           (size_t)a.dims[a.L] * (a.cw + 1);
+}
+#ifndef SKF_STAGE_FWD  // A/B builds: -DSKF_STAGE_FWD=1 / -DSKF_STAGE_BWD=1 stage the weights (measured slower: profiles/sk_split_r6.log)
+#define SKF_STAGE_FWD 0
+#endif
+#ifndef SKF_STAGE_BWD
+#define SKF_STAGE_BWD 0
+#endif
+__host__ __device__ __forceinline__ bool skf_cs_fwd_staged(const SkfArgs& a, size_t base_doubles) {
+    return SKF_STAGE_FWD && (base_doubles + skf_cs_fwd_stage_doubles(a)) * sizeof(double) <= 160 * 1024;
+}
+__host__ __device__ __forceinline__ bool skf_cs_bwd_staged(const SkfArgs& a) {
+    return SKF_STAGE_BWD && (skf_cs_bwd_base_doubles(a) + skf_cs_bwd_stage_doubles(a)) * sizeof(double) <= 160 * 1024;
+}
+static size_t skf_cs_fwd_lds(const SkfArgs& a) {
+    const size_t base = skf_lds_bytes(a) / sizeof(double);
+    return (base + (skf_cs_fwd_staged(a, base) ? skf_cs_fwd_stage_doubles(a) : 0)) * sizeof(double);
+}
+
+// LDS of skf_cs_bwd (doubles): the slice's activations / delta [16][ld(cw)], the raw input-gradient
+// partial [16][ld(K)], the k-split partials, and the slice's head weights + bias
+static size_t skf_cs_bwd_lds(const SkfArgs& a) {
+    return (skf_cs_bwd_base_doubles(a) + (skf_cs_bwd_staged(a) ? skf_cs_bwd_stage_doubles(a) : 0)) * sizeof(double);
+}
+
+__global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
+    extern __shared__ double lds[];
+    const int t = blockIdx.z, sl = blockIdx.y, rb = blockIdx.x;
+    if (a.active[t] == 0) return;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
+    const int ls = a.L - 2, Kl = a.dims[ls], Nl = a.dims[ls + 1], C = a.dims[a.L];
+    const int c0 = sl * a.cw, nc = min(a.cw, Nl - c0);
+    if (rb == 0 && sl == 0 && threadIdx.x == 0) a.step[t] += 1;  // this minibatch's Adam step
+    const double* P = a.params + (size_t)t * a.P;
+    auto ldof = [&](int l) { return skf_ld(skf_np(a.dims[l])); };
+    auto bufp = [&](int l) {
+        int o = 0;
+        for (int i = 0; i < l; ++i) o += ldof(i) * SKF_RB;
+        return lds + o;
+    };
+    double* red = bufp(a.L + 1);
+    double* wnar = red + SKF_RED_DOUBLES;  // the slice's head weights [C][nc]
+    const double* Wh = P + a.w_off[a.L - 1];
+    for (int e = threadIdx.x; e < C * nc; e += blockDim.x) {
+        const int c = e / nc, j = e - c * nc;
+        wnar[e] = Wh[(size_t)c * Nl + c0 + j];
+    }
+    // staged weights [W_0 | b_0 | ... | W_ls slice | b_ls slice], dense [N][K] rows (LDS): their
+    // loads are in flight with the gather's
+    double* wst = wnar + skf_narrow_doubles(a);
+    const size_t base_d = (size_t)(wst - lds);
+    const bool staged = skf_cs_fwd_staged(a, base_d);
+    int w_lds[SKF_MAXL], b_lds[SKF_MAXL];
+    {
+        int o = 0;
+        for (int l = 0; l <= ls; ++l) {
+            const int N = l < ls ? a.dims[l + 1] : nc, K = a.dims[l];
+            w_lds[l] = o;
+            b_lds[l] = o + N * K;
+            if (staged) {
+                const double* Wg = P + a.w_off[l] + (l < ls ? 0 : (size_t)c0 * Kl);
+                const double* bg = P + a.b_off[l] + (l < ls ? 0 : c0);
+                for (int e = threadIdx.x; e < N * K; e += blockDim.x) wst[o + e] = Wg[e];
+                for (int e = threadIdx.x; e < N; e += blockDim.x) wst[o + N * K + e] = bg[e];
+            }
+            o += N * K + (l < ls ? N : a.cw);
+        }
+    }
+    const int F = a.dims[0], fp = skf_np(F);
+    const int* perm = a.perms + (size_t)(*a.epoch_ctr) * a.n_perm + a.off + r0;
+    double* xg = a.xg + ((size_t)t * a.Bmax + r0) * F;
+    for (int e = threadIdx.x; e < SKF_RB * fp; e += blockDim.x) {
+        const int r = e / fp, f = e - r * fp;
+        double v = 0.0;
+        if (r < nr && f < F) {
+            v = a.X[(size_t)perm[r] * F + f];
+            if (sl == 0) skf_st(&xg[(size_t)r * F + f], v, a.wthru);
+        }
+        bufp(0)[r * ldof(0) + f] = v;
+    }
+    skf_lds_barrier();
+    for (int l = 0; l < ls; ++l) {  // the layers below the split layer, whole (slice 0 stores them)
+        const int K = a.dims[l], N = a.dims[l + 1];
+        if (staged)
+            skf_layer<true>(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), wst + w_lds[l], wst + b_lds[l], K, N, true, red,
+                            wave, lane, a.zero, nullptr);
+        else
+            skf_layer<true>(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), P + a.w_off[l], P + a.b_off[l], K, N, true,
+                            red, wave, lane, a.zero, a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[l] : nullptr);
+        skf_lds_barrier();
+        if (sl == 0) {
+            double* ag = a.acts + (((size_t)l * a.T + t) * a.Bmax + r0) * a.maxw;
+            for (int e = threadIdx.x; e < nr * N; e += blockDim.x) {
+                const int r = e / N, c = e - r * N;
+                skf_st(&ag[(size_t)r * a.maxw + c], bufp(l + 1)[r * ldof(l + 1) + c], a.wthru);
+            }
+        }
+    }
+    // the split layer's forward for output columns [c0, c0 + nc)
+    if (staged)
+        skf_layer<true>(bufp(ls), ldof(ls), bufp(ls + 1) + c0, ldof(ls + 1), wst + w_lds[ls], wst + b_lds[ls], Kl, nc,
+                        true, red, wave, lane, a.zero, nullptr);
+    else
+        skf_layer<true>(bufp(ls), ldof(ls), bufp(ls + 1) + c0, ldof(ls + 1), P + a.w_off[ls] + (size_t)c0 * Kl,
+                        P + a.b_off[ls] + c0, Kl, nc, true, red, wave, lane, a.zero,
+                        a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[ls] + c0 : nullptr, nullptr, Nl);
+    skf_lds_barrier();
+    {
+        double* ag = a.acts + (((size_t)ls * a.T + t) * a.Bmax + r0) * a.maxw + c0;
+        for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
+            const int r = e / nc, j = e - r * nc;
+            skf_st(&ag[(size_t)r * a.maxw + j], bufp(ls + 1)[r * ldof(ls + 1) + c0 + j], a.wthru);
+        }
+    }
+    // the slice's partial logits: wave w = row w, lanes over the slice's columns, xor-tree sum
+    {
+        const int r = wave;  // SKF_WAVES == SKF_RB
+        const double* ar = bufp(ls + 1) + r * ldof(ls + 1) + c0;
+        for (int c = 0; c < C; ++c) {
+            double s = 0.0;
+            for (int j = lane; j < nc; j += 64) s += ar[j] * wnar[c * nc + j];
+            s = skf_wave_sum(s);
+            if (lane == 0 && r < nr) a.zpart[(((size_t)t * a.split + sl) * a.Bmax + r0 + r) * C + c] = s;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
+    extern __shared__ double lds[];
+    __shared__ double dz_s[SKF_RB * SKF_NARROW];
+    const int t = blockIdx.z, sl = blockIdx.y, rb = blockIdx.x;
+    if (a.active[t] == 0) return;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
+    const int ls = a.L - 2, Kl = a.dims[ls], Nl = a.dims[ls + 1], C = a.dims[a.L];
+    const int c0 = sl * a.cw, nc = min(a.cw, Nl - c0);
+    const double* P = a.params + (size_t)t * a.P;
+    const int npc = skf_np(a.cw), lda = skf_ld(npc), ldk = skf_ld(skf_np(Kl));
+    double* as = lds;                      // [16][lda]: the slice's activations, then its delta
+    double* part = as + SKF_RB * lda;      // [16][ldk]: raw partial input gradient
+    double* red = part + SKF_RB * ldk;
+    double* wnar = red + SKF_RED_DOUBLES;  // [C][nc] head weights of the slice, then the bias [C]
+    const double* Wh = P + a.w_off[a.L - 1];
+    for (int e = threadIdx.x; e < C * nc; e += blockDim.x) {
+        const int c = e / nc, j = e - c * nc;
+        wnar[e] = Wh[(size_t)c * Nl + c0 + j];
+    }
+    if (threadIdx.x < C) wnar[C * nc + threadIdx.x] = P[a.b_off[a.L - 1] + threadIdx.x];
+    // the split layer's weight slice [nc][Kl] (the dgrad operand), staged with the first loads
+    double* wst = wnar + (size_t)C * (a.cw + 1);
+    const bool staged = ls >= 1 && skf_cs_bwd_staged(a);
+    if (staged) {
+        const double* Wg = P + a.w_off[ls] + (size_t)c0 * Kl;
+        for (int e = threadIdx.x; e < nc * Kl; e += blockDim.x) wst[e] = Wg[e];
+    }
+    const double* ag = a.acts + (((size_t)ls * a.T + t) * a.Bmax + r0) * a.maxw + c0;
+    for (int e = threadIdx.x; e < SKF_RB * npc; e += blockDim.x) {
+        const int r = e / npc, j = e - r * npc;
+        as[r * lda + j] = (r < nr && j < nc) ? ag[(size_t)r * a.maxw + j] : 0.0;
+    }
+    skf_lds_barrier();
+    // loss head on the logits = sum of the slices' partials (slice order) + bias
+    double lrow = 0.0;
+    if (threadIdx.x < SKF_RB) {
+        const int r = threadIdx.x;
+        const double eps = 2.220446049250313e-16;
+        double z[SKF_NARROW];
+        for (int c = 0; c < C; ++c) {
+            double s = 0.0;
+            if (r < nr)
+                for (int q = 0; q < a.split; ++q) s += a.zpart[(((size_t)t * a.split + q) * a.Bmax + r0 + r) * C + c];
+            z[c] = s + wnar[C * nc + c];
+        }
+        if (r >= nr) {
+            for (int c = 0; c < C; ++c) dz_s[r * C + c] = 0.0;
+        } else {
+            const int* perm = a.perms + (size_t)(*a.epoch_ctr) * a.n_perm + a.off + r0;
+            const int yy = a.y[perm[r]];
+            if (a.head == 1) {
+                const double p = 1.0 / (1.0 + exp(-z[0]));
+                const double pc = fmin(fmax(p, eps), 1.0 - eps);
+                lrow = yy ? -log(pc) : -log(1.0 - pc);
+                dz_s[r * C] = (p - (double)yy) * a.inv_rows;
+            } else {
+                double mx = z[0];
+                for (int c = 1; c < C; ++c) mx = fmax(mx, z[c]);
+                double se = 0.0;
+                for (int c = 0; c < C; ++c) se += exp(z[c] - mx);
+                const double py = fmin(fmax(exp(z[yy] - mx) / se, eps), 1.0 - eps);
+                lrow = -log(py);
+                for (int c = 0; c < C; ++c) dz_s[r * C + c] = (exp(z[c] - mx) / se - (c == yy ? 1.0 : 0.0)) * a.inv_rows;
+            }
+        }
+    }
+    if (sl == 0 && wave == 0) {
+        lrow = skf_wave_sum(lrow);
+        if (lane == 0) atomicAdd(&a.loss_acc[t], lrow);
+    }
+    skf_lds_barrier();
+    if (sl == 0) {  // the head delta: the head's wgrad operand
+        double* dg = a.deltas + (((size_t)(a.L - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
+        for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
+            const int r = e / C, c = e - r * C;
+            skf_st(&dg[(size_t)r * a.maxw + c], dz_s[r * C + c], a.wthru);
+        }
+    }
+    // the slice's delta: (head delta . W_head[:, slice]) masked by the slice's activations
+    for (int e = threadIdx.x; e < SKF_RB * npc; e += blockDim.x) {
+        const int r = e / npc, j = e - r * npc;
+        double v = 0.0;
+        if (j < nc) {
+            double s = 0.0;
+            for (int c = 0; c < C; ++c) s += dz_s[r * C + c] * wnar[c * nc + j];
+            v = as[r * lda + j] > 0.0 ? s : 0.0;
+        }
+        as[r * lda + j] = v;
+    }
+    skf_lds_barrier();
+    {
+        double* dg = a.deltas + (((size_t)ls * a.T + t) * a.Bmax + r0) * a.maxw + c0;
+        for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
+            const int r = e / nc, j = e - r * nc;
+            skf_st(&dg[(size_t)r * a.maxw + j], as[r * lda + j], a.wthru);
+        }
+    }
+    if (ls < 1) return;
+    // the slice's partial input gradient of the split layer: delta[:, slice] . W_ls[slice, :]
+    skf_layer<false>(as, lda, part, ldk, staged ? wst : P + a.w_off[ls] + (size_t)c0 * Kl, nullptr, Kl, nc, false,
+                     red, wave, lane, a.zero, nullptr, nullptr, 0, true);
+    skf_lds_barrier();
+    double* bp = a.bpart + (((size_t)t * a.split + sl) * a.Bmax + r0) * a.maxw;
+    if (ls >= 2) {  // skf_cs_tail sums the partials and runs the remaining layers
+        for (int e = threadIdx.x; e < nr * Kl; e += blockDim.x) {
+            const int r = e / Kl, k = e - r * Kl;
+            bp[(size_t)r * a.maxw + k] = part[r * ldk + k];
+        }
+        return;
+    }
+    // One layer below the split layer (L == 3, sklearn's two-hidden-layer nets): the LAST slice of
+    // this row block to get here sums every slice's partial in slice order, masks it with layer 0's
+    // activations and stores layer 0's delta -- no tail kernel.  The partials go through to memory
+    // (agent-scope stores, complete once acknowledged) before the arrival ticket; the last arriver
+    // reads them with agent-scope loads.  Nobody waits: the other slices just leave.
+    __shared__ int last_s;
+    for (int e = threadIdx.x; e < nr * Kl; e += blockDim.x) {
+        const int r = e / Kl, k = e - r * Kl;
+        __hip_atomic_store(&bp[(size_t)r * a.maxw + k], part[r * ldk + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int* cnt = a.arrive + (size_t)t * gridDim.x + rb;
+        const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = prev == a.split - 1;
+        if (last_s) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next step's ticket
+    }
+    __syncthreads();
+    if (!last_s) return;
+    const double* a0 = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;  // layer 0's activations (skf_cs_fwd)
+    double* dg = a.deltas + ((size_t)t * a.Bmax + r0) * a.maxw;
+    for (int e = threadIdx.x; e < nr * Kl; e += blockDim.x) {
+        const int r = e / Kl, k = e - r * Kl;
+        double sum = 0.0;
+        for (int q = 0; q < a.split; ++q)
+            sum += __hip_atomic_load(&a.bpart[(((size_t)t * a.split + q) * a.Bmax + r0 + r) * a.maxw + k],
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        skf_st(&dg[(size_t)r * a.maxw + k], a0[(size_t)r * a.maxw + k] > 0.0 ? sum : 0.0, a.wthru);
+    }
+}
+
+__global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_tail_kernel(SkfArgs a) {
+    extern __shared__ double lds[];
+    const int t = blockIdx.y, rb = blockIdx.x;
+    if (a.active[t] == 0) return;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
+    const int ls = a.L - 2;
+    const double* P = a.params + (size_t)t * a.P;
+    auto ldof = [&](int l) { return skf_ld(skf_np(a.dims[l])); };
+    auto bufp = [&](int l) {
+        int o = 0;
+        for (int i = 0; i < l; ++i) o += ldof(i) * SKF_RB;
+        return lds + o;
+    };
+    double* red = bufp(a.L + 1);
+    // the activations below the split layer (the masks of the deltas computed here)
+    for (int l = 0; l < ls; ++l) {
+        const int N = a.dims[l + 1], np = skf_np(N);
+        const double* ag = a.acts + (((size_t)l * a.T + t) * a.Bmax + r0) * a.maxw;
+        for (int e = threadIdx.x; e < SKF_RB * np; e += blockDim.x) {
+            const int r = e / np, c = e - r * np;
+            bufp(l + 1)[r * ldof(l + 1) + c] = (r < nr && c < N) ? ag[(size_t)r * a.maxw + c] : 0.0;
+        }
+    }
+    skf_lds_barrier();
+    // delta of layer ls - 1 = (sum of the slices' partials, slice order) masked by its activation
+    {
+        const int K = a.dims[ls], np = skf_np(K);
+        double* d = bufp(ls);
+        for (int e = threadIdx.x; e < SKF_RB * np; e += blockDim.x) {
+            const int r = e / np, k = e - r * np;
+            double v = 0.0;
+            if (r < nr && k < K) {
+                double s = 0.0;
+                for (int q = 0; q < a.split; ++q)
+                    s += a.bpart[(((size_t)t * a.split + q) * a.Bmax + r0 + r) * a.maxw + k];
+                v = d[r * ldof(ls) + k] > 0.0 ? s : 0.0;
+            }
+            d[r * ldof(ls) + k] = v;
+        }
+        skf_lds_barrier();
+        double* dg = a.deltas + (((size_t)(ls - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
+        for (int e = threadIdx.x; e < nr * K; e += blockDim.x) {
+            const int r = e / K, k = e - r * K;
+            skf_st(&dg[(size_t)r * a.maxw + k], d[r * ldof(ls) + k], a.wthru);
+        }
+    }
+    // the remaining layers' backward, as in skf_rowpass
+    for (int l = ls - 1; l >= 1; --l) {
+        const int K = a.dims[l], N = a.dims[l + 1];
+        skf_layer<false>(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), P + a.w_off[l], nullptr, K, N, false, red, wave,
+                         lane, a.zero, nullptr);
+        skf_lds_barrier();
+        double* dg = a.deltas + (((size_t)(l - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
+        for (int e = threadIdx.x; e < nr * K; e += blockDim.x) {
+            const int r = e / K, c = e - r * K;
+            skf_st(&dg[(size_t)r * a.maxw + c], bufp(l)[r * ldof(l) + c], a.wthru);
+        }
+    }
+}
+
 // One 16 x 16 tile of one layer's gradient [N][K + 1] (column K = bias) per workgroup; the 4
 // waves split the minibatch rows, partial tiles summed in wave order, Adam in the epilogue.
 __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
@@ -431,6 +828,11 @@ __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
     skf_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     const int n = n0 + lr, k = k0 + lr;
     constexpr int SB = 13;  // k-steps (4 rows each) whose operands are in flight together
+    // sklearn AdamOptimizer: lr_t = lr sqrt(1 - b2^t) / (1 - b1^t) -- two float64 pow()s, computed
+    // by wave 0 while its first operand loads are in flight (after the products they were on the
+    // epilogue's critical path)
+    double lr_t = 0.0;
+    bool have_lr = false;
     for (int s0 = rb; s0 < re; s0 += 4 * SB) {
         double av[SB], bv[SB];
 #pragma unroll
@@ -441,8 +843,20 @@ __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
             av[u] = (okr && n < N) ? dl[(size_t)r * a.maxw + n] : 0.0;
             bv[u] = (okr && k < K) ? in[(size_t)r * ldi + k] : ((okr && k == K) ? 1.0 : 0.0);
         }
+        if (!have_lr) {
+            have_lr = true;
+            if (wave == 0) {
+                const double step = (double)a.step[t];
+                lr_t = a.lr[t] * sqrt(1.0 - pow(a.beta2, step)) / (1.0 - pow(a.beta1, step));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int u = 0; u < SB; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+    }
+    if (!have_lr && wave == 0) {  // (a wave without rows)
+        const double step = (double)a.step[t];
+        lr_t = a.lr[t] * sqrt(1.0 - pow(a.beta2, step)) / (1.0 - pow(a.beta1, step));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) part[wave][lane][j] = acc[j];
@@ -451,9 +865,6 @@ __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
     double g4[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) g4[j] = ((part[0][lane][j] + part[1][lane][j]) + part[2][lane][j]) + part[3][lane][j];
-    // sklearn AdamOptimizer: lr_t = lr sqrt(1 - b2^t) / (1 - b1^t)
-    const double step = (double)a.step[t];
-    const double lr_t = a.lr[t] * sqrt(1.0 - pow(a.beta2, step)) / (1.0 - pow(a.beta1, step));
     const double wdec = a.alpha * a.inv_rows;
     double sq = 0.0;
 #pragma unroll
@@ -490,6 +901,12 @@ bool skf_supported(const SkfArgs& a) {
     if (a.L < 1 || a.L > SKF_MAXL) return false;
     if (a.dims[a.L] > 16) return false;                // one head tile
     if (skf_lds_bytes(a) > 160 * 1024) return false;   // CDNA4 LDS per workgroup
+    if (a.split > 1) {                                 // column split: narrow head, a hidden layer
+        if (a.L < 2 || a.dims[a.L] > SKF_NARROW || a.cw <= 0 || (a.cw & 15) || a.zpart == nullptr ||
+            (a.L >= 3 && a.bpart == nullptr) || (a.L == 3 && a.arrive == nullptr))
+            return false;
+        if (skf_cs_bwd_lds(a) > 160 * 1024) return false;
+    }
     return true;
 }
 
@@ -500,16 +917,21 @@ bool skf_supported(const SkfArgs& a) {
 hipError_t skf_prepare(const SkfArgs& a) {
     static std::mutex mu;
     static size_t lds_set[64] = {};
-    const size_t lds = skf_lds_bytes(a);
+    const size_t lds =
+        std::max(skf_lds_bytes(a), a.split > 1 ? std::max(skf_cs_bwd_lds(a), skf_cs_fwd_lds(a)) : (size_t)0);
     if (lds <= 64 * 1024) return hipSuccess;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> g(mu);
     if (lds <= lds_set[dev]) return hipSuccess;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(skf_rowpass_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e == hipSuccess) lds_set[dev] = lds;
-    return e;
+    const void* ks[] = {reinterpret_cast<const void*>(skf_rowpass_kernel), reinterpret_cast<const void*>(skf_cs_fwd_kernel),
+                        reinterpret_cast<const void*>(skf_cs_bwd_kernel), reinterpret_cast<const void*>(skf_cs_tail_kernel)};
+    for (const void* k : ks) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    lds_set[dev] = lds;
+    return hipSuccess;
 }
 
 hipError_t skf_step_launch(const SkfArgs& a, hipStream_t s) {
@@ -521,7 +943,21 @@ hipError_t skf_step_launch(const SkfArgs& a, hipStream_t s) {
         const hipError_t e = skf_prepare(a);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(skf_rowpass_kernel, dim3((a.rows + SKF_RB - 1) / SKF_RB, a.T), dim3(SKF_WAVES * 64), lds, s, a);
+    const int nrb = (a.rows + SKF_RB - 1) / SKF_RB;
+    if (a.split > 1) {
+        if (std::max(skf_cs_bwd_lds(a), skf_cs_fwd_lds(a)) > 64 * 1024) {
+            const hipError_t e = skf_prepare(a);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(skf_cs_fwd_kernel, dim3(nrb, a.split, a.T), dim3(SKF_WAVES * 64), skf_cs_fwd_lds(a), s, a);
+        hipLaunchKernelGGL(skf_cs_bwd_kernel, dim3(nrb, a.split, a.T), dim3(SKF_WAVES * 64), skf_cs_bwd_lds(a), s, a);
+        // (L == 3: the last slice of a row block to finish skf_cs_bwd forms the one delta below the
+        // split layer itself)
+        if (a.L >= 4)
+            hipLaunchKernelGGL(skf_cs_tail_kernel, dim3(nrb, a.T), dim3(SKF_WAVES * 64), lds, s, a);
+    } else {
+        hipLaunchKernelGGL(skf_rowpass_kernel, dim3(nrb, a.T), dim3(SKF_WAVES * 64), lds, s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(skf_wgrad_adam_kernel, dim3(skf_wgrad_tiles(a), a.T), dim3(256), 0, s, a);

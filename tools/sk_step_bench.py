@@ -26,6 +26,7 @@ def run(hl, T, epochs, fused, X, y):
     steps = sum(e.n_iter_ for e in ests[:1]) * ((len(X) + 199) // 200)
     return {"hidden": list(hl), "trials": T, "epochs": int(ests[0].n_iter_), "fused": bool(ests[0]._hip_fused),
             "wall_s": dt, "us_per_step": dt / steps * 1e6, "final_loss": float(ests[0].loss_),
+            "split": getattr(ests[0], "_hip_split", 1), "sk_split_env": os.environ.get("FEDMI_SK_SPLIT"),
             "stamps_us": [round(x, 2) for x in getattr(ests[0], "_hip_stamps", [])]}
 
 
