@@ -74,11 +74,10 @@ struct SkfArgs {
     const double* zero;                     // one 0.0 in device memory (branch-free masked loads)
     double* wt;                             // optional [T][P]: each layer's weights transposed [K][N] (kept by
                                             // the Adam epilogue; read by the forward), nullptr: none
-    // Column-split row pass (mlp_fused_f64.hip skf_cs_*): split > 1 slices the last hidden layer's
-    // output columns (cw each) over `split` workgroups per row block; zpart [T][split][Bmax][C] and
-    // bpart [T][split][Bmax][maxw] carry the slices' partial logits / input gradients
+    // Column-split row pass (mlp_fused_f64.hip skf_cs_*, two hidden layers): split > 1 slices hidden
+    // layer 1's output columns (cw each) over `split` workgroups per row block; bpart
+    // [T][split][Bmax][maxw] carries the slices' partial input gradients of that layer
     int split, cw;
-    double* zpart;
     double* bpart;
     int* arrive;                            // [T][row blocks] arrival tickets of skf_cs_bwd (zeroed; L == 3)
 };

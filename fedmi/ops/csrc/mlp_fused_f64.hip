@@ -98,14 +98,15 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
                                              int ld_d, const double* __restrict__ W, const double* __restrict__ bias,
                                              int K, int N, bool relu, double* __restrict__ red, int wave, int lane,
                                              const double* __restrict__ zero, const double* __restrict__ WT,
-                                             unsigned long long* dbg = nullptr, int ldwt = 0, bool raw = false) {
+                                             unsigned long long* dbg = nullptr, int ldwt = 0, bool raw = false,
+                                             int gmax = SKF_WAVES) {
     if (ldwt <= 0) ldwt = N;
     const int lr = lane & 15, lg = lane >> 4;
     if (dbg != nullptr && threadIdx.x == 0) dbg[0] = __builtin_amdgcn_s_memrealtime();
     const int ntiles = FWD ? (N + 15) >> 4 : (K + 15) >> 4;
     const int steps = FWD ? (K + 3) >> 2 : (N + 3) >> 2;
     const int nb = (steps + KB - 1) / KB;           // chunks per tile
-    const int G = ntiles < SKF_WAVES ? max(1, min(nb, SKF_WAVES / ntiles)) : 1;
+    const int G = min(gmax, ntiles < SKF_WAVES ? max(1, min(nb, SKF_WAVES / ntiles)) : 1);
     const int units = ntiles * G;
     const int bpg = (nb + G - 1) / G;               // chunks per unit
     const int my_units = wave < units ? (units - 1 - wave) / SKF_WAVES + 1 : 0;
@@ -219,14 +220,18 @@ __device__ __forceinline__ void skf_layer(const double* __restrict__ src, int ld
                                           const double* __restrict__ W, const double* __restrict__ bias, int K, int N,
                                           bool relu, double* __restrict__ red, int wave, int lane,
                                           const double* __restrict__ zero, const double* __restrict__ WT,
-                                          unsigned long long* dbg = nullptr, int ldwt = 0, bool raw = false) {
-    const int steps = FWD ? (K + 3) >> 2 : (N + 3) >> 2;
+                                          unsigned long long* dbg = nullptr, int ldwt = 0, bool raw = false,
+                                          int gmax = SKF_WAVES, int kb_steps = 0) {
+    // kb_steps > 0: pick the chunk length of a product this many k-steps deep (a slice of a wider
+    // product keeps the whole product's chunking, so its sums are the same)
+    const int steps = kb_steps > 0 ? kb_steps : (FWD ? (K + 3) >> 2 : (N + 3) >> 2);
     if (steps <= 4)
-        skf_layer_kb<FWD, 4>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw);
+        skf_layer_kb<FWD, 4>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw, gmax);
     else if (steps <= 8)
-        skf_layer_kb<FWD, 8>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw);
+        skf_layer_kb<FWD, 8>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw, gmax);
     else
-        skf_layer_kb<FWD, SKF_KB>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw);
+        skf_layer_kb<FWD, SKF_KB>(src, ld_s, dst, ld_d, W, bias, K, N, relu, red, wave, lane, zero, WT, dbg, ldwt, raw,
+                                  gmax);
 }
 
 // Narrow output layer (N <= SKF_NARROW) on the VALU, weights staged in LDS (Ws [N][K], bias at
@@ -395,85 +400,62 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
 }
 
 // ---------------------------------------------------------------------------------------
-// Column-split row pass (SkfArgs::split = S > 1).  skf_rowpass runs one 16-row block on ONE CU and
-// is bound by that CU's float64 MFMA pipes (MFMA busy 67 %): every row block streams and multiplies
-// the whole weight set alone, so a minibatch of 200 rows uses 13 CUs.  With a narrow head (binary
-// logistic / <= 4 classes, sklearn's [S] / [H] jobs) the last hidden layer's output columns are
-// sliced over S workgroups per row block -- S x more CUs for the widest products -- in three
-// kernels (no in-kernel waits across workgroups, so any number of trials can queue):
-//   skf_cs_fwd   (row block x slice x trial)  gather, the layers before the split layer (every slice
-//                recomputes them; slice 0 stores them), the split layer's forward for its columns,
-//                and the slice's partial logits = a[:, slice] . W_head[:, slice]^T -> zpart
-//   skf_cs_bwd   (row block x slice x trial)  logits = sum of the S partials in slice order + bias ->
-//                loss head -> the slice's delta (head delta . W_head, ReLU mask) -> the slice's
-//                partial input gradient of the split layer (raw product) -> bpart
-//   skf_cs_tail  (row block x trial)          delta below the split layer = sum of the S partials
-//                in slice order, masked; the remaining layers' backward as in skf_rowpass
-// Every sum is in a fixed order (deterministic); the orders differ from skf_rowpass's, so the two
-// agree to float64 rounding, not bitwise.
+// Column-split row pass (SkfArgs::split = S > 1), BIT-IDENTICAL to skf_rowpass.  skf_rowpass runs
+// one 16-row block on ONE CU and is bound by that CU's float64 MFMA pipes (MFMA busy 67 %): every
+// row block streams and multiplies the whole weight set alone, so a 200-row minibatch uses 13 CUs.
+// For two hidden layers and a narrow head (sklearn's [S] net (50, 400) and the [H] grid's
+// two-layer nets) the second hidden layer's columns are sliced over S workgroups per row block:
+//   skf_cs_fwd  (row block x slice x trial)  gather, hidden layer 0 (every slice recomputes it, slice
+//               0 stores it), hidden layer 1's forward for the slice's columns -> acts
+//   skf_cs_bwd  (row block x slice x trial)  the logits from ALL of layer 1's activations exactly as
+//               skf_fwd_narrow sums them, the loss head, the slice's delta (head delta . W_head, ReLU
+//               mask), the slice's partial input gradient of layer 1; the LAST slice of the row
+//               block to finish sums the S partials in slice order and stores layer 0's delta
+// Same sums as skf_rowpass, bit for bit: a slice is exactly one of the k-groups skf_layer<false>
+// splits layer 1's input gradient into (G groups of bpg chunks, summed in group order from 0), and
+// the forward keeps skf_rowpass's per-tile chains (gmax, kb_steps) -- so the split may only cut
+// where skf_rowpass already cuts (skf_pick_split), and the float64 estimator keeps tracking
+// scikit-learn epoch by epoch (tools/sklearn_parity.py).
 // ---------------------------------------------------------------------------------------
+struct SkfGroups { int KB, nb, G, bpg; };
+// skf_layer_kb's cut of a product: chunk length KB (k-steps), nb chunks per tile, G k-groups of
+// bpg chunks (the same arithmetic as skf_layer / skf_layer_kb)
+__host__ __device__ __forceinline__ SkfGroups skf_groups(int steps, int ntiles) {
+    SkfGroups g;
+    g.KB = steps <= 4 ? 4 : (steps <= 8 ? 8 : SKF_KB);
+    g.nb = (steps + g.KB - 1) / g.KB;
+    const int Gm = ntiles < SKF_WAVES ? (SKF_WAVES / ntiles < g.nb ? SKF_WAVES / ntiles : g.nb) : 1;
+    g.G = Gm < 1 ? 1 : Gm;
+    g.bpg = (g.nb + g.G - 1) / g.G;
+    return g;
+}
+
 void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw) {
     *split = 1;
     *cw = 0;
-    if (a.L < 2 || a.dims[a.L] > SKF_NARROW) return;
-    const int hk = a.dims[a.L - 1];
-    // default: slices of >= 64 columns, and about one workgroup per CU over all row blocks and
-    // trials (more queue behind each other: (50, 400) x 9 trials 65 us per step at 2 slices, 100 at 7;
-    // x 1 trial 39 us at 7, 58 unsplit -- profiles/sk_split_r6.log)
-    const int nrb = (a.Bmax + SKF_RB - 1) / SKF_RB;  // row blocks of a full minibatch
-    int S = want;
-    if (S <= 0) {
-        const int by_cols = hk >= 96 ? (hk + 63) / 64 : 1;
-        const int by_cus = 256 / std::max(1, nrb * a.T);
-        S = std::min(by_cols, std::max(1, by_cus));
-    }
-    S = S < 1 ? 1 : (S > 16 ? 16 : S);
-    if (S <= 1) return;
-    const int w = (((hk + S - 1) / S) + 15) & ~15;  // slices of whole 16-column tiles
+    if (a.L != 3 || a.dims[a.L] > SKF_NARROW || want == 1) return;
+    const int K = a.dims[1], N = a.dims[2];   // hidden layer 1: K -> N
+    // skf_rowpass's input gradient of layer 1: steps over N, tiles over K
+    const SkfGroups g = skf_groups((N + 3) >> 2, (K + 15) >> 4);
+    if (g.G < 2) return;                      // one k-group: no cut that keeps the sums
+    const int w = g.bpg * g.KB * 4;           // columns per k-group (a multiple of 16)
+    const int S = (N + w - 1) / w;
+    if (S < 2) return;
+    // slices only while the grid stays within about one workgroup per CU (more queue behind each
+    // other: profiles/sk_split_r6.log); FEDMI_SK_SPLIT=<n> > 1 forces the split
+    const int nrb = (a.Bmax + SKF_RB - 1) / SKF_RB;
+    if (want <= 0 && nrb * a.T * S > 256) return;
+    *split = S;
     *cw = w;
-    *split = (hk + w - 1) / w;
-    if (*split <= 1) *cw = 0;
 }
 
-// Weights a split kernel stages in LDS at its start, in flight with its other first loads (a layer's
-// weights streamed from memory are one more dependent round trip each): skf_cs_fwd the layers
-// below the split layer + the split layer's slice (+ biases), skf_cs_bwd the split layer's slice
-// (dgrad operand).  Only when they fit beside the kernel's buffers (160 KB of LDS).
-__host__ __device__ __forceinline__ int skf_cs_fwd_stage_doubles(const SkfArgs& a) {
-    const int ls = a.L - 2;
-    int d = 0;
-    for (int l = 0; l < ls; ++l) d += a.dims[l + 1] * a.dims[l] + a.dims[l + 1];
-    return d + a.cw * a.dims[ls] + a.cw;
-}
-__host__ __device__ __forceinline__ int skf_cs_bwd_stage_doubles(const SkfArgs& a) {
-    return a.L >= 3 ? a.cw * a.dims[a.L - 2] : 0;
-}
-__host__ __device__ __forceinline__ size_t skf_cs_bwd_base_doubles(const SkfArgs& a) {
-    const int ls = a.L - 2;
-    return (size_t)SKF_RB * skf_ld(skf_np(a.cw)) + (size_t)SKF_RB * skf_ld(skf_np(a.dims[ls])) + SKF_RED_DOUBLES +
-           (size_t)a.dims[a.L] * (a.cw + 1);
-}
-#ifndef SKF_STAGE_FWD  // A/B builds: -DSKF_STAGE_FWD=1 / -DSKF_STAGE_BWD=1 stage the weights (measured slower: profiles/sk_split_r6.log)
-#define SKF_STAGE_FWD 0
-#endif
-#ifndef SKF_STAGE_BWD
-#define SKF_STAGE_BWD 0
-#endif
-__host__ __device__ __forceinline__ bool skf_cs_fwd_staged(const SkfArgs& a, size_t base_doubles) {
-    return SKF_STAGE_FWD && (base_doubles + skf_cs_fwd_stage_doubles(a)) * sizeof(double) <= 160 * 1024;
-}
-__host__ __device__ __forceinline__ bool skf_cs_bwd_staged(const SkfArgs& a) {
-    return SKF_STAGE_BWD && (skf_cs_bwd_base_doubles(a) + skf_cs_bwd_stage_doubles(a)) * sizeof(double) <= 160 * 1024;
-}
-static size_t skf_cs_fwd_lds(const SkfArgs& a) {
-    const size_t base = skf_lds_bytes(a) / sizeof(double);
-    return (base + (skf_cs_fwd_staged(a, base) ? skf_cs_fwd_stage_doubles(a) : 0)) * sizeof(double);
-}
-
-// LDS of skf_cs_bwd (doubles): the slice's activations / delta [16][ld(cw)], the raw input-gradient
-// partial [16][ld(K)], the k-split partials, and the slice's head weights + bias
+// LDS of skf_cs_bwd (doubles): layer 1's activations (all columns, the logits' operand; the slice's
+// columns become its delta) [16][ld(N)], the partial input gradient [16][ld(K)], the k-split
+// partials, the head weights + bias
 static size_t skf_cs_bwd_lds(const SkfArgs& a) {
-    return (skf_cs_bwd_base_doubles(a) + (skf_cs_bwd_staged(a) ? skf_cs_bwd_stage_doubles(a) : 0)) * sizeof(double);
+    const size_t d = (size_t)SKF_RB * skf_ld(skf_np(a.dims[2])) + (size_t)SKF_RB * skf_ld(skf_np(a.dims[1])) +
+                     SKF_RED_DOUBLES + (size_t)a.dims[3] * (a.dims[2] + 1);
+    return d * sizeof(double);
 }
 
 __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
@@ -482,44 +464,15 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
     if (a.active[t] == 0) return;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
-    const int ls = a.L - 2, Kl = a.dims[ls], Nl = a.dims[ls + 1], C = a.dims[a.L];
-    const int c0 = sl * a.cw, nc = min(a.cw, Nl - c0);
+    const int K1 = a.dims[1], N1 = a.dims[2];
+    const int c0 = sl * a.cw, nc = min(a.cw, N1 - c0);
     if (rb == 0 && sl == 0 && threadIdx.x == 0) a.step[t] += 1;  // this minibatch's Adam step
     const double* P = a.params + (size_t)t * a.P;
     auto ldof = [&](int l) { return skf_ld(skf_np(a.dims[l])); };
-    auto bufp = [&](int l) {
-        int o = 0;
-        for (int i = 0; i < l; ++i) o += ldof(i) * SKF_RB;
-        return lds + o;
-    };
-    double* red = bufp(a.L + 1);
-    double* wnar = red + SKF_RED_DOUBLES;  // the slice's head weights [C][nc]
-    const double* Wh = P + a.w_off[a.L - 1];
-    for (int e = threadIdx.x; e < C * nc; e += blockDim.x) {
-        const int c = e / nc, j = e - c * nc;
-        wnar[e] = Wh[(size_t)c * Nl + c0 + j];
-    }
-    // staged weights [W_0 | b_0 | ... | W_ls slice | b_ls slice], dense [N][K] rows (LDS): their
-    // loads are in flight with the gather's
-    double* wst = wnar + skf_narrow_doubles(a);
-    const size_t base_d = (size_t)(wst - lds);
-    const bool staged = skf_cs_fwd_staged(a, base_d);
-    int w_lds[SKF_MAXL], b_lds[SKF_MAXL];
-    {
-        int o = 0;
-        for (int l = 0; l <= ls; ++l) {
-            const int N = l < ls ? a.dims[l + 1] : nc, K = a.dims[l];
-            w_lds[l] = o;
-            b_lds[l] = o + N * K;
-            if (staged) {
-                const double* Wg = P + a.w_off[l] + (l < ls ? 0 : (size_t)c0 * Kl);
-                const double* bg = P + a.b_off[l] + (l < ls ? 0 : c0);
-                for (int e = threadIdx.x; e < N * K; e += blockDim.x) wst[o + e] = Wg[e];
-                for (int e = threadIdx.x; e < N; e += blockDim.x) wst[o + N * K + e] = bg[e];
-            }
-            o += N * K + (l < ls ? N : a.cw);
-        }
-    }
+    double* b0 = lds;                               // inputs [16][ld(F)]
+    double* b1 = b0 + ldof(0) * SKF_RB;             // hidden 0 [16][ld(K1)]
+    double* b2 = b1 + ldof(1) * SKF_RB;             // hidden 1 [16][ld(N1)] (this slice's columns)
+    double* red = b2 + ldof(2) * SKF_RB;
     const int F = a.dims[0], fp = skf_np(F);
     const int* perm = a.perms + (size_t)(*a.epoch_ctr) * a.n_perm + a.off + r0;
     double* xg = a.xg + ((size_t)t * a.Bmax + r0) * F;
@@ -530,119 +483,94 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
             v = a.X[(size_t)perm[r] * F + f];
             if (sl == 0) skf_st(&xg[(size_t)r * F + f], v, a.wthru);
         }
-        bufp(0)[r * ldof(0) + f] = v;
+        b0[r * ldof(0) + f] = v;
     }
     skf_lds_barrier();
-    for (int l = 0; l < ls; ++l) {  // the layers below the split layer, whole (slice 0 stores them)
-        const int K = a.dims[l], N = a.dims[l + 1];
-        if (staged)
-            skf_layer<true>(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), wst + w_lds[l], wst + b_lds[l], K, N, true, red,
-                            wave, lane, a.zero, nullptr);
-        else
-            skf_layer<true>(bufp(l), ldof(l), bufp(l + 1), ldof(l + 1), P + a.w_off[l], P + a.b_off[l], K, N, true,
-                            red, wave, lane, a.zero, a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[l] : nullptr);
-        skf_lds_barrier();
-        if (sl == 0) {
-            double* ag = a.acts + (((size_t)l * a.T + t) * a.Bmax + r0) * a.maxw;
-            for (int e = threadIdx.x; e < nr * N; e += blockDim.x) {
-                const int r = e / N, c = e - r * N;
-                skf_st(&ag[(size_t)r * a.maxw + c], bufp(l + 1)[r * ldof(l + 1) + c], a.wthru);
-            }
-        }
-    }
-    // the split layer's forward for output columns [c0, c0 + nc)
-    if (staged)
-        skf_layer<true>(bufp(ls), ldof(ls), bufp(ls + 1) + c0, ldof(ls + 1), wst + w_lds[ls], wst + b_lds[ls], Kl, nc,
-                        true, red, wave, lane, a.zero, nullptr);
-    else
-        skf_layer<true>(bufp(ls), ldof(ls), bufp(ls + 1) + c0, ldof(ls + 1), P + a.w_off[ls] + (size_t)c0 * Kl,
-                        P + a.b_off[ls] + c0, Kl, nc, true, red, wave, lane, a.zero,
-                        a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[ls] + c0 : nullptr, nullptr, Nl);
+    // hidden layer 0, whole (the same call as skf_rowpass); slice 0 stores it
+    skf_layer<true>(b0, ldof(0), b1, ldof(1), P + a.w_off[0], P + a.b_off[0], F, K1, true, red, wave, lane, a.zero,
+                    a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[0] : nullptr);
     skf_lds_barrier();
-    {
-        double* ag = a.acts + (((size_t)ls * a.T + t) * a.Bmax + r0) * a.maxw + c0;
-        for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
-            const int r = e / nc, j = e - r * nc;
-            skf_st(&ag[(size_t)r * a.maxw + j], bufp(ls + 1)[r * ldof(ls + 1) + c0 + j], a.wthru);
+    if (sl == 0) {
+        double* ag = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;
+        for (int e = threadIdx.x; e < nr * K1; e += blockDim.x) {
+            const int r = e / K1, c = e - r * K1;
+            skf_st(&ag[(size_t)r * a.maxw + c], b1[r * ldof(1) + c], a.wthru);
         }
     }
-    // the slice's partial logits: wave w = row w, lanes over the slice's columns, xor-tree sum
-    {
-        const int r = wave;  // SKF_WAVES == SKF_RB
-        const double* ar = bufp(ls + 1) + r * ldof(ls + 1) + c0;
-        for (int c = 0; c < C; ++c) {
-            double s = 0.0;
-            for (int j = lane; j < nc; j += 64) s += ar[j] * wnar[c * nc + j];
-            s = skf_wave_sum(s);
-            if (lane == 0 && r < nr) a.zpart[(((size_t)t * a.split + sl) * a.Bmax + r0 + r) * C + c] = s;
-        }
+    // hidden layer 1's forward for output columns [c0, c0 + nc): skf_rowpass's per-tile chains
+    // (its chunk length and k-groups for the whole product)
+    const SkfGroups gf = skf_groups((K1 + 3) >> 2, (N1 + 15) >> 4);
+    skf_layer<true>(b1, ldof(1), b2 + c0, ldof(2), P + a.w_off[1] + (size_t)c0 * K1, P + a.b_off[1] + c0, K1, nc, true,
+                    red, wave, lane, a.zero, a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[1] + c0 : nullptr,
+                    nullptr, N1, false, gf.G, (K1 + 3) >> 2);
+    skf_lds_barrier();
+    double* ag = a.acts + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw + c0;
+    for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
+        const int r = e / nc, j = e - r * nc;
+        skf_st(&ag[(size_t)r * a.maxw + j], b2[r * ldof(2) + c0 + j], a.wthru);
     }
 }
 
 __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     extern __shared__ double lds[];
     __shared__ double dz_s[SKF_RB * SKF_NARROW];
+    __shared__ int last_s;
     const int t = blockIdx.z, sl = blockIdx.y, rb = blockIdx.x;
     if (a.active[t] == 0) return;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
-    const int ls = a.L - 2, Kl = a.dims[ls], Nl = a.dims[ls + 1], C = a.dims[a.L];
-    const int c0 = sl * a.cw, nc = min(a.cw, Nl - c0);
+    const int K1 = a.dims[1], N1 = a.dims[2], C = a.dims[3];
+    const int c0 = sl * a.cw, nc = min(a.cw, N1 - c0);
     const double* P = a.params + (size_t)t * a.P;
-    const int npc = skf_np(a.cw), lda = skf_ld(npc), ldk = skf_ld(skf_np(Kl));
-    double* as = lds;                      // [16][lda]: the slice's activations, then its delta
-    double* part = as + SKF_RB * lda;      // [16][ldk]: raw partial input gradient
+    const int np2 = skf_np(N1), ld2 = skf_ld(np2), ldk = skf_ld(skf_np(K1));
+    double* h = lds;                       // [16][ld2]: layer 1's activations; the slice's columns -> delta
+    double* part = h + SKF_RB * ld2;       // [16][ldk]: the slice's partial input gradient of layer 1
     double* red = part + SKF_RB * ldk;
-    double* wnar = red + SKF_RED_DOUBLES;  // [C][nc] head weights of the slice, then the bias [C]
-    const double* Wh = P + a.w_off[a.L - 1];
-    for (int e = threadIdx.x; e < C * nc; e += blockDim.x) {
-        const int c = e / nc, j = e - c * nc;
-        wnar[e] = Wh[(size_t)c * Nl + c0 + j];
-    }
-    if (threadIdx.x < C) wnar[C * nc + threadIdx.x] = P[a.b_off[a.L - 1] + threadIdx.x];
-    // the split layer's weight slice [nc][Kl] (the dgrad operand), staged with the first loads
-    double* wst = wnar + (size_t)C * (a.cw + 1);
-    const bool staged = ls >= 1 && skf_cs_bwd_staged(a);
-    if (staged) {
-        const double* Wg = P + a.w_off[ls] + (size_t)c0 * Kl;
-        for (int e = threadIdx.x; e < nc * Kl; e += blockDim.x) wst[e] = Wg[e];
-    }
-    const double* ag = a.acts + (((size_t)ls * a.T + t) * a.Bmax + r0) * a.maxw + c0;
-    for (int e = threadIdx.x; e < SKF_RB * npc; e += blockDim.x) {
-        const int r = e / npc, j = e - r * npc;
-        as[r * lda + j] = (r < nr && j < nc) ? ag[(size_t)r * a.maxw + j] : 0.0;
+    double* wh = red + SKF_RED_DOUBLES;    // head weights [C][N1], then its bias [C]
+    const double* Wh = P + a.w_off[2];
+    for (int e = threadIdx.x; e < C * N1; e += blockDim.x) wh[e] = Wh[e];
+    if (threadIdx.x < C) wh[C * N1 + threadIdx.x] = P[a.b_off[2] + threadIdx.x];
+    const double* ag = a.acts + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw;
+    for (int e = threadIdx.x; e < SKF_RB * np2; e += blockDim.x) {
+        const int r = e / np2, j = e - r * np2;
+        h[r * ld2 + j] = (r < nr && j < N1) ? ag[(size_t)r * a.maxw + j] : 0.0;
     }
     skf_lds_barrier();
-    // loss head on the logits = sum of the slices' partials (slice order) + bias
+    // logits: skf_fwd_narrow's sums (wave w = row w, lanes over k, xor tree, + bias)
+    {
+        const int r = wave;
+        for (int c = 0; c < C; ++c) {
+            double sum = 0.0;
+            for (int k = lane; k < N1; k += 64) sum += h[r * ld2 + k] * wh[c * N1 + k];
+            sum = skf_wave_sum(sum);
+            if (lane == 0) dz_s[r * C + c] = sum + wh[C * N1 + c];
+        }
+    }
+    skf_lds_barrier();
+    // loss head (skf_rowpass's): the logits become the head delta in place
     double lrow = 0.0;
     if (threadIdx.x < SKF_RB) {
         const int r = threadIdx.x;
         const double eps = 2.220446049250313e-16;
-        double z[SKF_NARROW];
-        for (int c = 0; c < C; ++c) {
-            double s = 0.0;
-            if (r < nr)
-                for (int q = 0; q < a.split; ++q) s += a.zpart[(((size_t)t * a.split + q) * a.Bmax + r0 + r) * C + c];
-            z[c] = s + wnar[C * nc + c];
-        }
+        double* zr = dz_s + r * C;
         if (r >= nr) {
-            for (int c = 0; c < C; ++c) dz_s[r * C + c] = 0.0;
+            for (int c = 0; c < C; ++c) zr[c] = 0.0;
         } else {
             const int* perm = a.perms + (size_t)(*a.epoch_ctr) * a.n_perm + a.off + r0;
             const int yy = a.y[perm[r]];
             if (a.head == 1) {
-                const double p = 1.0 / (1.0 + exp(-z[0]));
+                const double p = 1.0 / (1.0 + exp(-zr[0]));
                 const double pc = fmin(fmax(p, eps), 1.0 - eps);
                 lrow = yy ? -log(pc) : -log(1.0 - pc);
-                dz_s[r * C] = (p - (double)yy) * a.inv_rows;
+                zr[0] = (p - (double)yy) * a.inv_rows;
             } else {
-                double mx = z[0];
-                for (int c = 1; c < C; ++c) mx = fmax(mx, z[c]);
+                double mx = zr[0];
+                for (int c = 1; c < C; ++c) mx = fmax(mx, zr[c]);
                 double se = 0.0;
-                for (int c = 0; c < C; ++c) se += exp(z[c] - mx);
-                const double py = fmin(fmax(exp(z[yy] - mx) / se, eps), 1.0 - eps);
+                for (int c = 0; c < C; ++c) se += exp(zr[c] - mx);
+                const double py = fmin(fmax(exp(zr[yy] - mx) / se, eps), 1.0 - eps);
                 lrow = -log(py);
-                for (int c = 0; c < C; ++c) dz_s[r * C + c] = (exp(z[c] - mx) / se - (c == yy ? 1.0 : 0.0)) * a.inv_rows;
+                for (int c = 0; c < C; ++c) zr[c] = (exp(zr[c] - mx) / se - (c == yy ? 1.0 : 0.0)) * a.inv_rows;
             }
         }
     }
@@ -652,52 +580,44 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     }
     skf_lds_barrier();
     if (sl == 0) {  // the head delta: the head's wgrad operand
-        double* dg = a.deltas + (((size_t)(a.L - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
+        double* dg = a.deltas + (((size_t)2 * a.T + t) * a.Bmax + r0) * a.maxw;
         for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
             const int r = e / C, c = e - r * C;
             skf_st(&dg[(size_t)r * a.maxw + c], dz_s[r * C + c], a.wthru);
         }
     }
-    // the slice's delta: (head delta . W_head[:, slice]) masked by the slice's activations
+    // the slice's delta: skf_bwd_narrow's sums over the slice's columns, ReLU mask, in place
+    const int npc = skf_np(nc);
     for (int e = threadIdx.x; e < SKF_RB * npc; e += blockDim.x) {
-        const int r = e / npc, j = e - r * npc;
+        const int r = e / npc, j = e - r * npc, k = c0 + j;
         double v = 0.0;
         if (j < nc) {
-            double s = 0.0;
-            for (int c = 0; c < C; ++c) s += dz_s[r * C + c] * wnar[c * nc + j];
-            v = as[r * lda + j] > 0.0 ? s : 0.0;
+            double sum = 0.0;
+            for (int n = 0; n < C; ++n) sum += dz_s[r * C + n] * wh[n * N1 + k];
+            v = h[r * ld2 + k] > 0.0 ? sum : 0.0;
         }
-        as[r * lda + j] = v;
+        if (k < np2) h[r * ld2 + k] = v;
     }
     skf_lds_barrier();
     {
-        double* dg = a.deltas + (((size_t)ls * a.T + t) * a.Bmax + r0) * a.maxw + c0;
+        double* dg = a.deltas + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw + c0;
         for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
             const int r = e / nc, j = e - r * nc;
-            skf_st(&dg[(size_t)r * a.maxw + j], as[r * lda + j], a.wthru);
+            skf_st(&dg[(size_t)r * a.maxw + j], h[r * ld2 + c0 + j], a.wthru);
         }
     }
-    if (ls < 1) return;
-    // the slice's partial input gradient of the split layer: delta[:, slice] . W_ls[slice, :]
-    skf_layer<false>(as, lda, part, ldk, staged ? wst : P + a.w_off[ls] + (size_t)c0 * Kl, nullptr, Kl, nc, false,
-                     red, wave, lane, a.zero, nullptr, nullptr, 0, true);
+    // the slice's partial input gradient of layer 1 = ONE of skf_rowpass's k-groups: one group
+    // (gmax 1) with the whole product's chunk length (kb_steps)
+    skf_layer<false>(h + c0, ld2, part, ldk, P + a.w_off[1] + (size_t)c0 * K1, nullptr, K1, nc, false, red, wave, lane,
+                     a.zero, nullptr, nullptr, 0, true, 1, (N1 + 3) >> 2);
     skf_lds_barrier();
+    // The partials go through to memory (agent-scope stores, complete once acknowledged) before the
+    // arrival ticket; the LAST slice of this row block sums them in slice order from 0 (skf_layer's
+    // group order), masks with layer 0's activations and stores layer 0's delta.  Nobody waits:
+    // the other slices just leave.
     double* bp = a.bpart + (((size_t)t * a.split + sl) * a.Bmax + r0) * a.maxw;
-    if (ls >= 2) {  // skf_cs_tail sums the partials and runs the remaining layers
-        for (int e = threadIdx.x; e < nr * Kl; e += blockDim.x) {
-            const int r = e / Kl, k = e - r * Kl;
-            bp[(size_t)r * a.maxw + k] = part[r * ldk + k];
-        }
-        return;
-    }
-    // One layer below the split layer (L == 3, sklearn's two-hidden-layer nets): the LAST slice of
-    // this row block to get here sums every slice's partial in slice order, masks it with layer 0's
-    // activations and stores layer 0's delta -- no tail kernel.  The partials go through to memory
-    // (agent-scope stores, complete once acknowledged) before the arrival ticket; the last arriver
-    // reads them with agent-scope loads.  Nobody waits: the other slices just leave.
-    __shared__ int last_s;
-    for (int e = threadIdx.x; e < nr * Kl; e += blockDim.x) {
-        const int r = e / Kl, k = e - r * Kl;
+    for (int e = threadIdx.x; e < nr * K1; e += blockDim.x) {
+        const int r = e / K1, k = e - r * K1;
         __hip_atomic_store(&bp[(size_t)r * a.maxw + k], part[r * ldk + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -712,74 +632,13 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     if (!last_s) return;
     const double* a0 = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;  // layer 0's activations (skf_cs_fwd)
     double* dg = a.deltas + ((size_t)t * a.Bmax + r0) * a.maxw;
-    for (int e = threadIdx.x; e < nr * Kl; e += blockDim.x) {
-        const int r = e / Kl, k = e - r * Kl;
+    for (int e = threadIdx.x; e < nr * K1; e += blockDim.x) {
+        const int r = e / K1, k = e - r * K1;
         double sum = 0.0;
         for (int q = 0; q < a.split; ++q)
             sum += __hip_atomic_load(&a.bpart[(((size_t)t * a.split + q) * a.Bmax + r0 + r) * a.maxw + k],
                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         skf_st(&dg[(size_t)r * a.maxw + k], a0[(size_t)r * a.maxw + k] > 0.0 ? sum : 0.0, a.wthru);
-    }
-}
-
-__global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_tail_kernel(SkfArgs a) {
-    extern __shared__ double lds[];
-    const int t = blockIdx.y, rb = blockIdx.x;
-    if (a.active[t] == 0) return;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
-    const int ls = a.L - 2;
-    const double* P = a.params + (size_t)t * a.P;
-    auto ldof = [&](int l) { return skf_ld(skf_np(a.dims[l])); };
-    auto bufp = [&](int l) {
-        int o = 0;
-        for (int i = 0; i < l; ++i) o += ldof(i) * SKF_RB;
-        return lds + o;
-    };
-    double* red = bufp(a.L + 1);
-    // the activations below the split layer (the masks of the deltas computed here)
-    for (int l = 0; l < ls; ++l) {
-        const int N = a.dims[l + 1], np = skf_np(N);
-        const double* ag = a.acts + (((size_t)l * a.T + t) * a.Bmax + r0) * a.maxw;
-        for (int e = threadIdx.x; e < SKF_RB * np; e += blockDim.x) {
-            const int r = e / np, c = e - r * np;
-            bufp(l + 1)[r * ldof(l + 1) + c] = (r < nr && c < N) ? ag[(size_t)r * a.maxw + c] : 0.0;
-        }
-    }
-    skf_lds_barrier();
-    // delta of layer ls - 1 = (sum of the slices' partials, slice order) masked by its activation
-    {
-        const int K = a.dims[ls], np = skf_np(K);
-        double* d = bufp(ls);
-        for (int e = threadIdx.x; e < SKF_RB * np; e += blockDim.x) {
-            const int r = e / np, k = e - r * np;
-            double v = 0.0;
-            if (r < nr && k < K) {
-                double s = 0.0;
-                for (int q = 0; q < a.split; ++q)
-                    s += a.bpart[(((size_t)t * a.split + q) * a.Bmax + r0 + r) * a.maxw + k];
-                v = d[r * ldof(ls) + k] > 0.0 ? s : 0.0;
-            }
-            d[r * ldof(ls) + k] = v;
-        }
-        skf_lds_barrier();
-        double* dg = a.deltas + (((size_t)(ls - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
-        for (int e = threadIdx.x; e < nr * K; e += blockDim.x) {
-            const int r = e / K, k = e - r * K;
-            skf_st(&dg[(size_t)r * a.maxw + k], d[r * ldof(ls) + k], a.wthru);
-        }
-    }
-    // the remaining layers' backward, as in skf_rowpass
-    for (int l = ls - 1; l >= 1; --l) {
-        const int K = a.dims[l], N = a.dims[l + 1];
-        skf_layer<false>(bufp(l + 1), ldof(l + 1), bufp(l), ldof(l), P + a.w_off[l], nullptr, K, N, false, red, wave,
-                         lane, a.zero, nullptr);
-        skf_lds_barrier();
-        double* dg = a.deltas + (((size_t)(l - 1) * a.T + t) * a.Bmax + r0) * a.maxw;
-        for (int e = threadIdx.x; e < nr * K; e += blockDim.x) {
-            const int r = e / K, c = e - r * K;
-            skf_st(&dg[(size_t)r * a.maxw + c], bufp(l)[r * ldof(l) + c], a.wthru);
-        }
     }
 }
 
@@ -901,9 +760,9 @@ bool skf_supported(const SkfArgs& a) {
     if (a.L < 1 || a.L > SKF_MAXL) return false;
     if (a.dims[a.L] > 16) return false;                // one head tile
     if (skf_lds_bytes(a) > 160 * 1024) return false;   // CDNA4 LDS per workgroup
-    if (a.split > 1) {                                 // column split: narrow head, a hidden layer
-        if (a.L < 2 || a.dims[a.L] > SKF_NARROW || a.cw <= 0 || (a.cw & 15) || a.zpart == nullptr ||
-            (a.L >= 3 && a.bpart == nullptr) || (a.L == 3 && a.arrive == nullptr))
+    if (a.split > 1) {                                 // column split: two hidden layers, narrow head
+        if (a.L != 3 || a.dims[a.L] > SKF_NARROW || a.cw <= 0 || (a.cw & 15) || a.bpart == nullptr ||
+            a.arrive == nullptr)
             return false;
         if (skf_cs_bwd_lds(a) > 160 * 1024) return false;
     }
@@ -917,15 +776,14 @@ bool skf_supported(const SkfArgs& a) {
 hipError_t skf_prepare(const SkfArgs& a) {
     static std::mutex mu;
     static size_t lds_set[64] = {};
-    const size_t lds =
-        std::max(skf_lds_bytes(a), a.split > 1 ? std::max(skf_cs_bwd_lds(a), skf_cs_fwd_lds(a)) : (size_t)0);
+    const size_t lds = std::max(skf_lds_bytes(a), a.split > 1 ? skf_cs_bwd_lds(a) : (size_t)0);
     if (lds <= 64 * 1024) return hipSuccess;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> g(mu);
     if (lds <= lds_set[dev]) return hipSuccess;
     const void* ks[] = {reinterpret_cast<const void*>(skf_rowpass_kernel), reinterpret_cast<const void*>(skf_cs_fwd_kernel),
-                        reinterpret_cast<const void*>(skf_cs_bwd_kernel), reinterpret_cast<const void*>(skf_cs_tail_kernel)};
+                        reinterpret_cast<const void*>(skf_cs_bwd_kernel)};
     for (const void* k : ks) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -945,16 +803,12 @@ hipError_t skf_step_launch(const SkfArgs& a, hipStream_t s) {
     }
     const int nrb = (a.rows + SKF_RB - 1) / SKF_RB;
     if (a.split > 1) {
-        if (std::max(skf_cs_bwd_lds(a), skf_cs_fwd_lds(a)) > 64 * 1024) {
+        if (skf_cs_bwd_lds(a) > 64 * 1024) {
             const hipError_t e = skf_prepare(a);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(skf_cs_fwd_kernel, dim3(nrb, a.split, a.T), dim3(SKF_WAVES * 64), skf_cs_fwd_lds(a), s, a);
+        hipLaunchKernelGGL(skf_cs_fwd_kernel, dim3(nrb, a.split, a.T), dim3(SKF_WAVES * 64), lds, s, a);
         hipLaunchKernelGGL(skf_cs_bwd_kernel, dim3(nrb, a.split, a.T), dim3(SKF_WAVES * 64), skf_cs_bwd_lds(a), s, a);
-        // (L == 3: the last slice of a row block to finish skf_cs_bwd forms the one delta below the
-        // split layer itself)
-        if (a.L >= 4)
-            hipLaunchKernelGGL(skf_cs_tail_kernel, dim3(nrb, a.T), dim3(SKF_WAVES * 64), lds, s, a);
     } else {
         hipLaunchKernelGGL(skf_rowpass_kernel, dim3(nrb, a.T), dim3(SKF_WAVES * 64), lds, s, a);
     }

@@ -186,16 +186,15 @@ class MLPTrainerT {
             if (want && style_ == 1 && mu_ == 0.0 && wd_ == 0.0 && L_ <= SKF_MAXL) {
                 SkfArgs a = fused_args(0, 1);
                 fused_ = skf_supported(a);
-                // column-split row pass (mlp_fused_f64.hip skf_cs_*): FEDMI_SK_SPLIT=S forces S slices
-                // (1 = off), default: the heuristic of skf_pick_split
+                // column-split row pass (mlp_fused_f64.hip skf_cs_*, bit-identical to the one-workgroup
+                // row pass): FEDMI_SK_SPLIT=1 turns it off, >1 forces it where it keeps the sums,
+                // default: skf_pick_split's rule
                 if (fused_) {
                     const char* sp = std::getenv("FEDMI_SK_SPLIT");
                     int S = 1, cw = 0;
                     skf_pick_split(a, sp != nullptr && *sp ? std::atoi(sp) : 0, &S, &cw);
                     if (S > 1) {
-                        const int C = dims_[L_];
-                        TR_CHECK(hipMalloc(&zpart_, (size_t)T_ * S * B_ * C * sizeof(double)));
-                        if (L_ >= 3) TR_CHECK(hipMalloc(&bpart_, (size_t)T_ * S * B_ * maxw_ * sizeof(double)));
+                        TR_CHECK(hipMalloc(&bpart_, (size_t)T_ * S * B_ * maxw_ * sizeof(double)));
                         const size_t na = (size_t)T_ * ((B_ + 15) / 16) * sizeof(int);
                         TR_CHECK(hipMalloc(&arrive_, na));
                         TR_CHECK(hipMemset(arrive_, 0, na));
@@ -225,7 +224,6 @@ class MLPTrainerT {
         drop_graph();
         if (dbg_) (void)hipFree(dbg_);
         if (zero_) (void)hipFree(zero_);
-        if (zpart_) (void)hipFree(zpart_);
         if (bpart_) (void)hipFree(bpart_);
         if (arrive_) (void)hipFree(arrive_);
     }
@@ -351,13 +349,11 @@ class MLPTrainerT {
         a.wt = wt_;
         a.split = split_;
         a.cw = cw_;
-        a.zpart = zpart_;
         a.bpart = bpart_;
         a.arrive = arrive_;
         return a;
     }
     int split_ = 1, cw_ = 0;             // column-split row pass (SkfArgs::split / cw)
-    double* zpart_ = nullptr;            // SkfArgs::zpart / bpart
     double* bpart_ = nullptr;
     int* arrive_ = nullptr;              // SkfArgs::arrive
     unsigned long long* dbg_ = nullptr;  // FEDMI_SK_STAMPS=1: phase stamps of the fused row pass

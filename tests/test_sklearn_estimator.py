@@ -198,3 +198,26 @@ def test_hip_float64_fused_step_equals_layered(data, hl, monkeypatch):
         np.testing.assert_allclose(f.loss_curve_, l.loss_curve_, rtol=1e-11)
         for u, v in zip(f.coefs_ + f.intercepts_, l.coefs_ + l.intercepts_):
             np.testing.assert_allclose(u, v, rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hl,split", [((50, 400), 4), ((50, 200), 4), ((100, 400), 2)])
+def test_hip_float64_column_split_is_bit_identical(data, hl, split, monkeypatch):
+    """The column-split row pass (mlp_fused_f64.hip skf_cs_*: hidden layer 1's columns over
+    `split` workgroups per row block, cut only where the one-workgroup row pass already cuts its
+    sums) gives the one-workgroup row pass's weights bit for bit (FEDMI_SK_SPLIT=1), packed
+    trials included; the epoch loss (an atomic sum over row blocks in both) to rounding."""
+    X, y = data
+    lrs = [0.004, 0.02]
+    mk = lambda: [MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=15, random_state=42,
+                                backend="hip", dtype="float64") for lr in lrs]
+    monkeypatch.setenv("FEDMI_SK_SPLIT", "1")
+    one = fit_packed(mk(), X, y)
+    monkeypatch.delenv("FEDMI_SK_SPLIT")
+    cut = fit_packed(mk(), X, y)
+    for a, b in zip(one, cut):
+        assert a._hip_split == 1 and b._hip_split == split, (a._hip_split, b._hip_split)
+        assert a.n_iter_ == b.n_iter_
+        np.testing.assert_allclose(a.loss_curve_, b.loss_curve_, rtol=1e-13)
+        for u, v in zip(a.coefs_ + a.intercepts_, b.coefs_ + b.intercepts_):
+            np.testing.assert_array_equal(u, v)
