@@ -324,7 +324,22 @@ def main(argv=None):
 
     rows_local = a.rows_per_client or reference_rows(a.total_rows, N, comm.rank)
     rows_total = a.rows_per_client * N if a.rows_per_client else a.total_rows
-    dt, eng, primed, ktrace = timed_rounds(rows_local, rows_total, trace=max(0, a.trace_rounds))
+    from fedmi.parallel.peer import PeerFailure
+    plane_failure = None
+    try:
+        dt, eng, primed, ktrace = timed_rounds(rows_local, rows_total, trace=max(0, a.trace_rounds))
+    except PeerFailure as e:
+        # The xGMI plane reported a failure (a wait timed out): every rank's failure word is set,
+        # so every rank lands here together.  Re-run the timed rounds on the next data plane (RCCL,
+        # else the host) and label the record, instead of ending the run without a number.
+        if N == 1:
+            raise
+        plane_failure = str(e)[:300]
+        print(f"[bench] rank {comm.rank}: {plane_failure}; re-running the timed rounds without the xGMI plane",
+              file=sys.stderr, flush=True)
+        comm.peer_allreduce = False
+        gc.collect()
+        dt, eng, primed, ktrace = timed_rounds(rows_local, rows_total, trace=max(0, a.trace_rounds))
     h = eng.history()
     # every rank must hold the same global model and metric history (raises otherwise: no number
     # is reported for a run whose FedAvg was not FedAvg)
@@ -364,11 +379,14 @@ def main(argv=None):
         if N == 1 and rows_local == REF_TRAIN_ROWS:
             weak = {"value": value, "us_per_round": dt / a.steps * 1e6, "rows_per_client": REF_TRAIN_ROWS}
         else:
-            dtw, engw, _, _ = timed_rounds(REF_TRAIN_ROWS, REF_TRAIN_ROWS * N)
-            weak = {"value": REF_TRAIN_ROWS * N * a.steps / dtw, "us_per_round": dtw / a.steps * 1e6,
-                    "rows_per_client": REF_TRAIN_ROWS, "scaling": "weak",
-                    "replicas_consistent": check_replicas(comm, [engw.global_flat()])}
-            del engw
+            try:
+                dtw, engw, _, _ = timed_rounds(REF_TRAIN_ROWS, REF_TRAIN_ROWS * N)
+                weak = {"value": REF_TRAIN_ROWS * N * a.steps / dtw, "us_per_round": dtw / a.steps * 1e6,
+                        "rows_per_client": REF_TRAIN_ROWS, "scaling": "weak",
+                        "replicas_consistent": check_replicas(comm, [engw.global_flat()])}
+                del engw
+            except PeerFailure as e:   # (every rank raises together: the failure word is on every rank)
+                weak = {"error": f"PeerFailure: {e}"[:400]}
             gc.collect()
     anchor = None
     if not a.no_anchor:
@@ -431,6 +449,8 @@ def main(argv=None):
             "replicas_consistent": replicas_ok,
             "rounds_to_target": None,
         }
+        if plane_failure is not None:
+            rec["data_plane_failure"] = plane_failure
         if N > 1 and design["aggregation"] == "host":
             rec["warning"] = ("FedAvg went through the HOST plane (gloo all-gather, rank-order sums): the xGMI "
                               "peer set-up and the RCCL bootstrap were both unavailable; this is not the device "

@@ -255,6 +255,9 @@ def make_peer_allreduce(comm, n_floats: int, device, timeout_s: Optional[float] 
     return h
 
 
+_TEST_ERROR_FIRED = False
+
+
 class PeerFailure(RuntimeError):
     """A rank of the xGMI data plane failed (timed out waiting for a peer, or aborted)."""
 
@@ -278,6 +281,10 @@ def check_peer_error(h) -> None:
     if h is None:
         return
     word = int(h.error())
+    global _TEST_ERROR_FIRED
+    if not word and not _TEST_ERROR_FIRED and os.environ.get("FEDMI_TEST_PEER_ERROR", "") == "1":
+        _TEST_ERROR_FIRED = True   # test knob: one simulated failure report per process (every rank alike)
+        word = (1 << 16) | (0xFF << 8) | 0xFF
     if word:
         raise PeerFailure("xGMI data plane failed: " + describe_peer_error(word, getattr(h, "timeout_s", None))
                           + "; rounds since then are invalid")

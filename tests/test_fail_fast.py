@@ -345,3 +345,20 @@ def test_bench_labels_the_host_plane():
     rec = json.loads(lines[0])
     assert rec["config"]["data_plane"] == "host" and "HOST plane" in rec["warning"], rec
     assert rec["replicas_consistent"] is True and rec["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_reruns_on_the_next_plane_after_a_peer_failure():
+    """A failure reported on the xGMI plane during the headline's rounds (FEDMI_TEST_PEER_ERROR=1:
+    one simulated report on every rank) does not end the bench without a number: every rank re-runs
+    the timed rounds on the next plane (ranks sharing a GPU: the host) and the record says so."""
+    import json
+    env = dict(os.environ, FEDMI_TEST_PEER_ERROR="1")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu", "--steps", "20", "--warmup", "5",
+                        "--no-convergence", "--no-anchor", "--no-weak"], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=380)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert "xGMI data plane failed" in rec["data_plane_failure"], rec
+    assert rec["config"]["data_plane"] == "host" and rec["replicas_consistent"] is True and rec["value"] > 0
