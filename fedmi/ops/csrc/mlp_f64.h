@@ -74,14 +74,11 @@ struct SkfArgs {
     const double* zero;                     // one 0.0 in device memory (branch-free masked loads)
     double* wt;                             // optional [T][P]: each layer's weights transposed [K][N] (kept by
                                             // the Adam epilogue; read by the forward), nullptr: none
-    // Column-split row pass (mlp_fused_f64.hip skf_cs_*, two hidden layers): split > 1 slices hidden
-    // layer 1's output columns (cw each) over `split` workgroups per row block; bpart
-    // [T][split][Bmax][maxw] carries the slices' partial input gradients of that layer
+    // Tile-split row pass (mlp_fused_f64.hip skf_cs_*, two hidden layers): split > 1 cuts hidden layer
+    // 1's forward and input-gradient products by output tiles over `split` workgroups per row block
     int split, cw;
-    double* bpart;
-    int* arrive;                            // [T][row blocks] arrival tickets of skf_cs_bwd (zeroed; L == 3)
 };
-// Column slice width and count for the last hidden layer of a fused job (split 1: no split).
+// Slices of the tile-split row pass for a fused job (split 1: none; cw is unused, > 0).
 void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw);
 bool skf_supported(const SkfArgs& a);
 size_t skf_lds_bytes(const SkfArgs& a);

@@ -90,9 +90,10 @@ __device__ __forceinline__ double skf_wave_sum(double v) {
 // selected after the load) and every MFMA runs (a zero weight operand, an in-range activation
 // column), so the compiler keeps the next chunk's loads in flight across the current chunk's
 // MFMAs -- with predicated loads / MFMAs it waited for ALL loads before every MFMA.
-// Column-split row pass (skf_cs_* below) extras: `ldwt` = row stride of WT (the full layer's N when
-// W / WT / bias point at a slice of its output columns; 0 = N); `raw` (BWD) = store the product
-// itself instead of masking the activation in dst (a partial over a slice of N, summed later).
+// Split row pass (skf_cs_* below) extras: `ldwt` = row stride of WT (FWD) / of W (BWD) when W / WT /
+// bias point at a slice of the layer's output columns (0: the layer's own N / K); `raw` (BWD) = store
+// the product itself instead of masking the activation in dst; `gmax` caps the k-groups (a slice
+// keeps the whole product's); skf_layer's `kb_steps` keeps the whole product's chunk length.
 template <bool FWD, int KB>
 __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int ld_s, double* __restrict__ dst,
                                              int ld_d, const double* __restrict__ W, const double* __restrict__ bias,
@@ -100,7 +101,7 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
                                              const double* __restrict__ zero, const double* __restrict__ WT,
                                              unsigned long long* dbg = nullptr, int ldwt = 0, bool raw = false,
                                              int gmax = SKF_WAVES) {
-    if (ldwt <= 0) ldwt = N;
+    if (ldwt <= 0) ldwt = FWD ? N : K;   // FWD: row stride of WT [K][N]; BWD: row stride of W [N][K]
     const int lr = lane & 15, lg = lane >> 4;
     if (dbg != nullptr && threadIdx.x == 0) dbg[0] = __builtin_amdgcn_s_memrealtime();
     const int ntiles = FWD ? (N + 15) >> 4 : (K + 15) >> 4;
@@ -125,7 +126,7 @@ __device__ __forceinline__ void skf_layer_kb(const double* __restrict__ src, int
             // FWD reads the transposed copy WT [K][N] when there is one (SkfArgs::wt): 16 consecutive
             // output columns per k-row -- whole cache lines -- instead of 16 rows x 32 bytes
             const double* q = ok ? (FWD ? (WT != nullptr ? WT + (size_t)kk * ldwt + col : W + (size_t)col * K + kk)
-                                        : W + (size_t)kk * K + col)
+                                        : W + (size_t)kk * ldwt + col)
                                  : zero;
             bw[i] = *q;
         }
@@ -400,22 +401,22 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_rowpass_kernel(SkfArgs a) 
 }
 
 // ---------------------------------------------------------------------------------------
-// Column-split row pass (SkfArgs::split = S > 1), BIT-IDENTICAL to skf_rowpass.  skf_rowpass runs
-// one 16-row block on ONE CU and is bound by that CU's float64 MFMA pipes (MFMA busy 67 %): every
-// row block streams and multiplies the whole weight set alone, so a 200-row minibatch uses 13 CUs.
-// For two hidden layers and a narrow head (sklearn's [S] net (50, 400) and the [H] grid's
-// two-layer nets) the second hidden layer's columns are sliced over S workgroups per row block:
+// Tile-split row pass (SkfArgs::split = S > 1), BIT-IDENTICAL to skf_rowpass.  skf_rowpass runs one
+// 16-row block on ONE CU and is bound by that CU's float64 MFMA pipes (MFMA busy 67 %): every row
+// block streams and multiplies the whole weight set alone, so a 200-row minibatch uses 13 CUs.  For
+// two hidden layers and a narrow head (sklearn's [S] net (50, 400) and the [H] grid's two-layer
+// nets) the two products of hidden layer 1 -- its forward (output tiles over its N columns) and its
+// input gradient (output tiles over its K inputs) -- are split by OUTPUT TILES over S workgroups per
+// row block.  Every output tile is a complete sum in one workgroup, with skf_rowpass's chunk length
+// and k-groups for the whole product (kb_steps, gmax), so nothing is re-associated:
 //   skf_cs_fwd  (row block x slice x trial)  gather, hidden layer 0 (every slice recomputes it, slice
-//               0 stores it), hidden layer 1's forward for the slice's columns -> acts
-//   skf_cs_bwd  (row block x slice x trial)  the logits from ALL of layer 1's activations exactly as
-//               skf_fwd_narrow sums them, the loss head, the slice's delta (head delta . W_head, ReLU
-//               mask), the slice's partial input gradient of layer 1; the LAST slice of the row
-//               block to finish sums the S partials in slice order and stores layer 0's delta
-// Same sums as skf_rowpass, bit for bit: a slice is exactly one of the k-groups skf_layer<false>
-// splits layer 1's input gradient into (G groups of bpg chunks, summed in group order from 0), and
-// the forward keeps skf_rowpass's per-tile chains (gmax, kb_steps) -- so the split may only cut
-// where skf_rowpass already cuts (skf_pick_split), and the float64 estimator keeps tracking
-// scikit-learn epoch by epoch (tools/sklearn_parity.py).
+//               0 stores it), the slice's forward tiles of hidden layer 1 -> acts
+//   skf_cs_bwd  (row block x slice x trial)  the logits from ALL of layer 1's activations in
+//               skf_fwd_narrow's order, the loss head, layer 1's delta (skf_bwd_narrow's sums; every
+//               slice, slice 0 stores it), the slice's tiles of layer 1's input gradient masked by
+//               layer 0's activations -> layer 0's delta
+// The weights are therefore those of skf_rowpass bit for bit, and the float64 estimator keeps
+// tracking scikit-learn epoch by epoch (tools/sklearn_parity.py).
 // ---------------------------------------------------------------------------------------
 struct SkfGroups { int KB, nb, G, bpg; };
 // skf_layer_kb's cut of a product: chunk length KB (k-steps), nb chunks per tile, G k-groups of
@@ -429,29 +430,45 @@ __host__ __device__ __forceinline__ SkfGroups skf_groups(int steps, int ntiles) 
     g.bpg = (g.nb + g.G - 1) / g.G;
     return g;
 }
+// Tiles of slice `sl` of a product with `ntiles` output tiles cut into `S` slices: [t0, t0 + n)
+__host__ __device__ __forceinline__ void skf_slice_tiles(int ntiles, int S, int sl, int* t0, int* n) {
+    const int per = (ntiles + S - 1) / S;
+    *t0 = sl * per;
+    const int e = *t0 + per < ntiles ? *t0 + per : ntiles;
+    *n = e > *t0 ? e - *t0 : 0;
+}
 
 void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw) {
     *split = 1;
     *cw = 0;
     if (a.L != 3 || a.dims[a.L] > SKF_NARROW || want == 1) return;
     const int K = a.dims[1], N = a.dims[2];   // hidden layer 1: K -> N
-    // skf_rowpass's input gradient of layer 1: steps over N, tiles over K
-    const SkfGroups g = skf_groups((N + 3) >> 2, (K + 15) >> 4);
-    if (g.G < 2) return;                      // one k-group: no cut that keeps the sums
-    const int w = g.bpg * g.KB * 4;           // columns per k-group (a multiple of 16)
-    const int S = (N + w - 1) / w;
+    const int nt_f = (N + 15) >> 4, nt_b = (K + 15) >> 4;
+    int S = nt_f < nt_b ? nt_f : nt_b;        // every slice owns >= 1 tile of both products
+    if (S > 8) S = 8;
+    if (want > 1) {
+        S = want < S ? want : S;
+    } else {
+        // about one workgroup per CU over all row blocks and trials (more queue behind each other)
+        const int nrb = (a.Bmax + SKF_RB - 1) / SKF_RB;
+        const int by_cus = 256 / std::max(1, nrb * a.T);
+        S = S < by_cus ? S : by_cus;
+    }
+    // every slice must own tiles of both products (the last slice of a ceil-cut can be empty)
+    for (; S >= 2; --S) {
+        int t0, nf, nb;
+        skf_slice_tiles(nt_f, S, S - 1, &t0, &nf);
+        skf_slice_tiles(nt_b, S, S - 1, &t0, &nb);
+        if (nf >= 1 && nb >= 1) break;
+    }
     if (S < 2) return;
-    // slices only while the grid stays within about one workgroup per CU (more queue behind each
-    // other: profiles/sk_split_r6.log); FEDMI_SK_SPLIT=<n> > 1 forces the split
-    const int nrb = (a.Bmax + SKF_RB - 1) / SKF_RB;
-    if (want <= 0 && nrb * a.T * S > 256) return;
     *split = S;
-    *cw = w;
+    *cw = 16;   // (unused by the tile split; kept > 0 for skf_supported)
 }
 
-// LDS of skf_cs_bwd (doubles): layer 1's activations (all columns, the logits' operand; the slice's
-// columns become its delta) [16][ld(N)], the partial input gradient [16][ld(K)], the k-split
-// partials, the head weights + bias
+// LDS of skf_cs_bwd (doubles): layer 1's activations -> its delta [16][ld(N)], layer 0's activations
+// of the slice's input-gradient tiles -> layer 0's delta [16][ld(K)], the k-split partials, the head
+// weights + bias
 static size_t skf_cs_bwd_lds(const SkfArgs& a) {
     const size_t d = (size_t)SKF_RB * skf_ld(skf_np(a.dims[2])) + (size_t)SKF_RB * skf_ld(skf_np(a.dims[1])) +
                      SKF_RED_DOUBLES + (size_t)a.dims[3] * (a.dims[2] + 1);
@@ -465,7 +482,9 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
     const int K1 = a.dims[1], N1 = a.dims[2];
-    const int c0 = sl * a.cw, nc = min(a.cw, N1 - c0);
+    int tf0, ntf;
+    skf_slice_tiles((N1 + 15) >> 4, a.split, sl, &tf0, &ntf);
+    const int c0 = tf0 * 16, nc = min(ntf * 16, N1 - c0);   // this slice's output columns of layer 1
     if (rb == 0 && sl == 0 && threadIdx.x == 0) a.step[t] += 1;  // this minibatch's Adam step
     const double* P = a.params + (size_t)t * a.P;
     auto ldof = [&](int l) { return skf_ld(skf_np(a.dims[l])); };
@@ -497,8 +516,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
             skf_st(&ag[(size_t)r * a.maxw + c], b1[r * ldof(1) + c], a.wthru);
         }
     }
-    // hidden layer 1's forward for output columns [c0, c0 + nc): skf_rowpass's per-tile chains
-    // (its chunk length and k-groups for the whole product)
+    // the slice's output tiles of hidden layer 1's forward, with skf_rowpass's chunking and k-groups
     const SkfGroups gf = skf_groups((K1 + 3) >> 2, (N1 + 15) >> 4);
     skf_layer<true>(b1, ldof(1), b2 + c0, ldof(2), P + a.w_off[1] + (size_t)c0 * K1, P + a.b_off[1] + c0, K1, nc, true,
                     red, wave, lane, a.zero, a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[1] + c0 : nullptr,
@@ -514,18 +532,19 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
 __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     extern __shared__ double lds[];
     __shared__ double dz_s[SKF_RB * SKF_NARROW];
-    __shared__ int last_s;
     const int t = blockIdx.z, sl = blockIdx.y, rb = blockIdx.x;
     if (a.active[t] == 0) return;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int r0 = rb * SKF_RB, nr = min(SKF_RB, a.rows - r0);
     const int K1 = a.dims[1], N1 = a.dims[2], C = a.dims[3];
-    const int c0 = sl * a.cw, nc = min(a.cw, N1 - c0);
+    int tb0, ntb;
+    skf_slice_tiles((K1 + 15) >> 4, a.split, sl, &tb0, &ntb);
+    const int k0 = tb0 * 16, nk = min(ntb * 16, K1 - k0);   // this slice's input-gradient columns
     const double* P = a.params + (size_t)t * a.P;
     const int np2 = skf_np(N1), ld2 = skf_ld(np2), ldk = skf_ld(skf_np(K1));
-    double* h = lds;                       // [16][ld2]: layer 1's activations; the slice's columns -> delta
-    double* part = h + SKF_RB * ld2;       // [16][ldk]: the slice's partial input gradient of layer 1
-    double* red = part + SKF_RB * ldk;
+    double* h = lds;                       // [16][ld2]: layer 1's activations, then its delta
+    double* a0s = h + SKF_RB * ld2;        // [16][ldk]: layer 0's activations of the slice -> its delta
+    double* red = a0s + SKF_RB * ldk;
     double* wh = red + SKF_RED_DOUBLES;    // head weights [C][N1], then its bias [C]
     const double* Wh = P + a.w_off[2];
     for (int e = threadIdx.x; e < C * N1; e += blockDim.x) wh[e] = Wh[e];
@@ -534,6 +553,12 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     for (int e = threadIdx.x; e < SKF_RB * np2; e += blockDim.x) {
         const int r = e / np2, j = e - r * np2;
         h[r * ld2 + j] = (r < nr && j < N1) ? ag[(size_t)r * a.maxw + j] : 0.0;
+    }
+    const double* a0g = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;
+    const int npk = skf_np(nk);
+    for (int e = threadIdx.x; e < SKF_RB * npk; e += blockDim.x) {
+        const int r = e / npk, j = e - r * npk;
+        a0s[r * ldk + j] = (r < nr && j < nk) ? a0g[(size_t)r * a.maxw + k0 + j] : 0.0;
     }
     skf_lds_barrier();
     // logits: skf_fwd_narrow's sums (wave w = row w, lanes over k, xor tree, + bias)
@@ -586,59 +611,32 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
             skf_st(&dg[(size_t)r * a.maxw + c], dz_s[r * C + c], a.wthru);
         }
     }
-    // the slice's delta: skf_bwd_narrow's sums over the slice's columns, ReLU mask, in place
-    const int npc = skf_np(nc);
-    for (int e = threadIdx.x; e < SKF_RB * npc; e += blockDim.x) {
-        const int r = e / npc, j = e - r * npc, k = c0 + j;
-        double v = 0.0;
-        if (j < nc) {
-            double sum = 0.0;
-            for (int n = 0; n < C; ++n) sum += dz_s[r * C + n] * wh[n * N1 + k];
-            v = h[r * ld2 + k] > 0.0 ? sum : 0.0;
-        }
-        if (k < np2) h[r * ld2 + k] = v;
-    }
-    skf_lds_barrier();
-    {
-        double* dg = a.deltas + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw + c0;
-        for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
-            const int r = e / nc, j = e - r * nc;
-            skf_st(&dg[(size_t)r * a.maxw + j], h[r * ld2 + c0 + j], a.wthru);
-        }
-    }
-    // the slice's partial input gradient of layer 1 = ONE of skf_rowpass's k-groups: one group
-    // (gmax 1) with the whole product's chunk length (kb_steps)
-    skf_layer<false>(h + c0, ld2, part, ldk, P + a.w_off[1] + (size_t)c0 * K1, nullptr, K1, nc, false, red, wave, lane,
-                     a.zero, nullptr, nullptr, 0, true, 1, (N1 + 3) >> 2);
-    skf_lds_barrier();
-    // The partials go through to memory (agent-scope stores, complete once acknowledged) before the
-    // arrival ticket; the LAST slice of this row block sums them in slice order from 0 (skf_layer's
-    // group order), masks with layer 0's activations and stores layer 0's delta.  Nobody waits:
-    // the other slices just leave.
-    double* bp = a.bpart + (((size_t)t * a.split + sl) * a.Bmax + r0) * a.maxw;
-    for (int e = threadIdx.x; e < nr * K1; e += blockDim.x) {
-        const int r = e / K1, k = e - r * K1;
-        __hip_atomic_store(&bp[(size_t)r * a.maxw + k], part[r * ldk + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int* cnt = a.arrive + (size_t)t * gridDim.x + rb;
-        const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_s = prev == a.split - 1;
-        if (last_s) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next step's ticket
-    }
-    __syncthreads();
-    if (!last_s) return;
-    const double* a0 = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;  // layer 0's activations (skf_cs_fwd)
-    double* dg = a.deltas + ((size_t)t * a.Bmax + r0) * a.maxw;
-    for (int e = threadIdx.x; e < nr * K1; e += blockDim.x) {
-        const int r = e / K1, k = e - r * K1;
+    // layer 1's delta, every column (skf_bwd_narrow's sums, ReLU mask), in place
+    for (int e = threadIdx.x; e < SKF_RB * np2; e += blockDim.x) {
+        const int r = e / np2, k = e - r * np2;
         double sum = 0.0;
-        for (int q = 0; q < a.split; ++q)
-            sum += __hip_atomic_load(&a.bpart[(((size_t)t * a.split + q) * a.Bmax + r0 + r) * a.maxw + k],
-                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        skf_st(&dg[(size_t)r * a.maxw + k], a0[(size_t)r * a.maxw + k] > 0.0 ? sum : 0.0, a.wthru);
+        for (int n = 0; n < C; ++n) sum += dz_s[r * C + n] * (k < N1 ? wh[n * N1 + k] : 0.0);
+        double* p = h + r * ld2 + k;
+        *p = (k < N1 && *p > 0.0) ? sum : 0.0;
+    }
+    skf_lds_barrier();
+    if (sl == 0) {  // layer 1's delta: the wgrad operand of layer 1
+        double* dg = a.deltas + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw;
+        for (int e = threadIdx.x; e < nr * N1; e += blockDim.x) {
+            const int r = e / N1, c = e - r * N1;
+            skf_st(&dg[(size_t)r * a.maxw + c], h[r * ld2 + c], a.wthru);
+        }
+    }
+    // the slice's tiles of layer 1's input gradient, masked in place over layer 0's activations:
+    // skf_rowpass's chunk length and k-groups for the whole product (each tile a complete sum)
+    const SkfGroups gb = skf_groups((N1 + 3) >> 2, (K1 + 15) >> 4);
+    skf_layer<false>(h, ld2, a0s, ldk, P + a.w_off[1] + k0, nullptr, nk, N1, false, red, wave, lane, a.zero, nullptr,
+                     nullptr, K1, false, gb.G, (N1 + 3) >> 2);
+    skf_lds_barrier();
+    double* dg = a.deltas + ((size_t)t * a.Bmax + r0) * a.maxw + k0;
+    for (int e = threadIdx.x; e < nr * nk; e += blockDim.x) {
+        const int r = e / nk, j = e - r * nk;
+        skf_st(&dg[(size_t)r * a.maxw + j], a0s[r * ldk + j], a.wthru);
     }
 }
 
@@ -760,10 +758,8 @@ bool skf_supported(const SkfArgs& a) {
     if (a.L < 1 || a.L > SKF_MAXL) return false;
     if (a.dims[a.L] > 16) return false;                // one head tile
     if (skf_lds_bytes(a) > 160 * 1024) return false;   // CDNA4 LDS per workgroup
-    if (a.split > 1) {                                 // column split: two hidden layers, narrow head
-        if (a.L != 3 || a.dims[a.L] > SKF_NARROW || a.cw <= 0 || (a.cw & 15) || a.bpart == nullptr ||
-            a.arrive == nullptr)
-            return false;
+    if (a.split > 1) {                                 // tile split: two hidden layers, narrow head
+        if (a.L != 3 || a.dims[a.L] > SKF_NARROW) return false;
         if (skf_cs_bwd_lds(a) > 160 * 1024) return false;
     }
     return true;

@@ -186,18 +186,14 @@ class MLPTrainerT {
             if (want && style_ == 1 && mu_ == 0.0 && wd_ == 0.0 && L_ <= SKF_MAXL) {
                 SkfArgs a = fused_args(0, 1);
                 fused_ = skf_supported(a);
-                // column-split row pass (mlp_fused_f64.hip skf_cs_*, bit-identical to the one-workgroup
-                // row pass): FEDMI_SK_SPLIT=1 turns it off, >1 forces it where it keeps the sums,
-                // default: skf_pick_split's rule
+                // tile-split row pass (mlp_fused_f64.hip skf_cs_*, bit-identical to the one-workgroup
+                // row pass): FEDMI_SK_SPLIT=1 turns it off, S > 1 asks for S slices, default:
+                // skf_pick_split's rule
                 if (fused_) {
                     const char* sp = std::getenv("FEDMI_SK_SPLIT");
                     int S = 1, cw = 0;
                     skf_pick_split(a, sp != nullptr && *sp ? std::atoi(sp) : 0, &S, &cw);
                     if (S > 1) {
-                        TR_CHECK(hipMalloc(&bpart_, (size_t)T_ * S * B_ * maxw_ * sizeof(double)));
-                        const size_t na = (size_t)T_ * ((B_ + 15) / 16) * sizeof(int);
-                        TR_CHECK(hipMalloc(&arrive_, na));
-                        TR_CHECK(hipMemset(arrive_, 0, na));
                         split_ = S;
                         cw_ = cw;
                         if (!skf_supported(fused_args(0, 1))) {  // (LDS of the split kernels): no split
@@ -224,8 +220,6 @@ class MLPTrainerT {
         drop_graph();
         if (dbg_) (void)hipFree(dbg_);
         if (zero_) (void)hipFree(zero_);
-        if (bpart_) (void)hipFree(bpart_);
-        if (arrive_) (void)hipFree(arrive_);
     }
     int split() const { return split_; }
     // Last fused row pass's phase stamps (FEDMI_SK_STAMPS=1), microseconds since its start.
@@ -349,13 +343,9 @@ class MLPTrainerT {
         a.wt = wt_;
         a.split = split_;
         a.cw = cw_;
-        a.bpart = bpart_;
-        a.arrive = arrive_;
         return a;
     }
-    int split_ = 1, cw_ = 0;             // column-split row pass (SkfArgs::split / cw)
-    double* bpart_ = nullptr;
-    int* arrive_ = nullptr;              // SkfArgs::arrive
+    int split_ = 1, cw_ = 0;             // tile-split row pass (SkfArgs::split / cw)
     unsigned long long* dbg_ = nullptr;  // FEDMI_SK_STAMPS=1: phase stamps of the fused row pass
     double* zero_ = nullptr;             // SkfArgs::zero
     double* wt_ = nullptr;               // SkfArgs::wt (bufs["wt"], optional)

@@ -201,12 +201,14 @@ def test_hip_float64_fused_step_equals_layered(data, hl, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hl,split", [((50, 400), 4), ((50, 200), 4), ((100, 400), 2)])
-def test_hip_float64_column_split_is_bit_identical(data, hl, split, monkeypatch):
-    """The column-split row pass (mlp_fused_f64.hip skf_cs_*: hidden layer 1's columns over
-    `split` workgroups per row block, cut only where the one-workgroup row pass already cuts its
-    sums) gives the one-workgroup row pass's weights bit for bit (FEDMI_SK_SPLIT=1), packed
-    trials included; the epoch loss (an atomic sum over row blocks in both) to rounding."""
+@pytest.mark.parametrize("hl,split", [((50, 400), 4), ((50, 200), 4), ((100, 400), 7), ((400, 200), 7),
+                                      ((200, 100), 7)])
+def test_hip_float64_tile_split_is_bit_identical(data, hl, split, monkeypatch):
+    """The tile-split row pass (mlp_fused_f64.hip skf_cs_*: hidden layer 1's forward and input
+    gradient cut by output tiles over `split` workgroups per row block, every tile a whole sum with
+    the one-workgroup row pass's chunking) gives the one-workgroup row pass's weights bit for bit
+    (FEDMI_SK_SPLIT=1), packed trials included; the epoch loss (an atomic sum over row blocks in
+    both) to rounding."""
     X, y = data
     lrs = [0.004, 0.02]
     mk = lambda: [MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=15, random_state=42,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# sklearn float64 estimator on the GPU: parity tests, then the minibatch step with the column-split row pass off
+# sklearn float64 estimator on the GPU: parity tests, then the minibatch step with the tile-split row pass off
 # (FEDMI_SK_SPLIT=1) and at its default, then the kernel split of the [S] step under rocprofv3.
 export FEDMI_NO_BUILD=1
 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_sklearn_estimator.py -m gpu 2>&1 | tail -3 || exit 1

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Interleaved A/B of the column-split row pass (FEDMI_SK_SPLIT=1: off, "": default heuristic, or a slice count)
+# Interleaved A/B of the tile-split row pass (FEDMI_SK_SPLIT=1: off, "": default heuristic, or a slice count)
 # on the sklearn minibatch step.  Usage (GPU box): tools/sk_split_env_ab.sh <reps> <case> <split>...
 export FEDMI_NO_BUILD=1
 reps=$1; case=$2; shift 2

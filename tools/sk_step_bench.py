@@ -34,7 +34,8 @@ def main():
     from fedmi.data.tabular import load_tabular
     ds = load_tabular(with_mean=False)
     X, y = ds.X_train, ds.y_train
-    cases = [((50, 400), 1, 40), ((400, 200), 9, 10), ((50,), 9, 40), ((50, 400), 9, 20)]
+    cases = [((50, 400), 1, 40), ((400, 200), 9, 10), ((50,), 9, 40), ((50, 400), 9, 20), ((400, 200), 1, 40),
+             ((100, 400), 9, 20)]
     for i, arg in enumerate(sys.argv):
         if arg == "--case":
             cases = [cases[int(sys.argv[i + 1])]]
