@@ -723,28 +723,33 @@ __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) g4[j] = ((part[0][lane][j] + part[1][lane][j]) + part[2][lane][j]) + part[3][lane][j];
     const double wdec = a.alpha * a.inv_rows;
+    const bool coef = k0 + lr < K;   // a coefficient (not a bias): L2 term, and its loss
     double sq = 0.0;
+    // every update computed before the first store, the stores back to back (computed between the
+    // stores, each update waited for the previous one's: 0.4-0.7 us per step, profiles/sk_tile_split_ab_r6.log)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        if (!pok[j]) continue;
-        const size_t i = pidx[j];
-        double p = pp[j];
-        double g = g4[j];
-        if (k0 + lr < K) {  // coefficient: L2 term, and its loss
+        double p = pp[j], g = g4[j];
+        if (coef && pok[j]) {
             sq += p * p;
             g += wdec * p;
         }
-        double m = pm[j], v = pv[j];
-        m = a.beta1 * m + (1.0 - a.beta1) * g;
-        v = a.beta2 * v + (1.0 - a.beta2) * g * g;
-        p = p - lr_t * m / (sqrt(v) + a.eps);
-        M[i] = m;
-        V[i] = v;
-        P[i] = p;
-        if (a.wt != nullptr && k0 + lr < K)  // the transposed copy the forward reads
-            a.wt[(size_t)t * a.P + a.w_off[l] + (size_t)(k0 + lr) * N + (n0 + lg + 4 * j)] = p;
+        const double m = a.beta1 * pm[j] + (1.0 - a.beta1) * g;
+        const double v = a.beta2 * pv[j] + (1.0 - a.beta2) * g * g;
+        pm[j] = m;
+        pv[j] = v;
+        pp[j] = p - lr_t * m / (sqrt(v) + a.eps);
     }
     sq = skf_wave_sum(sq);
+    double* wtl = a.wt != nullptr && coef ? a.wt + (size_t)t * a.P + a.w_off[l] + (size_t)(k0 + lr) * N + n0 + lg : nullptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (!pok[j]) continue;
+        M[pidx[j]] = pm[j];
+        V[pidx[j]] = pv[j];
+        P[pidx[j]] = pp[j];
+        if (wtl != nullptr) wtl[4 * j] = pp[j];   // the transposed copy the forward reads
+    }
     if (lane == 0 && a.l2_coef != 0.0) atomicAdd(&a.loss_acc[t], a.l2_coef * sq);
 }
 
