@@ -264,7 +264,8 @@ __device__ __forceinline__ void skf_bwd_narrow(const double* __restrict__ d, int
     }
 }
 
-// phase stamps (profiling, SkfArgs::dbg): thread 0 of row block (0, 0), 100 MHz clock
+// phase stamps (profiling, SkfArgs::dbg): thread 0 of row block (0, 0), 100 MHz clock; the tile split's
+// skf_cs_fwd writes 0-4, skf_cs_bwd 5-10 (a stamp's store makes later code wait for it: they perturb)
 #define SKF_STAMP(i)                                                                              \
     do {                                                                                          \
         if (a.dbg != nullptr && threadIdx.x == 0 && rb == 0 && blockIdx.y == 0)                   \
@@ -485,6 +486,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
     int tf0, ntf;
     skf_slice_tiles((N1 + 15) >> 4, a.split, sl, &tf0, &ntf);
     const int c0 = tf0 * 16, nc = min(ntf * 16, N1 - c0);   // this slice's output columns of layer 1
+    SKF_STAMP(0);
     if (rb == 0 && sl == 0 && threadIdx.x == 0) a.step[t] += 1;  // this minibatch's Adam step
     const double* P = a.params + (size_t)t * a.P;
     auto ldof = [&](int l) { return skf_ld(skf_np(a.dims[l])); };
@@ -505,10 +507,12 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
         b0[r * ldof(0) + f] = v;
     }
     skf_lds_barrier();
+    SKF_STAMP(1);
     // hidden layer 0, whole (the same call as skf_rowpass); slice 0 stores it
     skf_layer<true>(b0, ldof(0), b1, ldof(1), P + a.w_off[0], P + a.b_off[0], F, K1, true, red, wave, lane, a.zero,
                     a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[0] : nullptr);
     skf_lds_barrier();
+    SKF_STAMP(2);
     if (sl == 0) {
         double* ag = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;
         for (int e = threadIdx.x; e < nr * K1; e += blockDim.x) {
@@ -522,11 +526,14 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
                     red, wave, lane, a.zero, a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[1] + c0 : nullptr,
                     nullptr, N1, false, gf.G, (K1 + 3) >> 2);
     skf_lds_barrier();
+    SKF_STAMP(3);
     double* ag = a.acts + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw + c0;
     for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
         const int r = e / nc, j = e - r * nc;
         skf_st(&ag[(size_t)r * a.maxw + j], b2[r * ldof(2) + c0 + j], a.wthru);
     }
+    if (a.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SKF_STAMP(4);
 }
 
 __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
@@ -540,6 +547,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     int tb0, ntb;
     skf_slice_tiles((K1 + 15) >> 4, a.split, sl, &tb0, &ntb);
     const int k0 = tb0 * 16, nk = min(ntb * 16, K1 - k0);   // this slice's input-gradient columns
+    SKF_STAMP(5);
     const double* P = a.params + (size_t)t * a.P;
     const int np2 = skf_np(N1), ld2 = skf_ld(np2), ldk = skf_ld(skf_np(K1));
     double* h = lds;                       // [16][ld2]: layer 1's activations, then its delta
@@ -561,6 +569,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
         a0s[r * ldk + j] = (r < nr && j < nk) ? a0g[(size_t)r * a.maxw + k0 + j] : 0.0;
     }
     skf_lds_barrier();
+    SKF_STAMP(6);
     // logits: skf_fwd_narrow's sums (wave w = row w, lanes over k, xor tree, + bias)
     {
         const int r = wave;
@@ -572,6 +581,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
         }
     }
     skf_lds_barrier();
+    SKF_STAMP(7);
     // loss head (skf_rowpass's): the logits become the head delta in place
     double lrow = 0.0;
     if (threadIdx.x < SKF_RB) {
@@ -620,6 +630,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
         *p = (k < N1 && *p > 0.0) ? sum : 0.0;
     }
     skf_lds_barrier();
+    SKF_STAMP(8);
     if (sl == 0) {  // layer 1's delta: the wgrad operand of layer 1
         double* dg = a.deltas + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw;
         for (int e = threadIdx.x; e < nr * N1; e += blockDim.x) {
@@ -633,11 +644,14 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     skf_layer<false>(h, ld2, a0s, ldk, P + a.w_off[1] + k0, nullptr, nk, N1, false, red, wave, lane, a.zero, nullptr,
                      nullptr, K1, false, gb.G, (N1 + 3) >> 2);
     skf_lds_barrier();
+    SKF_STAMP(9);
     double* dg = a.deltas + ((size_t)t * a.Bmax + r0) * a.maxw + k0;
     for (int e = threadIdx.x; e < nr * nk; e += blockDim.x) {
         const int r = e / nk, j = e - r * nk;
         skf_st(&dg[(size_t)r * a.maxw + j], a0s[r * ldk + j], a.wthru);
     }
+    if (a.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SKF_STAMP(10);
 }
 
 // One 16 x 16 tile of one layer's gradient [N][K + 1] (column K = bias) per workgroup; the 4
