@@ -76,10 +76,11 @@ struct SkfArgs {
                                             // the Adam epilogue; read by the forward), nullptr: none
     // Tile-split row pass (mlp_fused_f64.hip skf_cs_*, two hidden layers): split > 1 cuts hidden layer
     // 1's forward and input-gradient products by output tiles over `split` workgroups per row block
-    int split, cw;
+    int split;
 };
-// Slices of the tile-split row pass for a fused job (split 1: none; cw is unused, > 0).
-void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw);
+// Slices of the tile-split row pass for a fused job (1: none) on a device with `cus` CUs; `want`:
+// 0 = the rule, 1 = off, > 1 = at most that many.
+int skf_pick_split(const SkfArgs& a, int want, int cus);
 bool skf_supported(const SkfArgs& a);
 size_t skf_lds_bytes(const SkfArgs& a);
 hipError_t skf_prepare(const SkfArgs& a);

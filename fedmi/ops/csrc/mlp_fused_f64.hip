@@ -439,10 +439,8 @@ __host__ __device__ __forceinline__ void skf_slice_tiles(int ntiles, int S, int 
     *n = e > *t0 ? e - *t0 : 0;
 }
 
-void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw) {
-    *split = 1;
-    *cw = 0;
-    if (a.L != 3 || a.dims[a.L] > SKF_NARROW || want == 1) return;
+int skf_pick_split(const SkfArgs& a, int want, int cus) {
+    if (a.L != 3 || a.dims[a.L] > SKF_NARROW || want == 1) return 1;
     const int K = a.dims[1], N = a.dims[2];   // hidden layer 1: K -> N
     const int nt_f = (N + 15) >> 4, nt_b = (K + 15) >> 4;
     int S = nt_f < nt_b ? nt_f : nt_b;        // every slice owns >= 1 tile of both products
@@ -450,9 +448,10 @@ void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw) {
     if (want > 1) {
         S = want < S ? want : S;
     } else {
-        // about one workgroup per CU over all row blocks and trials (more queue behind each other)
+        // about one workgroup per CU over all row blocks and trials (more queue behind each other:
+        // profiles/sk_tile_split_ab_r6.log)
         const int nrb = (a.Bmax + SKF_RB - 1) / SKF_RB;
-        const int by_cus = 256 / std::max(1, nrb * a.T);
+        const int by_cus = std::max(1, cus) / std::max(1, nrb * a.T);
         S = S < by_cus ? S : by_cus;
     }
     // every slice must own tiles of both products (the last slice of a ceil-cut can be empty)
@@ -462,9 +461,7 @@ void skf_pick_split(const SkfArgs& a, int want, int* split, int* cw) {
         skf_slice_tiles(nt_b, S, S - 1, &t0, &nb);
         if (nf >= 1 && nb >= 1) break;
     }
-    if (S < 2) return;
-    *split = S;
-    *cw = 16;   // (unused by the tile split; kept > 0 for skf_supported)
+    return S < 2 ? 1 : S;
 }
 
 // LDS of skf_cs_bwd (doubles): layer 1's activations -> its delta [16][ld(N)], layer 0's activations

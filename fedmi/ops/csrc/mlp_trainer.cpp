@@ -191,15 +191,14 @@ class MLPTrainerT {
                 // skf_pick_split's rule
                 if (fused_) {
                     const char* sp = std::getenv("FEDMI_SK_SPLIT");
-                    int S = 1, cw = 0;
-                    skf_pick_split(a, sp != nullptr && *sp ? std::atoi(sp) : 0, &S, &cw);
+                    int cus = 0, dev = 0;
+                    if (hipGetDevice(&dev) != hipSuccess ||
+                        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                        cus = 0;
+                    const int S = skf_pick_split(a, sp != nullptr && *sp ? std::atoi(sp) : 0, cus);
                     if (S > 1) {
                         split_ = S;
-                        cw_ = cw;
-                        if (!skf_supported(fused_args(0, 1))) {  // (LDS of the split kernels): no split
-                            split_ = 1;
-                            cw_ = 0;
-                        }
+                        if (!skf_supported(fused_args(0, 1))) split_ = 1;   // (LDS of the split kernels): no split
                     }
                 }
             }
@@ -342,10 +341,9 @@ class MLPTrainerT {
         a.zero = zero_;
         a.wt = wt_;
         a.split = split_;
-        a.cw = cw_;
         return a;
     }
-    int split_ = 1, cw_ = 0;             // tile-split row pass (SkfArgs::split / cw)
+    int split_ = 1;                      // tile-split row pass (SkfArgs::split)
     unsigned long long* dbg_ = nullptr;  // FEDMI_SK_STAMPS=1: phase stamps of the fused row pass
     double* zero_ = nullptr;             // SkfArgs::zero
     double* wt_ = nullptr;               // SkfArgs::wt (bufs["wt"], optional)
