@@ -189,6 +189,7 @@ def main(argv=None):
     # RCCL protocol pinned per workload: LL for the fused engine's small FedAvg images, Simple
     # for the wide MLP's large buckets (fedmi.parallel.comm.pin_rccl_env)
     comm = get_world(backend=a.backend, device=a.device, rccl_proto="Simple" if a.wide else "LL")
+    t_comm = time.perf_counter()
     if a.wide:
         return main_wide(a, comm)
     rank, size = comm.Get_rank(), comm.Get_size()
@@ -197,6 +198,7 @@ def main(argv=None):
 
     # every rank derives the same split locally: no broadcast of the table (C:243-246)
     ds = _dataset(a, comm) if a.synthetic else load_tabular(a.data, label=a.label, with_mean=True)
+    t_data = time.perf_counter()
     cfg = EngineConfig(hidden=tuple(a.hidden), lr=a.lr, step_size=a.step_size, gamma=a.gamma,
                        local_steps=a.local_steps, prox_mu=a.fedprox_mu, participation=a.participation, early_stop=not a.no_early_stop,
                        patience=a.patience, tolerance=a.tolerance, max_rounds=a.rounds,
@@ -207,6 +209,7 @@ def main(argv=None):
                                    shard_mode=a.partition, alpha=a.alpha, presharded=a.synthetic,
                                    output_size=2 if a.synthetic else None,
                                    n_total=a.synthetic_rows * size if a.synthetic else None)
+    t_setup = time.perf_counter()
     done = 0   # rounds restored from a checkpoint (not run by this process)
     if a.resume:
         done = resume(a.resume, trainer)
@@ -250,6 +253,8 @@ def main(argv=None):
         wall = time.perf_counter() - t_main
         print(f"main() wall {wall:.3f} s for {rounds_run} rounds ({t_train:.3f} s in train_and_evaluate): "
               f"e2e {len(trainer.X_local) * rounds_run / wall:,.0f} samples/s/client", flush=True)
+        print(f"main() phases: communicator {t_comm - t_main:.3f} s, data {t_data - t_comm:.3f} s, "
+              f"trainer set-up {t_setup - t_data:.3f} s, train_and_evaluate {t_train:.3f} s", flush=True)
     comm.close()
     return global_metrics
 
