@@ -192,9 +192,10 @@ def main(argv=None):
     ap.add_argument("--no-plane-companions", action="store_true",
                     help="N > 1 on the xGMI plane: skip the untimed-for-the-headline companions that time the same "
                          "shard with the pull protocol (FEDMI_PEER_LL=0) and with classic rounds (lagged_eval off)")
-    ap.add_argument("--companion-timeout", type=float, default=180.0,
-                    help="seconds the untimed extras (rounds-to-target, the N > 1 plane companions) may take before "
-                         "a watchdog prints the headline record and exits")
+    ap.add_argument("--companion-timeout", type=float, default=300.0,
+                    help="seconds the untimed extras (the weak-scaling companion, the eager anchor, the fp32 round, "
+                         "rounds-to-target, the N > 1 plane companions) may take before a watchdog prints the "
+                         "headline record and exits with status 3")
     ap.add_argument("--no-convergence", action="store_true")
     ap.add_argument("--no-anchor", action="store_true", help="skip the same-box eager torch anchor")
     ap.add_argument("--no-fp32", action="store_true", help="skip the untimed fp32-kernel round (one client)")
@@ -373,34 +374,6 @@ def main(argv=None):
     del eng
     gc.collect()
     torch.cuda.synchronize(dev)
-    # companion: per-GPU work fixed at the reference's one-client shard (8000 rows on every client)
-    weak = None
-    if not a.rows_per_client and not a.no_weak:
-        if N == 1 and rows_local == REF_TRAIN_ROWS:
-            weak = {"value": value, "us_per_round": dt / a.steps * 1e6, "rows_per_client": REF_TRAIN_ROWS}
-        else:
-            try:
-                dtw, engw, _, _ = timed_rounds(REF_TRAIN_ROWS, REF_TRAIN_ROWS * N)
-                weak = {"value": REF_TRAIN_ROWS * N * a.steps / dtw, "us_per_round": dtw / a.steps * 1e6,
-                        "rows_per_client": REF_TRAIN_ROWS, "scaling": "weak",
-                        "replicas_consistent": check_replicas(comm, [engw.global_flat()])}
-                del engw
-            except PeerFailure as e:   # (every rank raises together: the failure word is on every rank)
-                weak = {"error": f"PeerFailure: {e}"[:400]}
-            gc.collect()
-    anchor = None
-    if not a.no_anchor:
-        if comm.rank == 0:
-            anchor = torch_eager_anchor(X, y, dims)
-        barrier()
-    fp32_us = None
-    if N == 1 and a.dtype != "fp32" and not a.no_fp32:
-        # the reference-precision companion, timed EXACTLY like the headline: same shard, same
-        # --warmup / --steps, early-stop rule live, one graph replay of the timed steps
-        dtf, engf, _, _ = timed_rounds(rows_local, rows_total, dtype="fp32")
-        fp32_us = dtf / a.steps * 1e6
-        del engf
-        gc.collect()
     rec = None
     if comm.rank == 0:
         rec = {
@@ -442,9 +415,9 @@ def main(argv=None):
             "us_per_round": dt / a.steps * 1e6,
             "kernel_trace_us": ktrace,
             "plane_companions": None,
-            "weak_8000_rows_per_client": weak,
-            "torch_eager_us_per_round_1client": anchor,
-            "fp32_us_per_round": fp32_us if a.dtype != "fp32" else dt / a.steps * 1e6,
+            "weak_8000_rows_per_client": None,
+            "torch_eager_us_per_round_1client": None,
+            "fp32_us_per_round": None if a.dtype != "fp32" else dt / a.steps * 1e6,
             "final_train_acc_synthetic": design["final_acc"],
             "replicas_consistent": replicas_ok,
             "rounds_to_target": None,
@@ -455,11 +428,51 @@ def main(argv=None):
             rec["warning"] = ("FedAvg went through the HOST plane (gloo all-gather, rank-order sums): the xGMI "
                               "peer set-up and the RCCL bootstrap were both unavailable; this is not the device "
                               "data plane's number")
-    # The untimed extras run last under a watchdog: the headline record is complete now, and rank 0
-    # prints it exactly once whatever happens to them (an extra that raises is recorded; one stuck
-    # in a collective or a peer wait ends the process when the budget runs out).
+    # The untimed extras run under a watchdog once the headline record exists: rank 0 prints it
+    # exactly once whatever happens to them (an extra that raises is recorded; one stuck in a
+    # collective or a peer wait ends the process when the budget runs out) -- the weak-scaling
+    # companion, the eager anchor and the fp32 round included, so no extra can cost the headline.
     emit = _Emitter(rec)
     emit.arm(a.companion_timeout)
+    # companion: per-GPU work fixed at the reference's one-client shard (8000 rows on every client)
+    emit.stage = "weak_8000_rows_per_client"
+    weak = None
+    if not a.rows_per_client and not a.no_weak:
+        if N == 1 and rows_local == REF_TRAIN_ROWS:
+            weak = {"value": value, "us_per_round": dt / a.steps * 1e6, "rows_per_client": REF_TRAIN_ROWS}
+        else:
+            try:
+                dtw, engw, _, _ = timed_rounds(REF_TRAIN_ROWS, REF_TRAIN_ROWS * N)
+                weak = {"value": REF_TRAIN_ROWS * N * a.steps / dtw, "us_per_round": dtw / a.steps * 1e6,
+                        "rows_per_client": REF_TRAIN_ROWS, "scaling": "weak",
+                        "replicas_consistent": check_replicas(comm, [engw.global_flat()])}
+                del engw
+            except Exception as e:  # noqa: BLE001 -- recorded; a PeerFailure is raised on every rank together
+                weak = {"error": f"{type(e).__name__}: {e}"[:400]}
+            gc.collect()
+    if rec is not None:
+        rec["weak_8000_rows_per_client"] = weak
+    if not a.no_anchor:
+        emit.stage = "torch_eager_us_per_round_1client"
+        if comm.rank == 0:
+            try:
+                rec["torch_eager_us_per_round_1client"] = torch_eager_anchor(X, y, dims)
+            except Exception as e:  # noqa: BLE001
+                rec["torch_eager_us_per_round_1client"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+        barrier()
+    if N == 1 and a.dtype != "fp32" and not a.no_fp32:
+        # the reference-precision companion, timed EXACTLY like the headline: same shard, same
+        # --warmup / --steps, early-stop rule live, one graph replay of the timed steps
+        emit.stage = "fp32_us_per_round"
+        try:
+            dtf, engf, _, _ = timed_rounds(rows_local, rows_total, dtype="fp32")
+            if rec is not None:
+                rec["fp32_us_per_round"] = dtf / a.steps * 1e6
+            del engf
+        except Exception as e:  # noqa: BLE001 -- one client: nothing collective to leave behind
+            if rec is not None:
+                rec["fp32_us_per_round"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+        gc.collect()
     if not a.no_convergence:
         emit.stage = "rounds_to_target"
         ok = True
@@ -548,8 +561,10 @@ class _Emitter:
         with self.lock:
             if self.rec is not None and not self.done:
                 msg = f"watchdog: {stage} exceeded the extras' time budget"
-                key = "rounds_to_target" if stage == "rounds_to_target" else "plane_companions"
-                self.rec[key] = {**(self.rec.get(key) or {}), "error": msg}
+                # filed under the running extra's own field (the plane companions share one)
+                key = stage.split(".")[0] if stage.split(".")[0] in self.rec else "plane_companions"
+                prev = self.rec.get(key)
+                self.rec[key] = {**(prev if isinstance(prev, dict) else {}), "error": msg}
                 self.rec["watchdog"] = {"fired": True, "stage": stage}
         self.emit()
         print(f"[bench] rank {os.environ.get('RANK', '0')}: watchdog fired during {stage}", file=sys.stderr, flush=True)

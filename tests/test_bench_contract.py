@@ -128,13 +128,16 @@ def test_record_emitter_prints_once_and_watchdog_exits():
     assert "watchdog fired during plane_companions.ll_pull" in p.stderr
 
 
-def test_watchdog_names_rounds_to_target():
-    """A watchdog that fires during rounds-to-target records it there (not as a companion error)."""
+@pytest.mark.parametrize("stage", ["rounds_to_target", "weak_8000_rows_per_client", "fp32_us_per_round",
+                                   "torch_eager_us_per_round_1client"])
+def test_watchdog_names_the_running_extra(stage):
+    """A watchdog that fires during an untimed extra (every one runs after the headline record
+    exists) files the error under that extra's own field, not as a plane-companion error."""
     code = ("import sys, time; sys.path.insert(0, %r); import bench; "
-            "w = bench._Emitter({'value': 2.0, 'rounds_to_target': None}); w.stage = 'rounds_to_target'; "
-            "w.arm(0.3); time.sleep(20)") % ROOT
+            "w = bench._Emitter({'value': 2.0, %r: None}); w.stage = %r; "
+            "w.arm(0.3); time.sleep(20)") % (ROOT, stage, stage)
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert p.returncode == 3
     rec = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][0]
-    assert "rounds_to_target" in rec["rounds_to_target"]["error"]
+    assert stage in rec[stage]["error"] and rec["value"] == 2.0
     assert "plane_companions" not in rec
