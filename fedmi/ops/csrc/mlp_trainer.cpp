@@ -15,6 +15,7 @@
 #include <pybind11/stl.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -523,6 +524,17 @@ static void logits_confusion_py(uintptr_t z, int ldz, uintptr_t y, int M, int C,
 
 void register_trainer(py::module_& m) {
     m.def("logits_confusion", &logits_confusion_py);
+    // the tile-split row pass's slice rule (host arithmetic, CPU-testable): dims = [F, h0, h1, C]
+    m.def("sk_pick_split", [](std::vector<int> dims, int T, int Bmax, int want, int cus) {
+        SkfArgs a;
+        std::memset(&a, 0, sizeof(a));
+        if (dims.size() < 2 || (int)dims.size() > SKF_MAXL + 1) throw std::runtime_error("sk_pick_split: bad dims");
+        a.L = (int)dims.size() - 1;
+        for (size_t i = 0; i < dims.size(); ++i) a.dims[i] = dims[i];
+        a.T = T;
+        a.Bmax = Bmax;
+        return skf_pick_split(a, want, cus);
+    });
     m.def("colsum_split", &colsum_split_py);
     m.def("skinny_wgrad", &skinny_wgrad_py);
     m.def("gemm_nt", &gemm_nt_py, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("B"),

@@ -223,3 +223,27 @@ def test_hip_float64_tile_split_is_bit_identical(data, hl, split, monkeypatch):
         np.testing.assert_allclose(a.loss_curve_, b.loss_curve_, rtol=1e-13)
         for u, v in zip(a.coefs_ + a.intercepts_, b.coefs_ + b.intercepts_):
             np.testing.assert_array_equal(u, v)
+
+
+def test_tile_split_rule():
+    """The tile-split row pass's slice count (mlp_fused_f64.hip skf_pick_split, host arithmetic):
+    at most min(forward tiles, input-gradient tiles, 8) slices, about one workgroup per CU over
+    all row blocks and trials, every slice owning a tile of both products; off for other depths
+    and wide heads; FEDMI_SK_SPLIT-style overrides."""
+    from fedmi.ops import native_available, native
+    if not native_available():
+        pytest.skip("native extension not built")
+    f = native().sk_pick_split
+    assert f([14, 50, 400, 1], 1, 200, 0, 256) == 4      # [S]: 4 input-gradient tiles
+    assert f([14, 50, 200, 1], 2, 200, 0, 256) == 4
+    assert f([14, 100, 400, 1], 2, 200, 0, 256) == 7
+    assert f([14, 400, 200, 1], 1, 200, 0, 256) == 7      # 8 would leave the last forward slice empty
+    assert f([14, 200, 100, 1], 1, 200, 0, 256) == 7
+    assert f([14, 400, 200, 1], 9, 200, 0, 256) == 2      # packed [H] job: 13 row blocks x 9 trials
+    assert f([14, 50, 400, 1], 9, 200, 0, 256) == 2
+    assert f([14, 50, 400, 1], 1, 200, 0, 32) == 2        # a device with fewer CUs: fewer slices
+    assert f([14, 50, 400, 1], 1, 200, 0, 0) == 1         # CU count unknown: no split
+    assert f([14, 50, 1], 1, 200, 0, 256) == 1            # one hidden layer
+    assert f([14, 50, 400, 5], 1, 200, 0, 256) == 1       # head wider than the narrow path
+    assert f([14, 50, 400, 1], 1, 200, 1, 256) == 1       # FEDMI_SK_SPLIT=1: off
+    assert f([14, 50, 400, 1], 9, 200, 3, 256) == 2       # asked for 3: the last slice would be empty
