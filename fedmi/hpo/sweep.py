@@ -61,6 +61,11 @@ def run_sweep(X_local, y_local, comm, hidden_grid: Sequence = HIDDEN_GRID, lr_gr
 
 def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial,
            dtype="float64"):
+    import os
+    import sys
+    import time
+    timing = os.environ.get("FEDMI_SWEEP_TIMING", "0") == "1"   # phase times on stderr
+    t_start = time.perf_counter()
     out = {}
     groups = [[MLPClassifier(hidden_layer_sizes=hl, learning_rate_init=lr, max_iter=max_iter,
                              random_state=random_state, backend=backend, dtype=dtype) for lr in lr_grid]
@@ -77,10 +82,23 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
         # was invalidated (ranks sharing a GPU made the overlap likely); the threads then only
         # replay graphs and poll, and the results are copied back here
         jobs = [prepare_packed(ests, X_local, y_local) for ests in groups]
+        t_prep = time.perf_counter()
+
+        def run_timed(j):
+            t0 = time.perf_counter()
+            j.run()
+            return time.perf_counter() - t0
+
         with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
-            list(ex.map(lambda j: j.run(), jobs))
+            job_s = list(ex.map(run_timed, jobs))
+        t_run = time.perf_counter()
         for j in jobs:
             j.finish()
+        if timing:
+            print(f"[sweep] prepare (build + capture) {t_prep - t_start:.3f} s, concurrent runs {t_run - t_prep:.3f} s, "
+                  f"finish {time.perf_counter() - t_run:.3f} s; per job: "
+                  + ", ".join(f"{tuple(g[0].hidden_layer_sizes)} {t:.3f} s" for g, t in zip(groups, job_s)),
+                  file=sys.stderr, flush=True)
     elif packed:
         for ests in groups:
             fit_packed(ests, X_local, y_local)
@@ -101,6 +119,9 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
             out[(tuple(hl), float(lr))] = res
             if on_trial is not None:
                 on_trial(res)
+    if timing:
+        print(f"[sweep] total {time.perf_counter() - t_start:.3f} s (metrics + FedAvg of every trial included)",
+              file=sys.stderr, flush=True)
     return out
 
 
