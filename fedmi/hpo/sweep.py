@@ -59,6 +59,29 @@ def run_sweep(X_local, y_local, comm, hidden_grid: Sequence = HIDDEN_GRID, lr_gr
     return best, results
 
 
+def _predict_device(ests: Sequence[MLPClassifier], X) -> List[np.ndarray]:
+    """``[e.predict(X) for e in ests]`` as float64 products on the GPU (the host's numpy forward
+    took 0.74 s of the 3.4 s reference sweep: 8000 x 200 x 400 products for 90 trials,
+    profiles/h_sweep_phases_r6.log).  The same formula as MLPClassifier.predict -- ReLU hidden
+    layers, logistic > 0.5 or softmax argmax -- so only a row whose output sits within rounding of
+    the decision boundary could come out differently (tests/test_sklearn_estimator.py pins the
+    sweep's metrics to the host forward)."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    x = torch.as_tensor(np.ascontiguousarray(X, dtype=np.float64), device=dev)
+    out = []
+    for e in ests:
+        a = x
+        L = len(e.coefs_)
+        for i, (W, b) in enumerate(zip(e.coefs_, e.intercepts_)):
+            a = torch.addmm(torch.as_tensor(b, device=dev), a, torch.as_tensor(W, device=dev))
+            if i < L - 1:
+                a = torch.relu(a)
+        idx = (torch.sigmoid(a.ravel()) > 0.5).long() if e.n_outputs_ == 1 else torch.argmax(a, dim=1)
+        out.append(e.classes_[idx.cpu().numpy()])
+    return out
+
+
 def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state, backend, packed, n_cls, on_trial,
            dtype="float64"):
     import os
@@ -106,9 +129,10 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
         for ests in groups:
             for e in ests:
                 e.fit(X_local, y_local)
+    on_device = packed and bool(groups) and groups[0][0]._resolve_backend() == "hip"
     for hl, ests in zip(hidden_grid, groups):
-        for lr, est in zip(lr_grid, ests):
-            y_pred = est.predict(X_local)
+        preds = _predict_device(ests, X_local) if on_device else [e.predict(X_local) for e in ests]
+        for lr, est, y_pred in zip(lr_grid, ests, preds):
             local = metrics_from_confusion(confusion_matrix(y_local, y_pred, n_cls))
             gw = average_estimator_weights(est, comm, weighting="uniform")
             k = len(est.coefs_)

@@ -247,3 +247,24 @@ def test_tile_split_rule():
     assert f([14, 50, 400, 5], 1, 200, 0, 256) == 1       # head wider than the narrow path
     assert f([14, 50, 400, 1], 1, 200, 1, 256) == 1       # FEDMI_SK_SPLIT=1: off
     assert f([14, 50, 400, 1], 9, 200, 3, 256) == 2       # asked for 3: the last slice would be empty
+
+
+@pytest.mark.gpu
+def test_hip_sweep_device_predictions_match_the_host_forward(data):
+    """The [H] sweep predicts every trial's local rows with float64 products on the GPU
+    (fedmi.hpo.sweep._predict_device); its local metrics equal the host forward's
+    (MLPClassifier.predict, numpy) on the same weights, trial by trial."""
+    from fedmi.fl.metrics import confusion_matrix, metrics_from_confusion
+    from fedmi.hpo.sweep import run_sweep
+    X, y = data
+    best, res = run_sweep(X, y, None, [(50,), (50, 200), (200, 400)], [0.004, 0.02, 0.2], max_iter=12,
+                          backend="hip")
+    assert len(res) == 9
+    for r in res:   # one client: the averaged weights are the local ones
+        e = MLPClassifier(hidden_layer_sizes=r.hidden, backend="numpy")
+        k = len(r.hidden) + 1
+        e.coefs_, e.intercepts_ = r.weights[:k], r.weights[k:]
+        e.classes_ = np.unique(y)
+        e.n_outputs_, e.out_activation_ = 1, "logistic"
+        cm = confusion_matrix(y, e.predict(X), 2)
+        assert metrics_from_confusion(cm) == r.local, (r.hidden, r.lr)
