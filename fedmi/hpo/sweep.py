@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from ..fl.metrics import confusion_matrix, metrics_from_confusion
-from ..fl.sklearn_fed import allreduce_confusion, average_estimator_weights
+from ..fl.sklearn_fed import allreduce_confusion, average_many_estimator_weights
 from ..models.sklearn_mlp import MLPClassifier, fit_packed, prepare_packed
 
 HIDDEN_GRID: Tuple[Tuple[int, ...], ...] = ((50,), (100,), (50, 50), (100, 50), (50, 100), (50, 200), (50, 400),
@@ -130,19 +130,24 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
             for e in ests:
                 e.fit(X_local, y_local)
     on_device = packed and bool(groups) and groups[0][0]._resolve_backend() == "hip"
+    trials, cms = [], []
     for hl, ests in zip(hidden_grid, groups):
         preds = _predict_device(ests, X_local) if on_device else [e.predict(X_local) for e in ests]
         for lr, est, y_pred in zip(lr_grid, ests, preds):
-            local = metrics_from_confusion(confusion_matrix(y_local, y_pred, n_cls))
-            gw = average_estimator_weights(est, comm, weighting="uniform")
-            k = len(est.coefs_)
-            est.coefs_, est.intercepts_ = gw[:k], gw[k:]
-            cm = allreduce_confusion(confusion_matrix(y_local, y_pred, n_cls), comm)
-            res = TrialResult(tuple(hl), float(lr), local, metrics_from_confusion(cm), int(est.n_iter_),
-                              [np.copy(w) for w in gw])
-            out[(tuple(hl), float(lr))] = res
-            if on_trial is not None:
-                on_trial(res)
+            trials.append((hl, lr, est))
+            cms.append(confusion_matrix(y_local, y_pred, n_cls))
+    # every trial's FedAvg (uniform mean of coefs_ + intercepts_, H:24-46) and pooled confusion in
+    # TWO all-reduces instead of two per trial -- the same per-element arithmetic
+    gws = average_many_estimator_weights([est for _, _, est in trials], comm)
+    pooled = allreduce_confusion(np.stack(cms), comm) if cms else []
+    for (hl, lr, est), cm_local, gw, cm in zip(trials, cms, gws, pooled):
+        k = len(est.coefs_)
+        est.coefs_, est.intercepts_ = gw[:k], gw[k:]
+        res = TrialResult(tuple(hl), float(lr), metrics_from_confusion(cm_local), metrics_from_confusion(cm),
+                          int(est.n_iter_), [np.copy(w) for w in gw])
+        out[(tuple(hl), float(lr))] = res
+        if on_trial is not None:
+            on_trial(res)
     if timing:
         print(f"[sweep] total {time.perf_counter() - t_start:.3f} s (metrics + FedAvg of every trial included)",
               file=sys.stderr, flush=True)

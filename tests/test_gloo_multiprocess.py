@@ -168,3 +168,53 @@ def test_comm_scaled_allreduce_over_gloo():
     for _, a, b in out:
         assert a == [0.25 * 1 + 0.5 * 2] * 7
         assert b == [0.5 * 1 + 0.5 * 2] * 5
+
+
+def _avg_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    torch.set_num_threads(1)
+    from fedmi.fl.sklearn_fed import average_estimator_weights, average_many_estimator_weights
+    from fedmi.models.sklearn_mlp import MLPClassifier
+    from fedmi.parallel.comm import Comm
+    comm = Comm(backend="gloo", device="cpu")
+    rng = np.random.RandomState(rank)
+    ests = []
+    for hl in [(3,), (4, 5), (6,)]:
+        e = MLPClassifier(hidden_layer_sizes=hl, backend="numpy")
+        dims = [2, *hl, 1]
+        e.coefs_ = [rng.randn(a, b) for a, b in zip(dims[:-1], dims[1:])]
+        e.intercepts_ = [rng.randn(b) for b in dims[1:]]
+        ests.append(e)
+    many = average_many_estimator_weights(ests, comm)
+    one = [average_estimator_weights(e, comm, weighting="uniform") for e in ests]
+    q.put((rank, many, one))
+    comm.close()
+
+
+def test_batched_estimator_averaging_matches_one_by_one():
+    """The [H] sweep averages all its trials in ONE all-reduce (average_many_estimator_weights):
+    the per-trial averages (average_estimator_weights) at world 3 over gloo -- to the last bits, as
+    gloo's own reduction order depends on the buffer's length; every rank holds the same result."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_avg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, many, one in res:
+        assert len(many) == len(one) == 3
+        for m_ws, o_ws in zip(many, one):
+            assert [w.shape for w in m_ws] == [w.shape for w in o_ws]
+            for a, b in zip(m_ws, o_ws):
+                np.testing.assert_allclose(a, b, rtol=1e-14, atol=1e-15)
+    for _, many, _ in res[1:]:          # every rank holds the same averages
+        for a_ws, b_ws in zip(many, res[0][1]):
+            for a, b in zip(a_ws, b_ws):
+                np.testing.assert_array_equal(a, b)
