@@ -551,15 +551,20 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
         const char* buf = smem + (kt & 1) * 65536;
         const int mh = (r == 1 || r == 2) ? 1 : 0;
         const int fo = (r >= 2) ? fo1 : fo0;
-        if (r == 0) {
-            if (!tail || kt + 1 < KT) { dmaB(kt + 1, 2); dmaB(kt + 1, 3); }
-        } else if (r == 1) {
-            if (!tail || kt + 1 < KT) { dmaA(kt + 1, 0, 0); dmaA(kt + 1, 0, 1); }
-        } else if (r == 2) {
-            if (!tail || kt + 1 < KT) { dmaA(kt + 1, 1, 0); dmaA(kt + 1, 1, 1); }
-        } else {
-            if (!tail || kt + 2 < KT) { dmaB(kt + 2, 0); dmaB(kt + 2, 1); }
-        }
+        auto issue = [&]() {
+            if (r == 0) {
+                if (!tail || kt + 1 < KT) { dmaB(kt + 1, 2); dmaB(kt + 1, 3); }
+            } else if (r == 1) {
+                if (!tail || kt + 1 < KT) { dmaA(kt + 1, 0, 0); dmaA(kt + 1, 0, 1); }
+            } else if (r == 2) {
+                if (!tail || kt + 1 < KT) { dmaA(kt + 1, 1, 0); dmaA(kt + 1, 1, 1); }
+            } else {
+                if (!tail || kt + 2 < KT) { dmaB(kt + 2, 0); dmaB(kt + 2, 1); }
+            }
+        };
+#ifdef NT_DMA_FIRST
+        issue();   // (A/B: the round-5 order, DMA issue ahead of the phase's fragment reads)
+#endif
         if (r == 0) {
 #pragma unroll
             for (int y = 0; y < 4; ++y) bfr[y] = *reinterpret_cast<const bf16x8*>(buf + boff + y * 16 * 128 + fo0);
@@ -570,6 +575,9 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
 #pragma unroll
         for (int x = 0; x < 4; ++x)
             af[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + (mh * 64 + x * 16) * 128 + fo);
+#ifndef NT_DMA_FIRST
+        issue();   // after the fragment reads: 0.5-1 % faster at the wide shapes (profiles/nt_gm_r6.log)
+#endif
         // the last two K-tiles issue fewer pieces: exact counts there too (a vmcnt(0) right after
         // an issue would expose a whole DMA latency per phase)
         if (!tail || kt + 2 < KT) {
