@@ -463,6 +463,9 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
 // read.  Waits (before a phase's first barrier, retiring what the NEXT phase reads; pieces still
 // allowed in flight, in issue order): r = 0: 4 (B01, B23 of u+1) | r = 3: 4 (A m1 of u+1, B01 of
 // u+2) | r = 1, 2: none.
+#ifndef NT_PRIO
+#define NT_PRIO 1   // issue priority of a phase's MFMA cluster (A/B builds)
+#endif
 template <int F, bool BUF = false>
 __global__ void __launch_bounds__(NT2_THREADS)
 gemm_nt_bf16_fl_kernel(NTArgs g) {
@@ -590,7 +593,7 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_setprio(1);
+        if (NT_PRIO > 0) __builtin_amdgcn_s_setprio(NT_PRIO);
         if (r <= 1) {
 #pragma unroll
             for (int x = 0; x < 4; ++x)
@@ -604,7 +607,7 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
                 for (int y = 0; y < 4; ++y)
                     acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr1[y], acc[mh * 4 + x][y], 0, 0, 0);
         }
-        __builtin_amdgcn_s_setprio(0);
+        if (NT_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
     };
 
