@@ -547,7 +547,9 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
         vm_wait<0>();
     }
     __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();
+#ifndef NT_NO_STAGGER
+    if (wr == 1) __builtin_amdgcn_s_barrier();   // the second wave row runs one barrier behind
+#endif
     NT_STAMP(1);
 
     auto phase = [&](int kt, int r, bool tail) {
@@ -625,7 +627,9 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
         phase(kt, 2, true);
         phase(kt, 3, true);
     }
+#ifndef NT_NO_STAGGER
     if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second wave row's extra barrier
+#endif
     NT_STAMP(3);
     pp_epilogue<F>(g, smem, acc, m0, n0, w, l);
     NT_STAMP(4);  // output stores issued (not waited for)
