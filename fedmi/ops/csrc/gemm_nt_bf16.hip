@@ -463,6 +463,9 @@ gemm_nt_bf16_pp_kernel(NTArgs g) {
 // read.  Waits (before a phase's first barrier, retiring what the NEXT phase reads; pieces still
 // allowed in flight, in issue order): r = 0: 4 (B01, B23 of u+1) | r = 3: 4 (A m1 of u+1, B01 of
 // u+2) | r = 1, 2: none.
+#ifndef NT_MFMA_YX
+#define NT_MFMA_YX 0
+#endif
 #ifndef NT_PRIO
 #define NT_PRIO 1   // issue priority of a phase's MFMA cluster (A/B builds)
 #endif
@@ -596,18 +599,19 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (NT_PRIO > 0) __builtin_amdgcn_s_setprio(NT_PRIO);
+        // (NT_MFMA_YX: B-fragment-major issue order, A/B; independent accumulators either way)
         if (r <= 1) {
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y)
-                    acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr[y], acc[mh * 4 + x][y], 0, 0, 0);
+            for (int i = 0; i < 16; ++i) {
+                const int x = NT_MFMA_YX ? (i & 3) : (i >> 2), y = NT_MFMA_YX ? (i >> 2) : (i & 3);
+                acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr[y], acc[mh * 4 + x][y], 0, 0, 0);
+            }
         } else {
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y)
-                    acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr1[y], acc[mh * 4 + x][y], 0, 0, 0);
+            for (int i = 0; i < 16; ++i) {
+                const int x = NT_MFMA_YX ? (i & 3) : (i >> 2), y = NT_MFMA_YX ? (i >> 2) : (i & 3);
+                acc[mh * 4 + x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[x], bfr1[y], acc[mh * 4 + x][y], 0, 0, 0);
+            }
         }
         if (NT_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
