@@ -42,10 +42,23 @@ def main():
     modes = (True,) if "--fused-only" in sys.argv else (True, False)
     if "--stamps" in sys.argv:
         os.environ["FEDMI_SK_STAMPS"] = "1"
+    for i, arg in enumerate(sys.argv):
+        if arg == "--epochs":   # override every case's epoch count
+            cases = [(hl, T, int(sys.argv[i + 1])) for hl, T, _ in cases]
+    # --marginal: also fit 2x the epochs and report the marginal cost per step, (wall(2e) - wall(e)) /
+    # (steps(2e) - steps(e)) -- free of the fit's set-up (trainer build, graph capture, copies), which
+    # dominates short packed fits (10 epochs of 32 steps)
+    marginal = "--marginal" in sys.argv
     for hl, T, ep in cases:
         run(hl, T, 2, True, X, y)   # warm-up (build, first graph)
         for fused in modes:
-            print(json.dumps(run(hl, T, ep, fused, X, y)), flush=True)
+            r = run(hl, T, ep, fused, X, y)
+            if marginal:
+                r2 = run(hl, T, 2 * ep, fused, X, y)
+                s1 = r["wall_s"] / r["us_per_step"] * 1e6
+                s2 = r2["wall_s"] / r2["us_per_step"] * 1e6
+                r["marginal_us_per_step"] = (r2["wall_s"] - r["wall_s"]) / max(s2 - s1, 1) * 1e6
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
