@@ -555,10 +555,29 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
     for (int e = threadIdx.x; e < C * N1; e += blockDim.x) wh[e] = Wh[e];
     if (threadIdx.x < C) wh[C * N1 + threadIdx.x] = P[a.b_off[2] + threadIdx.x];
     const double* ag = a.acts + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw;
+#ifdef SKF_HLOAD_FLAT   // (A/B: the round-6 first version)
     for (int e = threadIdx.x; e < SKF_RB * np2; e += blockDim.x) {
         const int r = e / np2, j = e - r * np2;
         h[r * ld2 + j] = (r < nr && j < N1) ? ag[(size_t)r * a.maxw + j] : 0.0;
     }
+#else
+    {   // wave w = row w, 4 loads in flight per lane before the first LDS store (-1 us per [S] step,
+        // profiles/sk_step_marginal_r6.log)
+        const double* agr = ag + (size_t)wave * a.maxw;
+        double* hr = h + wave * ld2;
+        for (int k0 = lane; k0 < np2; k0 += 256) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + 64 * u;
+                v[u] = *((wave < nr && k < N1) ? agr + k : a.zero);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k0 + 64 * u < np2) hr[k0 + 64 * u] = v[u];
+        }
+    }
+#endif
     const double* a0g = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;
     const int npk = skf_np(nk);
     for (int e = threadIdx.x; e < SKF_RB * npk; e += blockDim.x) {
@@ -619,6 +638,7 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
         }
     }
     // layer 1's delta, every column (skf_bwd_narrow's sums, ReLU mask), in place
+#ifdef SKF_DELTA_FLAT   // (A/B: the round-6 first version)
     for (int e = threadIdx.x; e < SKF_RB * np2; e += blockDim.x) {
         const int r = e / np2, k = e - r * np2;
         double sum = 0.0;
@@ -626,6 +646,25 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
         double* p = h + r * ld2 + k;
         *p = (k < N1 && *p > 0.0) ? sum : 0.0;
     }
+#else
+    {   // wave w = row w, lanes over the columns (no index division), the same sums (-1.6 us per [S]
+        // step, profiles/sk_step_marginal_r6.log)
+        static_assert(SKF_RB == SKF_WAVES, "one row per wave");
+        const int r = wave;
+        double dzr[SKF_NARROW];
+#pragma unroll
+        for (int n = 0; n < SKF_NARROW; ++n) dzr[n] = n < C ? dz_s[r * C + n] : 0.0;
+        double* hr = h + r * ld2;
+        for (int k = lane; k < np2; k += 64) {
+            double sum = 0.0;
+#pragma unroll
+            for (int n = 0; n < SKF_NARROW; ++n)
+                if (n < C) sum += dzr[n] * (k < N1 ? wh[n * N1 + k] : 0.0);
+            const double m = hr[k];
+            hr[k] = (k < N1 && m > 0.0) ? sum : 0.0;
+        }
+    }
+#endif
     skf_lds_barrier();
     SKF_STAMP(8);
     if (sl == 0) {  // layer 1's delta: the wgrad operand of layer 1
