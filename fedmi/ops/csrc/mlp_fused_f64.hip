@@ -667,12 +667,9 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
 #endif
     skf_lds_barrier();
     SKF_STAMP(8);
-    if (sl == 0) {  // layer 1's delta: the wgrad operand of layer 1
-        double* dg = a.deltas + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw;
-        for (int e = threadIdx.x; e < nr * N1; e += blockDim.x) {
-            const int r = e / N1, c = e - r * N1;
-            skf_st(&dg[(size_t)r * a.maxw + c], h[r * ld2 + c], a.wthru);
-        }
+    if (sl == 0 && wave < nr) {  // layer 1's delta: the wgrad operand of layer 1 (a row per wave)
+        double* dg = a.deltas + (((size_t)a.T + t) * a.Bmax + r0 + wave) * a.maxw;
+        for (int c = lane; c < N1; c += 64) skf_st(&dg[c], h[wave * ld2 + c], a.wthru);
     }
     // the slice's tiles of layer 1's input gradient, masked in place over layer 0's activations:
     // skf_rowpass's chunk length and k-groups for the whole product (each tile a complete sum)
@@ -681,10 +678,9 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
                      nullptr, K1, false, gb.G, (N1 + 3) >> 2);
     skf_lds_barrier();
     SKF_STAMP(9);
-    double* dg = a.deltas + ((size_t)t * a.Bmax + r0) * a.maxw + k0;
-    for (int e = threadIdx.x; e < nr * nk; e += blockDim.x) {
-        const int r = e / nk, j = e - r * nk;
-        skf_st(&dg[(size_t)r * a.maxw + j], a0s[r * ldk + j], a.wthru);
+    if (wave < nr) {   // (a row per wave)
+        double* dg = a.deltas + ((size_t)t * a.Bmax + r0 + wave) * a.maxw + k0;
+        for (int j = lane; j < nk; j += 64) skf_st(&dg[j], a0s[wave * ldk + j], a.wthru);
     }
     if (a.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SKF_STAMP(10);
