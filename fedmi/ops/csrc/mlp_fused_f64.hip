@@ -510,12 +510,9 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
                     a.wt != nullptr ? a.wt + (size_t)t * a.P + a.w_off[0] : nullptr);
     skf_lds_barrier();
     SKF_STAMP(2);
-    if (sl == 0) {
-        double* ag = a.acts + ((size_t)t * a.Bmax + r0) * a.maxw;
-        for (int e = threadIdx.x; e < nr * K1; e += blockDim.x) {
-            const int r = e / K1, c = e - r * K1;
-            skf_st(&ag[(size_t)r * a.maxw + c], b1[r * ldof(1) + c], a.wthru);
-        }
+    if (sl == 0 && wave < nr) {   // (a row per wave)
+        double* ag = a.acts + ((size_t)t * a.Bmax + r0 + wave) * a.maxw;
+        for (int c = lane; c < K1; c += 64) skf_st(&ag[c], b1[wave * ldof(1) + c], a.wthru);
     }
     // the slice's output tiles of hidden layer 1's forward, with skf_rowpass's chunking and k-groups
     const SkfGroups gf = skf_groups((K1 + 3) >> 2, (N1 + 15) >> 4);
@@ -524,10 +521,9 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_fwd_kernel(SkfArgs a) {
                     nullptr, N1, false, gf.G, (K1 + 3) >> 2);
     skf_lds_barrier();
     SKF_STAMP(3);
-    double* ag = a.acts + (((size_t)a.T + t) * a.Bmax + r0) * a.maxw + c0;
-    for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
-        const int r = e / nc, j = e - r * nc;
-        skf_st(&ag[(size_t)r * a.maxw + j], b2[r * ldof(2) + c0 + j], a.wthru);
+    if (wave < nr) {   // (a row per wave)
+        double* ag = a.acts + (((size_t)a.T + t) * a.Bmax + r0 + wave) * a.maxw + c0;
+        for (int j = lane; j < nc; j += 64) skf_st(&ag[j], b2[wave * ldof(2) + c0 + j], a.wthru);
     }
     if (a.dbg != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SKF_STAMP(4);
