@@ -21,7 +21,7 @@ import numpy as np
 
 from ..fl.metrics import confusion_matrix, metrics_from_confusion
 from ..fl.sklearn_fed import allreduce_confusion, average_many_estimator_weights
-from ..models.sklearn_mlp import MLPClassifier, fit_packed, prepare_packed
+from ..models.sklearn_mlp import MLPClassifier, fit_packed, packed_inputs, prepare_packed
 
 HIDDEN_GRID: Tuple[Tuple[int, ...], ...] = ((50,), (100,), (50, 50), (100, 50), (50, 100), (50, 200), (50, 400),
                                             (100, 400), (400, 200), (200, 400))
@@ -104,7 +104,13 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
         # thread starts: a capture overlapping another thread's allocations / copies / polling
         # was invalidated (ranks sharing a GPU made the overlap likely); the threads then only
         # replay graphs and poll, and the results are copied back here
-        jobs = [prepare_packed(ests, X_local, y_local) for ests in groups]
+        # the host halves (estimator init + epoch orders, GIL-free in the native generator) of every
+        # job concurrently; then the device halves one after another
+        # (only with integer random_states: a shared RandomState must not be drawn from two threads)
+        own_rng = all(isinstance(g[0].random_state, (int, np.integer)) for g in groups)
+        with ThreadPoolExecutor(max_workers=min(8, len(groups)) if own_rng else 1) as ex:
+            inputs = list(ex.map(lambda g: packed_inputs(g, X_local, y_local), groups))
+        jobs = [prepare_packed(ests, X_local, y_local, inputs=inp) for ests, inp in zip(groups, inputs)]
         t_prep = time.perf_counter()
 
         def run_timed(j):

@@ -43,7 +43,20 @@ def _glorot(rs: np.random.RandomState, dims: Sequence[int]):
 
 
 def epoch_permutations(rs: np.random.RandomState, n: int, epochs: int) -> np.ndarray:
-    """sklearn's per-epoch ``sample_idx = shuffle(sample_idx, random_state=rs)`` sequence."""
+    """sklearn's per-epoch ``sample_idx = shuffle(sample_idx, random_state=rs)`` sequence.  With the
+    native extension the same MT19937 draws run in C++ without the GIL (sk_perms.cpp: numpy's
+    generator, state in / state out, bit for bit), so packed jobs prepare their orders concurrently."""
+    st = rs.get_state() if isinstance(rs, np.random.RandomState) else None
+    if st is not None and st[0] == "MT19937" and epochs > 0 and n > 0:
+        try:
+            from ..ops import native, native_available
+            m = native() if native_available() else None
+        except Exception:  # noqa: BLE001 -- the numpy loop below is the reference
+            m = None
+        if m is not None and hasattr(m, "sk_epoch_perms"):
+            perms, key, pos = m.sk_epoch_perms(st[1], int(st[2]), int(n), int(epochs))
+            rs.set_state((st[0], key, pos, st[3], st[4]))
+            return perms
     out = np.empty((epochs, n), dtype=np.int32)
     idx = np.arange(n)
     for e in range(epochs):
@@ -436,7 +449,7 @@ def fit_packed(ests: List[MLPClassifier], X, y):
     return ests
 
 
-def prepare_packed(ests: List[MLPClassifier], X, y) -> Optional["_HipJob"]:
+def prepare_packed(ests: List[MLPClassifier], X, y, inputs=None) -> Optional["_HipJob"]:
     """:func:`fit_packed` up to a built, graph-captured device job (None: a host backend, which
     has fitted the estimators already).  ``job.run()`` may then run beside other jobs from other
     host threads; ``job.finish()`` writes the results back."""
@@ -450,7 +463,19 @@ def prepare_packed(ests: List[MLPClassifier], X, y) -> Optional["_HipJob"]:
         for e in ests:
             e.fit(X, y)
         return None
-    rs = None
+    inputs = packed_inputs(ests, X, y) if inputs is None else inputs
+    codes, perms = inputs
+    return _fit_hip_prepare(ests, X, codes, e0._dims(X.shape[1]), perms, incremental=False)
+
+
+def packed_inputs(ests: List[MLPClassifier], X, y):
+    """The host half of :func:`prepare_packed`: every estimator's init (Glorot weights from its
+    random_state) and the epochs' sample orders -- no HIP call, so several jobs may prepare theirs
+    from several threads (the native order generator releases the GIL) before their device jobs are
+    built and captured one after another."""
+    X = np.asarray(X, dtype=np.float64)
+    e0 = ests[0]
+    rs, codes = None, None
     for e in ests:
         codes = e._encode(y, True)
         rs = e._rs()
@@ -461,4 +486,4 @@ def prepare_packed(ests: List[MLPClassifier], X, y) -> Optional["_HipJob"]:
         e._adam = None
     perms = epoch_permutations(rs, X.shape[0], e0.max_iter) if e0.shuffle else \
         np.tile(np.arange(X.shape[0], dtype=np.int32), (e0.max_iter, 1))
-    return _fit_hip_prepare(ests, X, codes, e0._dims(X.shape[1]), perms, incremental=False)
+    return codes, perms

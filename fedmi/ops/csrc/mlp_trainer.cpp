@@ -12,6 +12,7 @@
 // permutation is selected by a device counter), so the host issues one launch per epoch.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include <cstdlib>
@@ -22,6 +23,8 @@
 #include <vector>
 
 #include "gemm_mfma.h"
+
+void sk_epoch_perms(uint32_t* key, int* pos, int n, int epochs, int32_t* perms);  // sk_perms.cpp
 #include "gemm_nt_bf16.h"
 #include "mlp_f64.h"
 #include "mlp_ops.h"
@@ -524,6 +527,22 @@ static void logits_confusion_py(uintptr_t z, int ldz, uintptr_t y, int M, int C,
 
 void register_trainer(py::module_& m) {
     m.def("logits_confusion", &logits_confusion_py);
+    // sklearn's per-epoch shuffles (sk_perms.cpp): (key uint32[624], pos, n, epochs) -> (perms int32
+    // [epochs][n], key, pos) -- numpy's MT19937 stream, state in / state out
+    m.def("sk_epoch_perms", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> key, int pos, int n,
+                               int epochs) {
+        if (key.size() != 624 || n < 1 || epochs < 0 || pos < 0 || pos > 624)
+            throw std::runtime_error("sk_epoch_perms: bad MT19937 state or sizes");
+        std::vector<uint32_t> k(key.data(), key.data() + 624);
+        py::array_t<int32_t> perms({(py::ssize_t)epochs, (py::ssize_t)n});
+        {
+            py::gil_scoped_release nogil;
+            sk_epoch_perms(k.data(), &pos, n, epochs, perms.mutable_data());
+        }
+        py::array_t<uint32_t> kout(624);
+        std::copy(k.begin(), k.end(), kout.mutable_data());
+        return py::make_tuple(perms, kout, pos);
+    });
     // the tile-split row pass's slice rule (host arithmetic, CPU-testable): dims = [F, h0, h1, C]
     m.def("sk_pick_split", [](std::vector<int> dims, int T, int Bmax, int want, int cus) {
         SkfArgs a;

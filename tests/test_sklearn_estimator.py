@@ -268,3 +268,26 @@ def test_hip_sweep_device_predictions_match_the_host_forward(data):
         e.n_outputs_, e.out_activation_ = 1, "logistic"
         cm = confusion_matrix(y, e.predict(X), 2)
         assert metrics_from_confusion(cm) == r.local, (r.hidden, r.lr)
+
+
+@pytest.mark.parametrize("seed,n,epochs,skip", [(42, 8000, 40, 137), (0, 1000, 25, 0), (7, 3, 5, 11)])
+def test_native_epoch_orders_are_numpys(seed, n, epochs, skip):
+    """The native epoch-order generator (sk_perms.cpp) draws numpy's MT19937 stream bit for bit: the
+    same orders as the numpy loop, and the RandomState left in the same state."""
+    from fedmi.ops import native_available, native
+    if not native_available():
+        pytest.skip("native extension not built")
+    rs1, rs2 = np.random.RandomState(seed), np.random.RandomState(seed)
+    rs1.rand(skip), rs2.rand(skip)                    # e.g. the Glorot init's draws before the orders
+    want = np.empty((epochs, n), dtype=np.int32)       # the reference loop (sklearn's shuffle per epoch)
+    idx = np.arange(n)
+    for e in range(epochs):
+        ind = np.arange(n)
+        rs1.shuffle(ind)
+        idx = idx[ind]
+        want[e] = idx
+    got = epoch_permutations(rs2, n, epochs)
+    np.testing.assert_array_equal(got, want)
+    s1, s2 = rs1.get_state(), rs2.get_state()
+    np.testing.assert_array_equal(s1[1], s2[1])
+    assert s1[2] == s2[2] and rs1.rand() == rs2.rand()
