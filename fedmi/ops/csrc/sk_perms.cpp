@@ -8,6 +8,7 @@
 // (profiles/h_sweep_phases_r6.log: most of the [H] sweep's job preparation).  This is the same
 // generator (numpy's mt19937.c and random_interval, state in / state out), so the orders and the
 // RandomState's state afterwards are numpy's bit for bit (tests/test_sklearn_estimator.py).
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -78,7 +79,7 @@ void sk_epoch_perms(uint32_t* key, int* pos, int n, int epochs, int32_t* perms) 
         }
         for (int i = 0; i < n; ++i) nxt[i] = idx[ind[i]];
         idx.swap(nxt);
-        for (int i = 0; i < n; ++i) perms[(size_t)e * n + i] = idx[i];
+        for (int i = 0; i < n; ++i) perms[(std::size_t)e * n + i] = idx[i];
     }
     for (int i = 0; i < MT_N; ++i) key[i] = mt.key[i];
     *pos = mt.pos;
