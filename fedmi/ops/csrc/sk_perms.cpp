@@ -17,6 +17,7 @@ constexpr int MT_N = 624, MT_M = 397;
 
 struct Mt19937 {
     uint32_t key[MT_N];
+    uint32_t out[MT_N];   // the tempered outputs of the current block (filled by gen(): one vectorisable pass)
     int pos;
 
     void gen() {
@@ -34,29 +35,21 @@ struct Mt19937 {
         y = (key[MT_N - 1] & UPPER) | (key[0] & LOWER);
         key[MT_N - 1] = key[MT_M - 1] ^ (y >> 1) ^ (-(y & 1u) & A);
         pos = 0;
+        temper_all();
+    }
+    void temper_all() {
+        for (int i = 0; i < MT_N; ++i) {
+            uint32_t y = key[i];
+            y ^= (y >> 11);
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= (y >> 18);
+            out[i] = y;
+        }
     }
     uint32_t next32() {
         if (pos == MT_N) gen();
-        uint32_t y = key[pos++];
-        y ^= (y >> 11);
-        y ^= (y << 7) & 0x9d2c5680u;
-        y ^= (y << 15) & 0xefc60000u;
-        y ^= (y >> 18);
-        return y;
-    }
-    // numpy random_interval for max < 2^32: masked rejection sampling
-    uint32_t interval(uint32_t max) {
-        if (max == 0) return 0;
-        uint32_t mask = max;
-        mask |= mask >> 1;
-        mask |= mask >> 2;
-        mask |= mask >> 4;
-        mask |= mask >> 8;
-        mask |= mask >> 16;
-        uint32_t v;
-        while ((v = (next32() & mask)) > max) {
-        }
-        return v;
+        return out[pos++];
     }
 };
 }  // namespace
@@ -67,12 +60,24 @@ void sk_epoch_perms(uint32_t* key, int* pos, int n, int epochs, int32_t* perms) 
     Mt19937 mt;
     for (int i = 0; i < MT_N; ++i) mt.key[i] = key[i];
     mt.pos = *pos;
+    mt.temper_all();   // (the block numpy is in the middle of: positions pos.. are still to be drawn)
     std::vector<int32_t> idx(n), ind(n), nxt(n);
     for (int i = 0; i < n; ++i) idx[i] = i;
     for (int e = 0; e < epochs; ++e) {
         for (int i = 0; i < n; ++i) ind[i] = i;
+        // random_interval(i)'s mask (the smallest 2^k - 1 >= i) only shrinks as i falls: kept, not
+        // recomputed per draw (the same values: masked rejection sampling either way)
+        uint32_t mask = (uint32_t)(n - 1);
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        mask |= mask >> 8;
+        mask |= mask >> 16;
         for (int i = n - 1; i >= 1; --i) {
-            const uint32_t j = mt.interval((uint32_t)i);
+            if ((uint32_t)i <= (mask >> 1)) mask >>= 1;
+            uint32_t j;
+            while ((j = (mt.next32() & mask)) > (uint32_t)i) {
+            }
             const int32_t t = ind[i];
             ind[i] = ind[j];
             ind[j] = t;
