@@ -477,7 +477,16 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
     if (g.dbg != nullptr && threadIdx.x == 0) g.dbg[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
     NT_STAMP(0);
     const int mt = g.M / NT2_BM, nt = g.N / NT2_BM;
-    const int bid = xcd_remap_nt(blockIdx.x, mt * nt);
+#ifdef NT_PERSIST
+    // (A/B) one resident block per CU walks tiles blockIdx.x, + gridDim.x, ...: the next tile's
+    // prologue DMAs start while the previous tile's output stores drain (gridDim.x % 8 == 0, so a
+    // virtual block keeps the XCD of the block that runs it and the remap below is unchanged)
+    for (int vb = blockIdx.x; vb < mt * nt; vb += gridDim.x) {
+#else
+    {
+        const int vb = blockIdx.x;
+#endif
+    const int bid = xcd_remap_nt(vb, mt * nt);
 #ifndef NT_GM
 #define NT_GM 4
 #endif
@@ -637,6 +646,10 @@ gemm_nt_bf16_fl_kernel(NTArgs g) {
     NT_STAMP(3);
     pp_epilogue<F>(g, smem, acc, m0, n0, w, l);
     NT_STAMP(4);  // output stores issued (not waited for)
+#ifdef NT_PERSIST
+    __syncthreads();   // the epilogue's LDS reads are done before the next tile's DMAs land
+#endif
+    }
 #undef NT_STAMP
 }
 
@@ -668,7 +681,18 @@ hipError_t gemm_nt_bf16_launch(const NTArgs& g_in, hipStream_t s) {
         (g.CbT == nullptr || (g.ldct % 4 == 0 && (reinterpret_cast<uintptr_t>(g.CbT) & 7) == 0)) &&
         (g.mask == nullptr || (g.ldmask % 8 == 0 && (reinterpret_cast<uintptr_t>(g.mask) & 15) == 0)) &&
         (g.Cbf16 == nullptr || (g.ldcb % 8 == 0 && (reinterpret_cast<uintptr_t>(g.Cbf16) & 15) == 0))) {
-        const int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
+        int blocks = (g.M / NT2_BM) * (g.N / NT2_BM);
+#ifdef NT_PERSIST
+        static int cus = 0;
+        if (cus == 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8)
+                cus = 256;
+            cus &= ~7;   // a multiple of 8: the kernel's XCD remap of virtual blocks needs it
+        }
+        if (blocks > cus) blocks = cus;
+#endif
         // The buffer-resource DMAs address a block's operand rows with 32-bit offsets from the
         // block's first row (num_records 0x7fffffff): an out-of-range offset would read zeros
         // silently, so operands whose per-block span (a 256-row tile of A or B, + K) reaches 2^31
