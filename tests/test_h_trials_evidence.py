@@ -37,3 +37,10 @@ def test_k1_trials_within_sklearns_own_spread():
     worst = max(abs(a[k][0] - b[k][0]) for k in a)
     self_worst = max(abs(b2[k][0] - b[k][0]) for k in a)
     assert worst <= self_worst + 0.005
+
+
+@pytest.mark.parametrize("k,best", [(2, ((100, 400), 0.004)), (4, ((100, 400), 0.002))])
+def test_k2_k4_trials_equal_sklearn_but_one(k, best):
+    a, b = _pair(f"h_trials_hip_k{k}_r6.json", f"h_trials_sklearn_k{k}_1thr.json")
+    assert sum(a[k_][0] == b[k_][0] for k_ in a) >= 89
+    assert max(a, key=lambda k_: a[k_][0]) == best == max(b, key=lambda k_: b[k_][0])
