@@ -118,7 +118,10 @@ def _train(X_local, y_local, comm, hidden_grid, lr_grid, max_iter, random_state,
             j.run()
             return time.perf_counter() - t0
 
-        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+        # FEDMI_SWEEP_RUN_THREADS=1 replays the jobs one after another (profiling: rocprofv3's kernel trace
+        # crashed inside hipGraphLaunch with ten threads replaying graphs, profiles/h_sweep_kernels_r6.txt)
+        n_run = int(os.environ.get("FEDMI_SWEEP_RUN_THREADS", "0") or 0) or len(jobs)
+        with ThreadPoolExecutor(max_workers=min(n_run, len(jobs))) as ex:
             job_s = list(ex.map(run_timed, jobs))
         t_run = time.perf_counter()
         for j in jobs:
