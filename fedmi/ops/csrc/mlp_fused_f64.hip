@@ -687,12 +687,28 @@ __global__ void __launch_bounds__(SKF_WAVES * 64) skf_cs_bwd_kernel(SkfArgs a) {
 __global__ void __launch_bounds__(256) skf_wgrad_adam_kernel(SkfArgs a) {
     __shared__ double part[4][64][4];
     __shared__ double sq_s;
+#ifdef SKF_WG_XCD
+    // (A/B) XCD-grouped tiles: the dispatcher deals linear workgroup ids round-robin over the 8
+    // XCDs; remap so each XCD gets a contiguous trial-major range (one trial's tiles share their
+    // activation / delta columns in that XCD's L2).  Only the workgroup -> tile map changes.
+    // Not the default: -2.5 % per step with every trial active, +7 % on the [H] sweep, where converged
+    // trials' workgroups exit at once and leave their XCDs idle (profiles/sk_wgrad_xcd_r6_rejected.log).
+    const int gx = gridDim.x, nwg = gx * gridDim.y, hw = blockIdx.x + blockIdx.y * gx;
+    const int q = nwg / 8, r = nwg % 8, xcd = hw % 8;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + hw / 8;
+    const int t = lin / gx;
+#else
     const int t = blockIdx.y;
+#endif
     if (a.active[t] == 0) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     // which layer / tile
+#ifdef SKF_WG_XCD
+    int id = lin % gx, l = 0;
+#else
     int id = blockIdx.x, l = 0;
+#endif
     for (; l < a.L - 1; ++l) {
         const int n_t = ((a.dims[l + 1] + 15) >> 4) * ((a.dims[l] + 1 + 15) >> 4);
         if (id < n_t) break;
